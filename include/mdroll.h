@@ -1,0 +1,142 @@
+/*
+ * mdroll.h — C ABI of libmdroll.so, the MI355X (gfx950) MultiDismantler inference-rollout engine.
+ *
+ * The reference (KelvinRyman/MDCommunity, Python) runs the rollout as
+ *   GetSol / GetSolution          U/MultiDismantler_torch.py:759-784 / :711-736
+ *     -> PredictWithCurrentQNet   :304-306 -> Predict :263-302 -> test_forward
+ *                                 (U/MultiDismantler_net_graphsage.py:243-394)
+ *     -> np.argsort(-q)[:step]    :769 / :725
+ *     -> MvcEnv.stepWithoutReward U/mvc_env.py:74-87 -> getReward -> Mcc.MCC (U/Mcc.py:30-38)
+ * Each entry point below replaces one of those interfaces; the Python package
+ * `mdcommunity_amd` binds them with ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions: plain pointers and explicit sizes only; the caller owns every host buffer,
+ * the library owns every device allocation of a context; weights and graphs are copied in.
+ * Every function returns an md_status and never aborts across the ABI; md_last_error()
+ * gives the detail string of the last failure on that context.
+ * Threading: one context per (process, device); calls on one context must be serialised
+ * by the caller (the reference is single-threaded Python).  Contexts on different devices
+ * may be used concurrently (one process per GPU for the sharded configuration).
+ */
+#ifndef MDROLL_H
+#define MDROLL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  MD_OK = 0,
+  MD_EINVAL = 1,   /* bad argument (shape, id range, self-loop, ...)             */
+  MD_EHIP = 2,     /* HIP runtime error (launch, copy, device fault)              */
+  MD_EOOM = 3,     /* device allocation failed                                    */
+  MD_ESTATE = 4,   /* call not valid in the current state (e.g. no graphs loaded) */
+  MD_ETIMEOUT = 5, /* a device-side team barrier timed out (kernel drained)       */
+  MD_ECALLBACK = 6 /* the host tie-selection callback reported an error           */
+} md_status;
+
+/* Cost model: unit cost (U/) or degree cost (D/, D/mvc_env.py:127-134). */
+enum { MD_COST_UNIT = 0, MD_COST_DEGREE = 1 };
+
+/* Number of fp32 values in a packed weight blob (A.3 of SURVEY.md; state_dict of
+ * U/MultiDismantler_net_graphsage.py:42-89 + U/MRGNN/mutil_layer_weight.py:252-262),
+ * packed in this order, each row-major as in the state_dict:
+ *   w_n2l[2][64], p_node_conv[64][64], p_node_conv2[64][64], p_node_conv3[128][64],
+ *   h1_weight[64][32], h2_weight(=last_w)[36], cross_product[64], w_layer1[64][128],
+ *   w_layer2[128], trans[64][64], bias[64], logis.weight[64], logis.bias[1]          */
+#define MD_WEIGHT_FLOATS 31205
+
+typedef struct md_ctx md_ctx;
+
+/* Host tie-resolution callback.  The device picks the arg-max itself whenever the
+ * maximum Q is unique.  When k > 1 live nodes tie exactly at the maximum, the reference's
+ * choice is `np.argsort(-q)[:step]` (U/MultiDismantler_torch.py:769), i.e. numpy's
+ * unstable sort order, so the library hands the masked Q row (float64, masked entries =
+ * -1073741823.5 as U/MultiDismantler_torch.py:60,291-299) to the host, which writes
+ * `n_out` node ids, best first, into `actions`.  Return 0 on success. */
+typedef int (*md_select_cb)(void* user, int graph, const double* q, int n_nodes, int n_out,
+                            int32_t* actions);
+
+/* Create a context on HIP device `device`.  `weights` holds MD_WEIGHT_FLOATS floats
+ * (replaces MultiDismantler.LoadModel, U/MultiDismantler_torch.py:791-797). */
+md_status md_create(int device, const float* weights, size_t n_floats, int cost_mode, md_ctx** out);
+void md_destroy(md_ctx* ctx);
+const char* md_last_error(const md_ctx* ctx);
+
+/* Replace the weights of an existing context (LoadModel on a live agent). */
+md_status md_set_weights(md_ctx* ctx, const float* weights, size_t n_floats);
+
+/* Load a batch of two-layer graphs (replaces graph.Graph_test, U/graph.py:69-84, and
+ * MultiDismantler.InsertGraph :171-178).  Graph g has n_nodes[g] nodes (ids 0..n-1).
+ * Layer l's undirected edges of graph g are the pairs
+ *   edges_l[2*k], edges_l[2*k+1]   for k in [edge_off_l[g], edge_off_l[g+1])
+ * given in the reference's edge order (networkx G.edges(), U/graph.py:76): it fixes the
+ * neighbour-aggregation order (U/PrepareBatchGraph.py:151-160).  Self-loops and duplicate
+ * edges are rejected (MD_EINVAL).  `node_w` (degree cost only, else NULL) holds
+ * 2*sum(n_nodes) per-node weights: layer 0 of all graphs, then layer 1 (D/graph.py:91-115).
+ * Loading replaces any previously loaded batch and resets every graph (md_reset). */
+md_status md_load_graphs(md_ctx* ctx, int n_graphs, const int32_t* n_nodes,
+                         const int64_t* edge_off0, const int32_t* edges0,
+                         const int64_t* edge_off1, const int32_t* edges1,
+                         const float* node_w);
+
+/* MvcEnv.s0 for every loaded graph (U/mvc_env.py:31-52): clear covered/removed state and
+ * run the initial mutual-LMCC prune.  max_rank_out[g] (may be NULL) receives the initial
+ * LMCC size = Graph_test.max_rank (U/graph.py:80-84). */
+md_status md_reset(md_ctx* ctx, int32_t* max_rank_out);
+
+/* One Q evaluation of the current state of every graph (Predict, U/MultiDismantler_torch.py:263-302).
+ * q_out (may be NULL): sum(n_nodes) floats, graph-major; non-live nodes get -1073741823.5.
+ * argmax/n_tie/top_gap (may be NULL): per graph, arg-max node (-1 if terminal), number of
+ * nodes tied at the max, and the gap between the best and second-best live Q. */
+md_status md_predict(md_ctx* ctx, float* q_out, int32_t* argmax, int32_t* n_tie, float* top_gap);
+
+/* MvcEnv.stepWithoutReward for every graph with actions[g] >= 0 (U/mvc_env.py:74-87):
+ * cover the node, cascade the mutual-LMCC prune.  lmcc_out[g] (may be NULL) = LMCC size
+ * after the step (the `rank` of getReward :133-137); terminal_out[g] = isTerminal (:128-131). */
+md_status md_step(md_ctx* ctx, const int32_t* actions, int32_t* lmcc_out, uint8_t* terminal_out);
+
+/* The whole rollout of every graph from its current state to terminal, on the device
+ * (GetSol / GetSolution loop).  `step` = nodes removed per prediction (stepRatio, :676-679);
+ * with step > 1 every prediction goes through `cb`.  Outputs, per graph g with capacity
+ * n_nodes[g] entries at node_off(g) = sum_{h<g} n_nodes[h]:
+ *   seq_out   removal order;  lmcc_out  LMCC size after each removal;  seq_len[g] count.
+ * cb may be NULL only if no tie occurs (else MD_ECALLBACK). */
+md_status md_rollout(md_ctx* ctx, int step, int32_t* seq_out, int32_t* lmcc_out, int32_t* seq_len,
+                     md_select_cb cb, void* user);
+
+/* Per-step diagnostics of the last md_rollout for graph g (capacity n_nodes[g] rows):
+ * live nodes, alive edges in layer 0 and 1, number of nodes tied at the max, per prediction,
+ * and (float) the best Q and top-2 gap.  Returns the number of predictions made. */
+md_status md_rollout_trace(md_ctx* ctx, int graph, int32_t* n_live, int32_t* m0, int32_t* m1,
+                           int32_t* n_tie, float* qmax, float* gap, int32_t* n_pred);
+
+/* Read back the environment state of graph g (MvcEnv attributes, U/mvc_env.py:8-29):
+ * covered[n] (0/1), removed_l[e_l] (1 = pruned by MCC, i.e. in remove_edge[l]),
+ * counters[6] = {numCoveredEdges[0], numCoveredEdges[1], |removed0|, |removed1|, lmcc, terminal}. */
+md_status md_get_state(md_ctx* ctx, int graph, uint8_t* covered, uint8_t* removed0, uint8_t* removed1,
+                       int32_t* counters);
+
+/* Overwrite the state of graph g (PredictWithCurrentQNet on an arbitrary state): covered
+ * nodes and pruned edges; no MCC is run (the reference's Predict runs none). */
+md_status md_set_state(md_ctx* ctx, int graph, const uint8_t* covered, const uint8_t* removed0,
+                       const uint8_t* removed1);
+
+/* Execution geometry: workgroups cooperating on one graph ("team"), 0 = automatic
+ * (whole GPU for one graph, one workgroup per graph for large batches). */
+md_status md_set_team_size(md_ctx* ctx, int team_size);
+
+/* Device time (ms) of the last md_rollout / md_predict kernel launches, measured with HIP
+ * events on the context's stream, and the number of launches they took. */
+md_status md_last_timing(md_ctx* ctx, double* kernel_ms, int32_t* launches);
+
+/* Library build string (arch, version). */
+const char* md_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MDROLL_H */

@@ -1,0 +1,667 @@
+// md_abi.cpp — C ABI of libmdroll.so (declared in include/mdroll.h).
+//
+// Owns all device memory of a context, builds the CSR adjacency in the reference's
+// neighbour order, drives the persistent rollout kernel and resolves exact Q ties on the
+// host through the caller's callback (the reference's np.argsort order).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/mdroll.h"
+#include "md_common.h"
+
+namespace md {
+int lds_bytes();
+int lds_mcc_cap();
+int weight_image_floats();
+void build_weight_image(const float* w, float* img);
+hipError_t launch_rollout(const Params& p, const float* wimg, int grid, hipStream_t s);
+hipError_t launch_reset(const Params& p, hipStream_t s);
+hipError_t set_kernel_attrs();
+}  // namespace md
+
+using namespace md;
+
+namespace {
+
+constexpr double QMASK = -(2147483647.0 / 2.0);  // U/MultiDismantler_torch.py:60
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t alloc(size_t count) {
+    release();
+    n = count;
+    if (count == 0) return hipSuccess;
+    return hipMalloc((void**)&p, count * sizeof(T));
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+}  // namespace
+
+struct md_ctx {
+  int device = 0;
+  int cost_mode = MD_COST_UNIT;
+  int cus = 256;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::string err;
+  int team_size_req = 0;
+  double last_ms = 0.0;
+  int last_launches = 0;
+
+  DevBuf<float> w, wimg;
+  // graphs
+  int ng = 0;
+  std::vector<GraphInfo> hinfo;
+  std::vector<GraphVar> hvar;
+  size_t tot_n = 0, tot_e[2] = {0, 0}, tot_c[2] = {0, 0}, tot_r[2] = {0, 0};
+  DevBuf<GraphInfo> ginfo;
+  DevBuf<GraphVar> gvar;
+  DevBuf<int> rowptr[2], adj[2], ceid[2], eu[2], ev[2];
+  DevBuf<uint8_t> estate[2], covered;
+  DevBuf<int> deg[2], live, gpar, pend, tr_action, tr_rank, tr_stat, glist, team_graph, ctl;
+  DevBuf<float> H[2][2], h0tab[2], q, spart, apart, tr_q, node_w;
+  bool need_gpar = false;
+
+  ~md_ctx() {
+    if (stream) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipStreamDestroy(stream);
+    }
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    w.release();
+    wimg.release();
+    free_graphs();
+  }
+  void free_graphs() {
+    ginfo.release();
+    gvar.release();
+    for (int l = 0; l < 2; ++l) {
+      rowptr[l].release(); adj[l].release(); ceid[l].release(); eu[l].release(); ev[l].release();
+      estate[l].release(); deg[l].release(); h0tab[l].release();
+      H[l][0].release(); H[l][1].release();
+    }
+    covered.release(); live.release(); gpar.release(); pend.release(); tr_action.release(); tr_rank.release();
+    tr_stat.release(); glist.release(); team_graph.release(); ctl.release(); q.release(); spart.release();
+    apart.release(); tr_q.release(); node_w.release();
+    ng = 0;
+    hinfo.clear();
+    hvar.clear();
+  }
+};
+
+namespace {
+
+md_status fail(md_ctx* c, md_status s, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return s;
+}
+
+#define HIPCHK(ctx, call)                                                                          \
+  do {                                                                                             \
+    hipError_t e_ = (call);                                                                        \
+    if (e_ != hipSuccess) return fail(ctx, e_ == hipErrorOutOfMemory ? MD_EOOM : MD_EHIP, "%s: %s", \
+                                      #call, hipGetErrorString(e_));                               \
+  } while (0)
+
+// Control block layout (ints): [0] queue head, [1] error word, [4..4+MAX_TEAM) barrier counters.
+constexpr int CTL_QUEUE = 0, CTL_ERR = 1, CTL_BAR = 4, CTL_WORDS = 4 + MAX_TEAM;
+
+Params make_params(md_ctx* c) {
+  Params p{};
+  p.w = c->w.p;
+  p.ginfo = c->ginfo.p;
+  p.gvar = c->gvar.p;
+  for (int l = 0; l < 2; ++l) {
+    p.rowptr[l] = c->rowptr[l].p;
+    p.adj[l] = c->adj[l].p;
+    p.ceid[l] = c->ceid[l].p;
+    p.eu[l] = c->eu[l].p;
+    p.ev[l] = c->ev[l].p;
+    p.estate[l] = c->estate[l].p;
+    p.deg[l] = c->deg[l].p;
+    p.h0tab[l] = c->h0tab[l].p;
+    p.H[l][0] = c->H[l][0].p;
+    p.H[l][1] = c->H[l][1].p;
+  }
+  p.covered = c->covered.p;
+  p.live = c->live.p;
+  p.q = c->q.p;
+  p.gpar = c->gpar.p;
+  p.spart = c->spart.p;
+  p.apart = c->apart.p;
+  p.pend = c->pend.p;
+  p.tr_action = c->tr_action.p;
+  p.tr_rank = c->tr_rank.p;
+  p.tr_stat = c->tr_stat.p;
+  p.tr_q = c->tr_q.p;
+  p.node_w = c->cost_mode == MD_COST_DEGREE ? c->node_w.p : nullptr;
+  p.bar = (unsigned*)(c->ctl.p + CTL_BAR);
+  p.team_graph = c->team_graph.p;
+  p.queue = c->ctl.p + CTL_QUEUE;
+  p.err = c->ctl.p + CTL_ERR;
+  p.glist = c->glist.p;
+  p.lds_mcc_cap = lds_mcc_cap();
+  return p;
+}
+
+const char* err_name(int e) {
+  switch (e) {
+    case 1: return "team barrier timeout";
+    case 2: return "action on an already covered node";
+    case 3: return "live node sets differ between layers (U/PrepareBatchGraph.py:73)";
+    case 4: return "action out of range";
+    default: return "unknown device error";
+  }
+}
+
+md_status pull_vars(md_ctx* c) {
+  HIPCHK(c, hipMemcpyAsync(c->hvar.data(), c->gvar.p, sizeof(GraphVar) * c->ng, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MD_OK;
+}
+md_status push_vars(md_ctx* c) {
+  HIPCHK(c, hipMemcpyAsync(c->gvar.p, c->hvar.data(), sizeof(GraphVar) * c->ng, hipMemcpyHostToDevice, c->stream));
+  return MD_OK;
+}
+
+int auto_team_size(md_ctx* c, const std::vector<int>& gl) {
+  if (c->team_size_req > 0) return std::min(c->team_size_req, std::min(c->cus, MAX_TEAM));
+  int maxn = 1;
+  for (int g : gl) maxn = std::max(maxn, c->hinfo[g].n);
+  const int tiles = (maxn + TILE - 1) / TILE;
+  const int per_graph = std::max(1, c->cus / std::max(1, (int)gl.size()));
+  return std::max(1, std::min(std::min(per_graph, tiles), std::min(c->cus, MAX_TEAM)));
+}
+
+// One launch of the persistent kernel over the graphs in gl.
+md_status launch(md_ctx* c, const std::vector<int>& gl, int run_mode, int host_select) {
+  if (gl.empty()) return MD_OK;
+  const int tsz = auto_team_size(c, gl);
+  const int teams = std::max(1, std::min((int)gl.size(), c->cus / tsz));
+  HIPCHK(c, hipMemcpyAsync(c->glist.p, gl.data(), sizeof(int) * gl.size(), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->ctl.p, 0, sizeof(int) * CTL_WORDS, c->stream));
+  Params p = make_params(c);
+  p.nglist = (int)gl.size();
+  p.team_size = tsz;
+  p.run_mode = run_mode;
+  p.host_select = host_select;
+  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  HIPCHK(c, launch_rollout(p, c->wimg.p, teams * tsz, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  int dev_err = 0;
+  HIPCHK(c, hipMemcpyAsync(&dev_err, c->ctl.p + CTL_ERR, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  float ms = 0.f;
+  HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  c->last_ms += ms;
+  c->last_launches += 1;
+  if (dev_err) return fail(c, dev_err == 1 ? MD_ETIMEOUT : MD_EINVAL, "device: %s", err_name(dev_err));
+  return pull_vars(c);
+}
+
+void host_first_layer(const float* w, const float* nw, float* out) {
+  // degree cost: X = [w_l(i), 1.0] (D/PrepareBatchGraph.py:133-136); normalize(relu(X . w_n2l))
+  float x[64];
+  for (int c = 0; c < 64; ++c) {
+    float a = std::fma(nw[0], w[W_N2L + c], 0.f);
+    a = std::fma(1.0f, w[W_N2L + 64 + c], a);
+    x[c] = a > 0.f ? a : 0.f;
+  }
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int c = 0; c < 64; ++c) acc[c & 7] = std::fma(x[c], x[c], acc[c & 7]);
+  float s = acc[0];
+  for (int j = 1; j < 8; ++j) s = s + acc[j];
+  const float den = std::max(std::sqrt(s), 1e-12f);
+  for (int c = 0; c < 64; ++c) out[c] = x[c] / den;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* md_version(void) { return "libmdroll 0.1 (gfx950, HIP " HIP_VERSION_BUILD_NAME ")"; }
+
+const char* md_last_error(const md_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+md_status md_create(int device, const float* weights, size_t n_floats, int cost_mode, md_ctx** out) {
+  if (!out || !weights) return MD_EINVAL;
+  *out = nullptr;
+  if (n_floats != MD_WEIGHT_FLOATS) return MD_EINVAL;
+  if (cost_mode != MD_COST_UNIT && cost_mode != MD_COST_DEGREE) return MD_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MD_EHIP;
+  if (device < 0 || device >= ndev) return MD_EINVAL;
+  md_ctx* c = new md_ctx();
+  c->device = device;
+  c->cost_mode = cost_mode;
+  md_status st = MD_OK;
+  do {
+    if (hipSetDevice(device) != hipSuccess) { st = MD_EHIP; break; }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) { st = MD_EHIP; break; }
+    c->cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { st = MD_EHIP; break; }
+    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) { st = MD_EHIP; break; }
+    if (set_kernel_attrs() != hipSuccess) { st = MD_EHIP; break; }
+    st = md_set_weights(c, weights, n_floats);
+  } while (0);
+  if (st != MD_OK) {
+    delete c;
+    return st;
+  }
+  *out = c;
+  return MD_OK;
+}
+
+void md_destroy(md_ctx* ctx) { delete ctx; }
+
+md_status md_set_weights(md_ctx* c, const float* weights, size_t n_floats) {
+  if (!c || !weights || n_floats != MD_WEIGHT_FLOATS) return fail(c, MD_EINVAL, "weights: expected %d floats", MD_WEIGHT_FLOATS);
+  HIPCHK(c, hipSetDevice(c->device));
+  if (!c->w.p) HIPCHK(c, c->w.alloc(W_TOTAL + 3));
+  const int ni = weight_image_floats();
+  if (!c->wimg.p) HIPCHK(c, c->wimg.alloc(ni));
+  std::vector<float> img(ni);
+  build_weight_image(weights, img.data());
+  HIPCHK(c, hipMemcpyAsync(c->w.p, weights, sizeof(float) * W_TOTAL, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->wimg.p, img.data(), sizeof(float) * ni, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  // degree cost: the static first-layer input depends on the weights
+  if (c->ng > 0 && c->cost_mode == MD_COST_DEGREE) {
+    std::vector<float> nw(2 * c->tot_n);
+    HIPCHK(c, hipMemcpy(nw.data(), c->node_w.p, sizeof(float) * nw.size(), hipMemcpyDeviceToHost));
+    for (int l = 0; l < 2; ++l) {
+      std::vector<float> tab(c->tot_n * EMB);
+      for (size_t v = 0; v < c->tot_n; ++v) host_first_layer(weights, &nw[l * c->tot_n + v], &tab[v * EMB]);
+      HIPCHK(c, hipMemcpy(c->h0tab[l].p, tab.data(), sizeof(float) * tab.size(), hipMemcpyHostToDevice));
+    }
+  }
+  return MD_OK;
+}
+
+md_status md_set_team_size(md_ctx* c, int team_size) {
+  if (!c || team_size < 0) return MD_EINVAL;
+  c->team_size_req = team_size;
+  return MD_OK;
+}
+
+md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const int64_t* edge_off0,
+                         const int32_t* edges0, const int64_t* edge_off1, const int32_t* edges1,
+                         const float* node_w) {
+  if (!c) return MD_EINVAL;
+  if (n_graphs <= 0 || !n_nodes || !edge_off0 || !edge_off1) return fail(c, MD_EINVAL, "bad graph batch");
+  if (c->cost_mode == MD_COST_DEGREE && !node_w) return fail(c, MD_EINVAL, "degree cost needs node_w");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->free_graphs();
+  const int64_t* eo[2] = {edge_off0, edge_off1};
+  const int32_t* ed[2] = {edges0, edges1};
+  std::vector<GraphInfo> info(n_graphs);
+  size_t tn = 0, te[2] = {0, 0};
+  int maxn = 0;
+  for (int g = 0; g < n_graphs; ++g) {
+    const int n = n_nodes[g];
+    if (n <= 0) return fail(c, MD_EINVAL, "graph %d: n_nodes must be > 0", g);
+    GraphInfo& gi = info[g];
+    gi.n = n;
+    gi.node_off = (int)tn;
+    for (int l = 0; l < 2; ++l) {
+      const int64_t ne = eo[l][g + 1] - eo[l][g];
+      if (ne < 0) return fail(c, MD_EINVAL, "graph %d layer %d: negative edge count", g, l);
+      gi.e[l] = (int)ne;
+      gi.eoff[l] = (int)te[l];
+      gi.roff[l] = (int)(tn + g);
+      gi.coff[l] = (int)(2 * te[l]);
+      te[l] += ne;
+    }
+    tn += n;
+    maxn = std::max(maxn, n);
+  }
+  if (tn > (size_t)INT32_MAX / EMB || te[0] > (size_t)INT32_MAX / 2 || te[1] > (size_t)INT32_MAX / 2)
+    return fail(c, MD_EINVAL, "batch too large");
+  // host CSR in reference order
+  std::vector<int> rowptr[2], adj[2], ceid[2], eu[2], ev[2];
+  for (int l = 0; l < 2; ++l) {
+    rowptr[l].assign(tn + n_graphs, 0);
+    adj[l].resize(2 * te[l]);
+    ceid[l].resize(2 * te[l]);
+    eu[l].resize(te[l]);
+    ev[l].resize(te[l]);
+    for (int g = 0; g < n_graphs; ++g) {
+      const GraphInfo& gi = info[g];
+      const int n = gi.n;
+      int* rp = rowptr[l].data() + gi.roff[l];
+      std::unordered_set<uint64_t> seen;
+      seen.reserve(gi.e[l] * 2 + 1);
+      for (int k = 0; k < gi.e[l]; ++k) {
+        const int u = ed[l][2 * (eo[l][g] + k)], v = ed[l][2 * (eo[l][g] + k) + 1];
+        if (u < 0 || v < 0 || u >= n || v >= n) return fail(c, MD_EINVAL, "graph %d layer %d edge %d: node out of range", g, l, k);
+        if (u == v) return fail(c, MD_EINVAL, "graph %d layer %d edge %d: self-loop", g, l, k);
+        const uint64_t key = ((uint64_t)std::min(u, v) << 32) | (uint32_t)std::max(u, v);
+        if (!seen.insert(key).second) return fail(c, MD_EINVAL, "graph %d layer %d: duplicate edge %d-%d", g, l, u, v);
+        eu[l][gi.eoff[l] + k] = u;
+        ev[l][gi.eoff[l] + k] = v;
+        rp[u + 1]++;
+        rp[v + 1]++;
+      }
+      for (int i = 0; i < n; ++i) rp[i + 1] += rp[i];
+      std::vector<int> fill(rp, rp + n);
+      int* a = adj[l].data() + gi.coff[l];
+      int* ce = ceid[l].data() + gi.coff[l];
+      for (int k = 0; k < gi.e[l]; ++k) {
+        const int u = eu[l][gi.eoff[l] + k], v = ev[l][gi.eoff[l] + k];
+        a[fill[v]] = u; ce[fill[v]++] = k;  // in_edges[v] gets u (U/PrepareBatchGraph.py:157)
+        a[fill[u]] = v; ce[fill[u]++] = k;  // in_edges[u] gets v (:159)
+      }
+    }
+  }
+  c->ng = n_graphs;
+  c->hinfo = info;
+  c->hvar.assign(n_graphs, GraphVar{});
+  c->tot_n = tn;
+  c->need_gpar = maxn > lds_mcc_cap();
+  HIPCHK(c, c->ginfo.alloc(n_graphs));
+  HIPCHK(c, c->gvar.alloc(n_graphs));
+  for (int l = 0; l < 2; ++l) {
+    c->tot_e[l] = te[l];
+    HIPCHK(c, c->rowptr[l].alloc(rowptr[l].size()));
+    HIPCHK(c, c->adj[l].alloc(std::max<size_t>(1, adj[l].size())));
+    HIPCHK(c, c->ceid[l].alloc(std::max<size_t>(1, ceid[l].size())));
+    HIPCHK(c, c->eu[l].alloc(std::max<size_t>(1, eu[l].size())));
+    HIPCHK(c, c->ev[l].alloc(std::max<size_t>(1, ev[l].size())));
+    HIPCHK(c, c->estate[l].alloc(std::max<size_t>(1, te[l])));
+    HIPCHK(c, c->deg[l].alloc(tn));
+    HIPCHK(c, c->h0tab[l].alloc(tn * EMB));
+    HIPCHK(c, c->H[l][0].alloc(tn * EMB));
+    HIPCHK(c, c->H[l][1].alloc(tn * EMB));
+    HIPCHK(c, hipMemcpyAsync(c->rowptr[l].p, rowptr[l].data(), sizeof(int) * rowptr[l].size(), hipMemcpyHostToDevice, c->stream));
+    if (te[l]) {
+      HIPCHK(c, hipMemcpyAsync(c->adj[l].p, adj[l].data(), sizeof(int) * adj[l].size(), hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->ceid[l].p, ceid[l].data(), sizeof(int) * ceid[l].size(), hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->eu[l].p, eu[l].data(), sizeof(int) * eu[l].size(), hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->ev[l].p, ev[l].data(), sizeof(int) * ev[l].size(), hipMemcpyHostToDevice, c->stream));
+    }
+  }
+  HIPCHK(c, c->covered.alloc(tn));
+  HIPCHK(c, c->live.alloc(tn));
+  if (c->need_gpar) HIPCHK(c, c->gpar.alloc(2 * tn));
+  HIPCHK(c, c->pend.alloc(tn));
+  HIPCHK(c, c->tr_action.alloc(tn));
+  HIPCHK(c, c->tr_rank.alloc(tn));
+  HIPCHK(c, c->tr_stat.alloc(4 * tn));
+  HIPCHK(c, c->tr_q.alloc(2 * tn));
+  HIPCHK(c, c->q.alloc(tn));
+  HIPCHK(c, c->glist.alloc(n_graphs));
+  HIPCHK(c, c->team_graph.alloc(MAX_TEAM));
+  HIPCHK(c, c->ctl.alloc(CTL_WORDS));
+  HIPCHK(c, c->spart.alloc((size_t)MAX_TEAM * 3 * 128));
+  HIPCHK(c, c->apart.alloc((size_t)MAX_TEAM * 4));
+  HIPCHK(c, hipMemcpyAsync(c->ginfo.p, info.data(), sizeof(GraphInfo) * n_graphs, hipMemcpyHostToDevice, c->stream));
+  if (c->cost_mode == MD_COST_DEGREE) {
+    HIPCHK(c, c->node_w.alloc(2 * tn));
+    HIPCHK(c, hipMemcpyAsync(c->node_w.p, node_w, sizeof(float) * 2 * tn, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<float> wv(W_TOTAL);
+    HIPCHK(c, hipMemcpy(wv.data(), c->w.p, sizeof(float) * W_TOTAL, hipMemcpyDeviceToHost));
+    for (int l = 0; l < 2; ++l) {
+      std::vector<float> tab(tn * EMB);
+      for (size_t v = 0; v < tn; ++v) host_first_layer(wv.data(), &node_w[l * tn + v], &tab[v * EMB]);
+      HIPCHK(c, hipMemcpy(c->h0tab[l].p, tab.data(), sizeof(float) * tab.size(), hipMemcpyHostToDevice));
+    }
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return md_reset(c, nullptr);
+}
+
+md_status md_reset(md_ctx* c, int32_t* max_rank_out) {
+  if (!c) return MD_EINVAL;
+  if (c->ng == 0) return fail(c, MD_ESTATE, "no graphs loaded");
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<int> gl(c->ng);
+  for (int g = 0; g < c->ng; ++g) gl[g] = g;
+  HIPCHK(c, hipMemcpyAsync(c->glist.p, gl.data(), sizeof(int) * gl.size(), hipMemcpyHostToDevice, c->stream));
+  Params p = make_params(c);
+  p.nglist = c->ng;
+  HIPCHK(c, launch_reset(p, c->stream));
+  c->last_ms = 0.0;
+  c->last_launches = 0;
+  md_status st = launch(c, gl, RUN_STEP, 0);  // s0: initial prune (U/mvc_env.py:52)
+  if (st != MD_OK) return st;
+  if (max_rank_out)
+    for (int g = 0; g < c->ng; ++g) max_rank_out[g] = c->hvar[g].max_rank;
+  return MD_OK;
+}
+
+md_status md_predict(md_ctx* c, float* q_out, int32_t* argmax, int32_t* n_tie, float* top_gap) {
+  if (!c) return MD_EINVAL;
+  if (c->ng == 0) return fail(c, MD_ESTATE, "no graphs loaded");
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<int> gl;
+  for (int g = 0; g < c->ng; ++g) {
+    GraphVar& v = c->hvar[g];
+    if (v.alive[0] > 0 && v.alive[1] > 0 && v.n_live > 0) {
+      v.status = ST_RUN;
+      v.npend = 0;
+      gl.push_back(g);
+    }
+  }
+  md_status st = push_vars(c);
+  if (st != MD_OK) return st;
+  c->last_ms = 0.0;
+  c->last_launches = 0;
+  if (!gl.empty()) {
+    // graphs with no live node keep their (all masked) q
+    st = launch(c, gl, RUN_PREDICT, 0);
+    if (st != MD_OK) return st;
+  }
+  if (q_out) HIPCHK(c, hipMemcpy(q_out, c->q.p, sizeof(float) * c->tot_n, hipMemcpyDeviceToHost));
+  for (int g = 0; g < c->ng; ++g) {
+    const bool ran = std::find(gl.begin(), gl.end(), g) != gl.end();
+    if (argmax) argmax[g] = ran ? c->hvar[g].argmax : -1;
+    if (n_tie) n_tie[g] = ran ? c->hvar[g].ntie : 0;
+    if (top_gap) top_gap[g] = ran ? c->hvar[g].gap : 0.f;
+  }
+  return MD_OK;
+}
+
+md_status md_step(md_ctx* c, const int32_t* actions, int32_t* lmcc_out, uint8_t* terminal_out) {
+  if (!c || !actions) return MD_EINVAL;
+  if (c->ng == 0) return fail(c, MD_ESTATE, "no graphs loaded");
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<int> gl;
+  for (int g = 0; g < c->ng; ++g) {
+    const int a = actions[g];
+    if (a < 0) continue;
+    const GraphInfo& gi = c->hinfo[g];
+    if (a >= gi.n) return fail(c, MD_EINVAL, "graph %d: action %d out of range", g, a);
+    GraphVar& v = c->hvar[g];
+    if (v.alive[0] == 0 || v.alive[1] == 0) continue;  // terminal: stepping is a no-op
+    v.status = ST_RUN;
+    v.npend = 1;
+    HIPCHK(c, hipMemcpyAsync(c->pend.p + gi.node_off, &actions[g], sizeof(int), hipMemcpyHostToDevice, c->stream));
+    gl.push_back(g);
+  }
+  md_status st = push_vars(c);
+  if (st != MD_OK) return st;
+  c->last_ms = 0.0;
+  c->last_launches = 0;
+  st = launch(c, gl, RUN_STEP, 0);
+  if (st != MD_OK) return st;
+  for (int g = 0; g < c->ng; ++g) {
+    const GraphVar& v = c->hvar[g];
+    if (lmcc_out) lmcc_out[g] = v.lmcc;
+    if (terminal_out) terminal_out[g] = (v.alive[0] == 0 || v.alive[1] == 0) ? 1 : 0;
+  }
+  return MD_OK;
+}
+
+md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, int32_t* seq_len, md_select_cb cb,
+                     void* user) {
+  if (!c || step < 1) return MD_EINVAL;
+  if (c->ng == 0) return fail(c, MD_ESTATE, "no graphs loaded");
+  HIPCHK(c, hipSetDevice(c->device));
+  const int host_select = step > 1 ? 1 : 0;
+  c->last_ms = 0.0;
+  c->last_launches = 0;
+  std::vector<int> gl;
+  for (int g = 0; g < c->ng; ++g) {
+    GraphVar& v = c->hvar[g];
+    if (v.alive[0] > 0 && v.alive[1] > 0) {
+      v.status = ST_RUN;
+      v.npend = 0;
+      gl.push_back(g);
+    }
+  }
+  std::vector<float> qrow;
+  std::vector<double> qd;
+  std::vector<int32_t> acts;
+  while (!gl.empty()) {
+    md_status st = push_vars(c);
+    if (st != MD_OK) return st;
+    st = launch(c, gl, RUN_ROLLOUT, host_select);
+    if (st != MD_OK) return st;
+    std::vector<int> next;
+    for (int g : gl) {
+      GraphVar& v = c->hvar[g];
+      if (v.status != ST_NEED_HOST) continue;
+      const GraphInfo& gi = c->hinfo[g];
+      if (!cb) return fail(c, MD_ECALLBACK, "graph %d: %d nodes tie at the max Q and no selection callback was given", g, v.ntie);
+      qrow.resize(gi.n);
+      qd.resize(gi.n);
+      HIPCHK(c, hipMemcpy(qrow.data(), c->q.p + gi.node_off, sizeof(float) * gi.n, hipMemcpyDeviceToHost));
+      for (int i = 0; i < gi.n; ++i) qd[i] = std::isinf(qrow[i]) ? QMASK : (double)qrow[i];
+      const int nout = std::min(step, gi.n);
+      acts.assign(nout, -1);
+      if (cb(user, g, qd.data(), gi.n, nout, acts.data()) != 0) return fail(c, MD_ECALLBACK, "selection callback failed (graph %d)", g);
+      int k = 0;
+      for (int i = 0; i < nout; ++i) {
+        if (acts[i] < 0 || acts[i] >= gi.n) return fail(c, MD_ECALLBACK, "callback returned node %d out of range", acts[i]);
+        acts[k++] = acts[i];
+      }
+      HIPCHK(c, hipMemcpy(c->pend.p + gi.node_off, acts.data(), sizeof(int) * k, hipMemcpyHostToDevice));
+      v.npend = k;
+      v.status = ST_RUN;
+      next.push_back(g);
+    }
+    gl.swap(next);
+  }
+  std::vector<int> buf(c->tot_n);
+  if (seq_out) HIPCHK(c, hipMemcpy(seq_out, c->tr_action.p, sizeof(int) * c->tot_n, hipMemcpyDeviceToHost));
+  if (lmcc_out) HIPCHK(c, hipMemcpy(lmcc_out, c->tr_rank.p, sizeof(int) * c->tot_n, hipMemcpyDeviceToHost));
+  if (seq_len)
+    for (int g = 0; g < c->ng; ++g) seq_len[g] = c->hvar[g].steps;
+  return MD_OK;
+}
+
+md_status md_rollout_trace(md_ctx* c, int graph, int32_t* n_live, int32_t* m0, int32_t* m1, int32_t* n_tie,
+                           float* qmax, float* gap, int32_t* n_pred) {
+  if (!c || graph < 0 || graph >= c->ng) return MD_EINVAL;
+  const GraphInfo& gi = c->hinfo[graph];
+  const int np = std::min(c->hvar[graph].npred, gi.n);
+  std::vector<int> st(4 * (size_t)np);
+  std::vector<float> tq(2 * (size_t)np);
+  if (np > 0) {
+    HIPCHK(c, hipMemcpy(st.data(), c->tr_stat.p + 4 * (size_t)gi.node_off, sizeof(int) * st.size(), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(tq.data(), c->tr_q.p + 2 * (size_t)gi.node_off, sizeof(float) * tq.size(), hipMemcpyDeviceToHost));
+  }
+  for (int t = 0; t < np; ++t) {
+    if (n_live) n_live[t] = st[4 * t + 0];
+    if (m0) m0[t] = st[4 * t + 1];
+    if (m1) m1[t] = st[4 * t + 2];
+    if (n_tie) n_tie[t] = st[4 * t + 3];
+    if (qmax) qmax[t] = tq[2 * t + 0];
+    if (gap) gap[t] = tq[2 * t + 1];
+  }
+  if (n_pred) *n_pred = np;
+  return MD_OK;
+}
+
+md_status md_get_state(md_ctx* c, int graph, uint8_t* covered, uint8_t* removed0, uint8_t* removed1, int32_t* counters) {
+  if (!c || graph < 0 || graph >= c->ng) return MD_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  const GraphInfo& gi = c->hinfo[graph];
+  if (covered) HIPCHK(c, hipMemcpy(covered, c->covered.p + gi.node_off, gi.n, hipMemcpyDeviceToHost));
+  uint8_t* outs[2] = {removed0, removed1};
+  for (int l = 0; l < 2; ++l) {
+    if (!outs[l] || gi.e[l] == 0) continue;
+    HIPCHK(c, hipMemcpy(outs[l], c->estate[l].p + gi.eoff[l], gi.e[l], hipMemcpyDeviceToHost));
+    for (int e = 0; e < gi.e[l]; ++e) outs[l][e] = outs[l][e] == E_PRUNED ? 1 : 0;
+  }
+  if (counters) {
+    const GraphVar& v = c->hvar[graph];
+    counters[0] = v.counter[0];
+    counters[1] = v.counter[1];
+    counters[2] = v.removed[0];
+    counters[3] = v.removed[1];
+    counters[4] = v.lmcc;
+    counters[5] = (v.alive[0] == 0 || v.alive[1] == 0) ? 1 : 0;
+  }
+  return MD_OK;
+}
+
+md_status md_set_state(md_ctx* c, int graph, const uint8_t* covered, const uint8_t* removed0, const uint8_t* removed1) {
+  if (!c || graph < 0 || graph >= c->ng || !covered) return MD_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  const GraphInfo& gi = c->hinfo[graph];
+  GraphVar& v = c->hvar[graph];
+  std::vector<int> eu, ev;
+  int ncov = 0;
+  for (int i = 0; i < gi.n; ++i) ncov += covered[i] ? 1 : 0;
+  const uint8_t* rem[2] = {removed0, removed1};
+  for (int l = 0; l < 2; ++l) {
+    std::vector<uint8_t> st(std::max(1, gi.e[l]));
+    eu.resize(gi.e[l]);
+    ev.resize(gi.e[l]);
+    if (gi.e[l]) {
+      HIPCHK(c, hipMemcpy(eu.data(), c->eu[l].p + gi.eoff[l], sizeof(int) * gi.e[l], hipMemcpyDeviceToHost));
+      HIPCHK(c, hipMemcpy(ev.data(), c->ev[l].p + gi.eoff[l], sizeof(int) * gi.e[l], hipMemcpyDeviceToHost));
+    }
+    int ccov = 0, cpr = 0, calive = 0;
+    for (int e = 0; e < gi.e[l]; ++e) {
+      if (rem[l] && rem[l][e]) { st[e] = E_PRUNED; cpr++; }
+      else if (covered[eu[e]] || covered[ev[e]]) { st[e] = E_COVERED; ccov++; }
+      else { st[e] = E_ALIVE; calive++; }
+    }
+    if (gi.e[l]) HIPCHK(c, hipMemcpy(c->estate[l].p + gi.eoff[l], st.data(), gi.e[l], hipMemcpyHostToDevice));
+    v.counter[l] = ccov;
+    v.removed[l] = cpr;
+    v.alive[l] = calive;
+  }
+  HIPCHK(c, hipMemcpy(c->covered.p + gi.node_off, covered, gi.n, hipMemcpyHostToDevice));
+  v.n_cov = ncov;
+  v.s0_done = 1;
+  v.npend = 0;
+  v.status = ST_RUN;
+  v.n_live = 1;  // recomputed by the next prediction's phase A
+  return push_vars(c);
+}
+
+md_status md_last_timing(md_ctx* c, double* kernel_ms, int32_t* launches) {
+  if (!c) return MD_EINVAL;
+  if (kernel_ms) *kernel_ms = c->last_ms;
+  if (launches) *launches = c->last_launches;
+  return MD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,100 @@
+// md_common.h — structures shared by the host ABI (md_abi.cpp) and the gfx950 kernels
+// (md_kernels.hip) of libmdroll.so.  Everything lives in device memory, laid out as flat
+// arrays over all loaded graphs (graph g's nodes at [node_off, node_off+n), its layer-l
+// undirected edges at [eoff[l], eoff[l]+e[l]), its CSR entries at [coff[l], coff[l]+2e[l])).
+#pragma once
+#include <stdint.h>
+
+namespace md {
+
+constexpr int EMB = 64;          // EMBEDDING_SIZE, U/MultiDismantler_torch.py:36
+constexpr int REG_HIDDEN = 32;   // REG_HIDDEN, :57
+constexpr int AUX_DIM = 4;       // aux_dim, :64
+constexpr int BP_ITERS = 3;      // max_bp_iter, :62
+constexpr int NTHREADS = 512;    // 8 waves: waves 0-3 work on layer 0, waves 4-7 on layer 1
+constexpr int TILE = 16;         // node rows per MFMA tile (v_mfma_f32_16x16x4_f32)
+constexpr int MAX_TEAM = 256;    // workgroups cooperating on one graph (one per CU)
+
+// Offsets (floats) of each tensor in the packed weight blob (see include/mdroll.h).
+enum WOff : int {
+  W_N2L = 0, W_P1 = 128, W_P2 = 4224, W_P3 = 8320, W_H1 = 16512, W_W2 = 18560, W_CP = 18596,
+  W_WL1 = 18660, W_WL2 = 26852, W_T = 26980, W_TB = 31076, W_LW = 31140, W_LB = 31204,
+  W_TOTAL = 31205
+};
+
+// Edge state (per undirected edge and layer).
+enum : uint8_t { E_ALIVE = 0, E_COVERED = 1, E_PRUNED = 2 };
+
+// Per-graph run status.
+enum : int { ST_RUN = 0, ST_TERMINAL = 1, ST_NEED_HOST = 2, ST_PAUSED = 3 };
+
+// What a launch does with each graph.
+enum : int { RUN_ROLLOUT = 0, RUN_PREDICT = 1, RUN_STEP = 2 };
+
+struct GraphInfo {           // immutable after md_load_graphs
+  int n;                     // nodes
+  int node_off;              // into per-node arrays
+  int e[2];                  // undirected edges per layer
+  int eoff[2];               // into per-edge arrays
+  int roff[2];               // into row-pointer arrays (n + 1 entries per graph)
+  int coff[2];               // into CSR entry arrays (2 e entries per graph)
+};
+
+struct GraphVar {            // mutable per-graph state
+  int status;                // ST_*
+  int s0_done;               // initial MCC prune done (MvcEnv.s0)
+  int npend;                 // actions queued by the host (pend[node_off ..])
+  int max_rank;              // LMCC after s0 (Graph_test.max_rank)
+  int lmcc;                  // LMCC after the last step
+  int n_cov;                 // covered nodes
+  int n_live;                // nodes with an alive edge (compact list length)
+  int steps;                 // removals applied since reset
+  int npred;                 // predictions made since reset
+  int dmax[2];               // max residual degree over live nodes
+  int counter[2];            // numCoveredEdges (U/mvc_env.py:81-84)
+  int removed[2];            // |remove_edge[l]| / 2
+  int alive[2];              // alive edges
+  long long twohop[2];       // sum over live nodes of C(deg, 2) (U/PrepareBatchGraph.py:62-72)
+  int argmax;                // last prediction: best node (-1 when tied / none)
+  int ntie;                  // last prediction: nodes tied at the max
+  float qmax, gap;           // last prediction: best Q and top-2 gap
+};
+
+struct Params {
+  const float* w;                  // packed weights (reference layout)
+  const GraphInfo* ginfo;
+  GraphVar* gvar;
+  const int* rowptr[2];            // CSR (neighbour order = reference in_edges order)
+  const int* adj[2];
+  const int* ceid[2];              // CSR entry -> undirected edge id (graph-local)
+  const int* eu[2];                // undirected endpoints (graph-local ids)
+  const int* ev[2];
+  uint8_t* estate[2];
+  uint8_t* covered;
+  int* deg[2];                     // residual degree per node
+  int* live;                       // compact ascending live-node list per graph
+  float* H[2][2];                  // [layer][buffer] node embeddings, node-major x 64
+  float* h0tab[2];                 // [layer] first-layer embedding by residual degree, (n+1) x 64
+  float* q;                        // per node, masked
+  int* gpar;                       // global union-find scratch (2 per node) for large graphs
+  float* spart;                    // per workgroup: [3 sums][2 layers][64]
+  float* apart;                    // per workgroup argmax partial: {max, second, idx, count}
+  int* pend;                       // per node slot: host-queued actions
+  int* tr_action;                  // per node slot: removal order
+  int* tr_rank;                    // per node slot: LMCC after each removal
+  int* tr_stat;                    // per node slot x 4: n_live, m0, m1, ntie per prediction
+  float* tr_q;                     // per node slot x 2: qmax, gap per prediction
+  const float* node_w;             // degree cost: [2][total nodes] static features, else null
+  unsigned* bar;                   // per team barrier counter (zeroed per launch)
+  int* team_graph;                 // per team: graph being processed
+  int* queue;                      // work-queue head (zeroed per launch)
+  const int* glist;                // graphs to process this launch
+  int nglist;
+  int team_size;
+  int run_mode;                    // RUN_*
+  int host_select;                 // 1: every prediction goes to the host (step > 1)
+  int lds_mcc_cap;                 // max nodes whose MCC fits the LDS scratch
+  int* err;                        // device error word (nonzero = failure code)
+};
+
+}  // namespace md
