@@ -133,6 +133,13 @@ md_status md_set_team_size(md_ctx* ctx, int team_size);
  * events on the context's stream, and the number of launches they took. */
 md_status md_last_timing(md_ctx* ctx, double* kernel_ms, int32_t* launches);
 
+/* Diagnostics: record device wall-clock (100 MHz) phase timestamps of workgroup 0, 16 slots
+ * per removal step, for up to `steps` steps per launch of the following calls (0 disables).
+ * md_profile_read copies the timestamps accumulated since md_profile was called and returns
+ * the number of steps recorded in *n_steps. */
+md_status md_profile(md_ctx* ctx, int steps);
+md_status md_profile_read(md_ctx* ctx, uint64_t* out, int capacity_steps, int32_t* n_steps);
+
 /* Library build string (arch, version). */
 const char* md_version(void);
 

@@ -20,7 +20,7 @@ STATUS_NAMES = {1: "MD_EINVAL", 2: "MD_EHIP", 3: "MD_EOOM", 4: "MD_ESTATE", 5: "
 # Every symbol include/mdroll.h declares (checked by tests/test_abi.py).
 EXPORTS = ("md_create", "md_destroy", "md_last_error", "md_set_weights", "md_load_graphs", "md_reset",
            "md_predict", "md_step", "md_rollout", "md_rollout_trace", "md_get_state", "md_set_state",
-           "md_set_team_size", "md_last_timing", "md_version")
+           "md_set_team_size", "md_last_timing", "md_profile", "md_profile_read", "md_version")
 
 _i32p = ctypes.POINTER(ctypes.c_int32)
 _i64p = ctypes.POINTER(ctypes.c_int64)
@@ -61,6 +61,8 @@ def load_library(path=LIB_PATH):
         "md_set_state": (ctypes.c_int, [vp, ctypes.c_int, _u8p, _u8p, _u8p]),
         "md_set_team_size": (ctypes.c_int, [vp, ctypes.c_int]),
         "md_last_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), _i32p]),
+        "md_profile": (ctypes.c_int, [vp, ctypes.c_int]),
+        "md_profile_read": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, _i32p]),
         "md_version": (ctypes.c_char_p, []),
     }
     for name, (res, args) in proto.items():
@@ -213,6 +215,16 @@ class Engine:
         r0 = np.ascontiguousarray(removed0, dtype=np.uint8)
         r1 = np.ascontiguousarray(removed1, dtype=np.uint8)
         self._check(self.lib.md_set_state(self.h, g, _ptr(cov, _u8p), _ptr(r0, _u8p), _ptr(r1, _u8p)))
+
+    def profile(self, steps):
+        self._check(self.lib.md_profile(self.h, int(steps)))
+
+    def profile_read(self, cap=4096):
+        out = np.zeros((cap, 16), np.uint64)
+        k = ctypes.c_int32()
+        self._check(self.lib.md_profile_read(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), cap,
+                                             ctypes.byref(k)))
+        return out[:k.value]
 
     def last_timing(self):
         ms = ctypes.c_double()

@@ -19,8 +19,8 @@
 
 namespace md {
 int lds_bytes();
-int lds_mcc_cap();
 int weight_image_floats();
+bool phase_a_fits_lds_host(int n, int edges);
 void build_weight_image(const float* w, float* img);
 hipError_t launch_rollout(const Params& p, const float* wimg, int grid, hipStream_t s);
 hipError_t launch_reset(const Params& p, hipStream_t s);
@@ -71,11 +71,15 @@ struct md_ctx {
   size_t tot_n = 0, tot_e[2] = {0, 0}, tot_c[2] = {0, 0}, tot_r[2] = {0, 0};
   DevBuf<GraphInfo> ginfo;
   DevBuf<GraphVar> gvar;
-  DevBuf<int> rowptr[2], adj[2], ceid[2], eu[2], ev[2];
-  DevBuf<uint8_t> estate[2], covered;
-  DevBuf<int> deg[2], live, gpar, pend, tr_action, tr_rank, tr_stat, glist, team_graph, ctl;
-  DevBuf<float> H[2][2], h0tab[2], q, spart, apart, tr_q, node_w;
-  bool need_gpar = false;
+  size_t tot_tiles = 0;
+  DevBuf<int> rowptr[2], adj[2], epos[2], eu[2], ev[2];
+  DevBuf<uint8_t> estate[2], calive[2], covered;
+  DevBuf<int> deg[2], live, gscr, pend, tr_action, tr_rank, tr_stat, glist, ctl;
+  DevBuf<float> H[2][2], h0tab[2], q, spart, apart, ybuf, tr_q, node_w;
+  bool need_gscr = false;
+  DevBuf<unsigned long long> prof;
+  int prof_cap = 0;
+  std::vector<unsigned long long> prof_host;
 
   ~md_ctx() {
     if (stream) {
@@ -86,19 +90,20 @@ struct md_ctx {
     if (ev1) (void)hipEventDestroy(ev1);
     w.release();
     wimg.release();
+    prof.release();
     free_graphs();
   }
   void free_graphs() {
     ginfo.release();
     gvar.release();
     for (int l = 0; l < 2; ++l) {
-      rowptr[l].release(); adj[l].release(); ceid[l].release(); eu[l].release(); ev[l].release();
-      estate[l].release(); deg[l].release(); h0tab[l].release();
+      rowptr[l].release(); adj[l].release(); epos[l].release(); eu[l].release(); ev[l].release();
+      estate[l].release(); calive[l].release(); deg[l].release(); h0tab[l].release();
       H[l][0].release(); H[l][1].release();
     }
-    covered.release(); live.release(); gpar.release(); pend.release(); tr_action.release(); tr_rank.release();
-    tr_stat.release(); glist.release(); team_graph.release(); ctl.release(); q.release(); spart.release();
-    apart.release(); tr_q.release(); node_w.release();
+    covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
+    tr_stat.release(); glist.release(); ctl.release(); q.release(); spart.release();
+    apart.release(); ybuf.release(); tr_q.release(); node_w.release();
     ng = 0;
     hinfo.clear();
     hvar.clear();
@@ -124,8 +129,8 @@ md_status fail(md_ctx* c, md_status s, const char* fmt, ...) {
                                       #call, hipGetErrorString(e_));                               \
   } while (0)
 
-// Control block layout (ints): [0] queue head, [1] error word, [4..4+MAX_TEAM) barrier counters.
-constexpr int CTL_QUEUE = 0, CTL_ERR = 1, CTL_BAR = 4, CTL_WORDS = 4 + MAX_TEAM;
+// Control block layout (ints): [0] barrier counter, [1] error word (zeroed before each launch).
+constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_WORDS = 4;
 
 Params make_params(md_ctx* c) {
   Params p{};
@@ -135,7 +140,8 @@ Params make_params(md_ctx* c) {
   for (int l = 0; l < 2; ++l) {
     p.rowptr[l] = c->rowptr[l].p;
     p.adj[l] = c->adj[l].p;
-    p.ceid[l] = c->ceid[l].p;
+    p.calive[l] = c->calive[l].p;
+    p.epos[l] = c->epos[l].p;
     p.eu[l] = c->eu[l].p;
     p.ev[l] = c->ev[l].p;
     p.estate[l] = c->estate[l].p;
@@ -147,9 +153,10 @@ Params make_params(md_ctx* c) {
   p.covered = c->covered.p;
   p.live = c->live.p;
   p.q = c->q.p;
-  p.gpar = c->gpar.p;
+  p.gscr = c->gscr.p;
   p.spart = c->spart.p;
   p.apart = c->apart.p;
+  p.ybuf = c->ybuf.p;
   p.pend = c->pend.p;
   p.tr_action = c->tr_action.p;
   p.tr_rank = c->tr_rank.p;
@@ -157,11 +164,10 @@ Params make_params(md_ctx* c) {
   p.tr_q = c->tr_q.p;
   p.node_w = c->cost_mode == MD_COST_DEGREE ? c->node_w.p : nullptr;
   p.bar = (unsigned*)(c->ctl.p + CTL_BAR);
-  p.team_graph = c->team_graph.p;
-  p.queue = c->ctl.p + CTL_QUEUE;
   p.err = c->ctl.p + CTL_ERR;
   p.glist = c->glist.p;
-  p.lds_mcc_cap = lds_mcc_cap();
+  p.prof = c->prof_cap > 0 ? c->prof.p : nullptr;
+  p.prof_cap = c->prof_cap;
   return p;
 }
 
@@ -185,29 +191,28 @@ md_status push_vars(md_ctx* c) {
   return MD_OK;
 }
 
-int auto_team_size(md_ctx* c, const std::vector<int>& gl) {
-  if (c->team_size_req > 0) return std::min(c->team_size_req, std::min(c->cus, MAX_TEAM));
-  int maxn = 1;
-  for (int g : gl) maxn = std::max(maxn, c->hinfo[g].n);
-  const int tiles = (maxn + TILE - 1) / TILE;
-  const int per_graph = std::max(1, c->cus / std::max(1, (int)gl.size()));
-  return std::max(1, std::min(std::min(per_graph, tiles), std::min(c->cus, MAX_TEAM)));
+// Workgroups of one launch: enough for every graph's phase A and every 16-row tile, at most
+// one per CU (the kernel is persistent and relies on co-residency for its grid barrier).
+int grid_size(md_ctx* c, const std::vector<int>& gl) {
+  if (c->team_size_req > 0) return std::max(1, std::min(c->team_size_req, c->cus));
+  long tiles = 0;
+  for (int g : gl) tiles += (c->hinfo[g].n + TILE - 1) / TILE;
+  const long want = std::max<long>((long)gl.size(), tiles);
+  return (int)std::max<long>(1, std::min<long>(want, c->cus));
 }
 
-// One launch of the persistent kernel over the graphs in gl.
-md_status launch(md_ctx* c, const std::vector<int>& gl, int run_mode, int host_select) {
-  if (gl.empty()) return MD_OK;
-  const int tsz = auto_team_size(c, gl);
-  const int teams = std::max(1, std::min((int)gl.size(), c->cus / tsz));
-  HIPCHK(c, hipMemcpyAsync(c->glist.p, gl.data(), sizeof(int) * gl.size(), hipMemcpyHostToDevice, c->stream));
+// One launch of the persistent kernel over the graphs in gl (<= G_CAP of them).
+md_status launch_chunk(md_ctx* c, const int* gl, int ngl, int run_mode, int host_select) {
+  std::vector<int> v(gl, gl + ngl);
+  const int grid = grid_size(c, v);
+  HIPCHK(c, hipMemcpyAsync(c->glist.p, gl, sizeof(int) * ngl, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->ctl.p, 0, sizeof(int) * CTL_WORDS, c->stream));
   Params p = make_params(c);
-  p.nglist = (int)gl.size();
-  p.team_size = tsz;
+  p.nglist = ngl;
   p.run_mode = run_mode;
   p.host_select = host_select;
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-  HIPCHK(c, launch_rollout(p, c->wimg.p, teams * tsz, c->stream));
+  HIPCHK(c, launch_rollout(p, c->wimg.p, grid, c->stream));
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
   int dev_err = 0;
   HIPCHK(c, hipMemcpyAsync(&dev_err, c->ctl.p + CTL_ERR, sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -217,6 +222,24 @@ md_status launch(md_ctx* c, const std::vector<int>& gl, int run_mode, int host_s
   c->last_ms += ms;
   c->last_launches += 1;
   if (dev_err) return fail(c, dev_err == 1 ? MD_ETIMEOUT : MD_EINVAL, "device: %s", err_name(dev_err));
+  if (c->prof_cap > 0) {
+    std::vector<unsigned long long> tmp((size_t)c->prof_cap * 16);
+    HIPCHK(c, hipMemcpy(tmp.data(), c->prof.p, sizeof(unsigned long long) * tmp.size(), hipMemcpyDeviceToHost));
+    for (int s = 0; s < c->prof_cap; ++s) {
+      if (tmp[(size_t)s * 16] == 0) break;
+      c->prof_host.insert(c->prof_host.end(), tmp.begin() + (size_t)s * 16, tmp.begin() + (size_t)s * 16 + 16);
+    }
+    HIPCHK(c, hipMemset(c->prof.p, 0, sizeof(unsigned long long) * tmp.size()));
+  }
+  return MD_OK;
+}
+
+md_status launch(md_ctx* c, const std::vector<int>& gl, int run_mode, int host_select) {
+  for (size_t i = 0; i < gl.size(); i += G_CAP) {
+    const int k = (int)std::min<size_t>(G_CAP, gl.size() - i);
+    md_status st = launch_chunk(c, gl.data() + i, k, run_mode, host_select);
+    if (st != MD_OK) return st;
+  }
   return pull_vars(c);
 }
 
@@ -318,14 +341,16 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   const int64_t* eo[2] = {edge_off0, edge_off1};
   const int32_t* ed[2] = {edges0, edges1};
   std::vector<GraphInfo> info(n_graphs);
-  size_t tn = 0, te[2] = {0, 0};
-  int maxn = 0;
+  size_t tn = 0, te[2] = {0, 0}, tt = 0;
+  bool big = false;
   for (int g = 0; g < n_graphs; ++g) {
     const int n = n_nodes[g];
     if (n <= 0) return fail(c, MD_EINVAL, "graph %d: n_nodes must be > 0", g);
     GraphInfo& gi = info[g];
     gi.n = n;
     gi.node_off = (int)tn;
+    gi.tile_off = (int)tt;
+    gi.pad = 0;
     for (int l = 0; l < 2; ++l) {
       const int64_t ne = eo[l][g + 1] - eo[l][g];
       if (ne < 0) return fail(c, MD_EINVAL, "graph %d layer %d: negative edge count", g, l);
@@ -336,16 +361,18 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
       te[l] += ne;
     }
     tn += n;
-    maxn = std::max(maxn, n);
+    tt += (n + TILE - 1) / TILE;
+    if (!phase_a_fits_lds_host(n, gi.e[0] + gi.e[1])) big = true;
   }
-  if (tn > (size_t)INT32_MAX / EMB || te[0] > (size_t)INT32_MAX / 2 || te[1] > (size_t)INT32_MAX / 2)
+  if (tn > (size_t)INT32_MAX / EMB || te[0] > (size_t)INT32_MAX / 4 || te[1] > (size_t)INT32_MAX / 4)
     return fail(c, MD_EINVAL, "batch too large");
-  // host CSR in reference order
-  std::vector<int> rowptr[2], adj[2], ceid[2], eu[2], ev[2];
+  // static CSR in reference order: row i lists i's neighbours in the order the edges appear
+  // in G.edges() (the in_edges order of U/PrepareBatchGraph.py:151-160, U/graph_struct.py:63)
+  std::vector<int> rowptr[2], adj[2], epos[2], eu[2], ev[2];
   for (int l = 0; l < 2; ++l) {
     rowptr[l].assign(tn + n_graphs, 0);
     adj[l].resize(2 * te[l]);
-    ceid[l].resize(2 * te[l]);
+    epos[l].resize(2 * te[l]);
     eu[l].resize(te[l]);
     ev[l].resize(te[l]);
     for (int g = 0; g < n_graphs; ++g) {
@@ -368,11 +395,13 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
       for (int i = 0; i < n; ++i) rp[i + 1] += rp[i];
       std::vector<int> fill(rp, rp + n);
       int* a = adj[l].data() + gi.coff[l];
-      int* ce = ceid[l].data() + gi.coff[l];
+      int* ep = epos[l].data() + 2 * (size_t)gi.eoff[l];
       for (int k = 0; k < gi.e[l]; ++k) {
         const int u = eu[l][gi.eoff[l] + k], v = ev[l][gi.eoff[l] + k];
-        a[fill[v]] = u; ce[fill[v]++] = k;  // in_edges[v] gets u (U/PrepareBatchGraph.py:157)
-        a[fill[u]] = v; ce[fill[u]++] = k;  // in_edges[u] gets v (:159)
+        ep[2 * k] = fill[v];
+        a[fill[v]++] = u;  // in_edges[v] gets u (U/PrepareBatchGraph.py:157)
+        ep[2 * k + 1] = fill[u];
+        a[fill[u]++] = v;  // in_edges[u] gets v (:159)
       }
     }
   }
@@ -380,14 +409,16 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   c->hinfo = info;
   c->hvar.assign(n_graphs, GraphVar{});
   c->tot_n = tn;
-  c->need_gpar = maxn > lds_mcc_cap();
+  c->tot_tiles = tt;
+  c->need_gscr = big;
   HIPCHK(c, c->ginfo.alloc(n_graphs));
   HIPCHK(c, c->gvar.alloc(n_graphs));
   for (int l = 0; l < 2; ++l) {
     c->tot_e[l] = te[l];
     HIPCHK(c, c->rowptr[l].alloc(rowptr[l].size()));
     HIPCHK(c, c->adj[l].alloc(std::max<size_t>(1, adj[l].size())));
-    HIPCHK(c, c->ceid[l].alloc(std::max<size_t>(1, ceid[l].size())));
+    HIPCHK(c, c->epos[l].alloc(std::max<size_t>(1, epos[l].size())));
+    HIPCHK(c, c->calive[l].alloc(std::max<size_t>(1, 2 * te[l])));
     HIPCHK(c, c->eu[l].alloc(std::max<size_t>(1, eu[l].size())));
     HIPCHK(c, c->ev[l].alloc(std::max<size_t>(1, ev[l].size())));
     HIPCHK(c, c->estate[l].alloc(std::max<size_t>(1, te[l])));
@@ -398,14 +429,14 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
     HIPCHK(c, hipMemcpyAsync(c->rowptr[l].p, rowptr[l].data(), sizeof(int) * rowptr[l].size(), hipMemcpyHostToDevice, c->stream));
     if (te[l]) {
       HIPCHK(c, hipMemcpyAsync(c->adj[l].p, adj[l].data(), sizeof(int) * adj[l].size(), hipMemcpyHostToDevice, c->stream));
-      HIPCHK(c, hipMemcpyAsync(c->ceid[l].p, ceid[l].data(), sizeof(int) * ceid[l].size(), hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->epos[l].p, epos[l].data(), sizeof(int) * epos[l].size(), hipMemcpyHostToDevice, c->stream));
       HIPCHK(c, hipMemcpyAsync(c->eu[l].p, eu[l].data(), sizeof(int) * eu[l].size(), hipMemcpyHostToDevice, c->stream));
       HIPCHK(c, hipMemcpyAsync(c->ev[l].p, ev[l].data(), sizeof(int) * ev[l].size(), hipMemcpyHostToDevice, c->stream));
     }
   }
   HIPCHK(c, c->covered.alloc(tn));
   HIPCHK(c, c->live.alloc(tn));
-  if (c->need_gpar) HIPCHK(c, c->gpar.alloc(2 * tn));
+  if (c->need_gscr) HIPCHK(c, c->gscr.alloc(4 * tn));
   HIPCHK(c, c->pend.alloc(tn));
   HIPCHK(c, c->tr_action.alloc(tn));
   HIPCHK(c, c->tr_rank.alloc(tn));
@@ -413,10 +444,10 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->tr_q.alloc(2 * tn));
   HIPCHK(c, c->q.alloc(tn));
   HIPCHK(c, c->glist.alloc(n_graphs));
-  HIPCHK(c, c->team_graph.alloc(MAX_TEAM));
   HIPCHK(c, c->ctl.alloc(CTL_WORDS));
-  HIPCHK(c, c->spart.alloc((size_t)MAX_TEAM * 3 * 128));
-  HIPCHK(c, c->apart.alloc((size_t)MAX_TEAM * 4));
+  HIPCHK(c, c->spart.alloc(tt * 384));
+  HIPCHK(c, c->apart.alloc(tt * 4));
+  HIPCHK(c, c->ybuf.alloc((size_t)n_graphs * 128));
   HIPCHK(c, hipMemcpyAsync(c->ginfo.p, info.data(), sizeof(GraphInfo) * n_graphs, hipMemcpyHostToDevice, c->stream));
   if (c->cost_mode == MD_COST_DEGREE) {
     HIPCHK(c, c->node_w.alloc(2 * tn));
@@ -638,12 +669,19 @@ md_status md_set_state(md_ctx* c, int graph, const uint8_t* covered, const uint8
       HIPCHK(c, hipMemcpy(ev.data(), c->ev[l].p + gi.eoff[l], sizeof(int) * gi.e[l], hipMemcpyDeviceToHost));
     }
     int ccov = 0, cpr = 0, calive = 0;
+    std::vector<int> ep(2 * (size_t)std::max(1, gi.e[l]));
+    std::vector<uint8_t> ca(2 * (size_t)std::max(1, gi.e[l]), 1);
+    if (gi.e[l]) HIPCHK(c, hipMemcpy(ep.data(), c->epos[l].p + 2 * (size_t)gi.eoff[l], sizeof(int) * 2 * gi.e[l], hipMemcpyDeviceToHost));
     for (int e = 0; e < gi.e[l]; ++e) {
       if (rem[l] && rem[l][e]) { st[e] = E_PRUNED; cpr++; }
       else if (covered[eu[e]] || covered[ev[e]]) { st[e] = E_COVERED; ccov++; }
       else { st[e] = E_ALIVE; calive++; }
+      if (st[e] != E_ALIVE) ca[ep[2 * e]] = ca[ep[2 * e + 1]] = 0;
     }
-    if (gi.e[l]) HIPCHK(c, hipMemcpy(c->estate[l].p + gi.eoff[l], st.data(), gi.e[l], hipMemcpyHostToDevice));
+    if (gi.e[l]) {
+      HIPCHK(c, hipMemcpy(c->estate[l].p + gi.eoff[l], st.data(), gi.e[l], hipMemcpyHostToDevice));
+      HIPCHK(c, hipMemcpy(c->calive[l].p + gi.coff[l], ca.data(), 2 * (size_t)gi.e[l], hipMemcpyHostToDevice));
+    }
     v.counter[l] = ccov;
     v.removed[l] = cpr;
     v.alive[l] = calive;
@@ -655,6 +693,29 @@ md_status md_set_state(md_ctx* c, int graph, const uint8_t* covered, const uint8
   v.status = ST_RUN;
   v.n_live = 1;  // recomputed by the next prediction's phase A
   return push_vars(c);
+}
+
+md_status md_profile(md_ctx* c, int steps) {
+  if (!c || steps < 0) return MD_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  c->prof.release();
+  c->prof_cap = 0;
+  c->prof_host.clear();
+  if (steps > 0) {
+    HIPCHK(c, c->prof.alloc((size_t)steps * 16));
+    HIPCHK(c, hipMemset(c->prof.p, 0, sizeof(unsigned long long) * (size_t)steps * 16));
+    c->prof_cap = steps;
+  }
+  return MD_OK;
+}
+
+md_status md_profile_read(md_ctx* c, uint64_t* out, int capacity_steps, int32_t* n_steps) {
+  if (!c || capacity_steps < 0) return MD_EINVAL;
+  const int have = (int)(c->prof_host.size() / 16);
+  const int k = std::min(have, capacity_steps);
+  if (out) std::memcpy(out, c->prof_host.data(), sizeof(uint64_t) * 16 * (size_t)k);
+  if (n_steps) *n_steps = k;
+  return MD_OK;
 }
 
 md_status md_last_timing(md_ctx* c, double* kernel_ms, int32_t* launches) {

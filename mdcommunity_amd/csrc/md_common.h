@@ -1,7 +1,8 @@
 // md_common.h — structures shared by the host ABI (md_abi.cpp) and the gfx950 kernels
 // (md_kernels.hip) of libmdroll.so.  Everything lives in device memory, laid out as flat
 // arrays over all loaded graphs (graph g's nodes at [node_off, node_off+n), its layer-l
-// undirected edges at [eoff[l], eoff[l]+e[l]), its CSR entries at [coff[l], coff[l]+2e[l])).
+// undirected edges at [eoff[l], eoff[l]+e[l]), its CSR entries at [coff[l], coff[l]+2e[l]),
+// its 16-row tiles at [tile_off, tile_off + ceil(n/16))).
 #pragma once
 #include <stdint.h>
 
@@ -13,7 +14,7 @@ constexpr int AUX_DIM = 4;       // aux_dim, :64
 constexpr int BP_ITERS = 3;      // max_bp_iter, :62
 constexpr int NTHREADS = 512;    // 8 waves: waves 0-3 work on layer 0, waves 4-7 on layer 1
 constexpr int TILE = 16;         // node rows per MFMA tile (v_mfma_f32_16x16x4_f32)
-constexpr int MAX_TEAM = 256;    // workgroups cooperating on one graph (one per CU)
+constexpr int G_CAP = 512;       // graphs per kernel launch (the host chunks larger batches)
 
 // Offsets (floats) of each tensor in the packed weight blob (see include/mdroll.h).
 enum WOff : int {
@@ -38,6 +39,8 @@ struct GraphInfo {           // immutable after md_load_graphs
   int eoff[2];               // into per-edge arrays
   int roff[2];               // into row-pointer arrays (n + 1 entries per graph)
   int coff[2];               // into CSR entry arrays (2 e entries per graph)
+  int tile_off;              // into per-tile arrays (ceil(n / 16) tiles per graph)
+  int pad;
 };
 
 struct GraphVar {            // mutable per-graph state
@@ -64,9 +67,10 @@ struct Params {
   const float* w;                  // packed weights (reference layout)
   const GraphInfo* ginfo;
   GraphVar* gvar;
-  const int* rowptr[2];            // CSR (neighbour order = reference in_edges order)
+  const int* rowptr[2];            // static CSR (neighbour order = reference in_edges order)
   const int* adj[2];
-  const int* ceid[2];              // CSR entry -> undirected edge id (graph-local)
+  uint8_t* calive[2];              // per CSR entry: 1 while its edge is alive
+  const int* epos[2];              // per undirected edge: its two CSR entry positions
   const int* eu[2];                // undirected endpoints (graph-local ids)
   const int* ev[2];
   uint8_t* estate[2];
@@ -74,27 +78,26 @@ struct Params {
   int* deg[2];                     // residual degree per node
   int* live;                       // compact ascending live-node list per graph
   float* H[2][2];                  // [layer][buffer] node embeddings, node-major x 64
-  float* h0tab[2];                 // [layer] first-layer embedding by residual degree, (n+1) x 64
-  float* q;                        // per node, masked
-  int* gpar;                       // global union-find scratch (2 per node) for large graphs
-  float* spart;                    // per workgroup: [3 sums][2 layers][64]
-  float* apart;                    // per workgroup argmax partial: {max, second, idx, count}
+  float* h0tab[2];                 // [layer] first-layer embedding: by degree (unit) / by node (degree cost)
+  float* q;                        // per node (-inf = masked)
+  int* gscr;                       // phase-A scratch in global memory for graphs too big for LDS: 4 per node
+  float* spart;                    // per tile: [3 sums][2 layers][64] virtual-node partial sums
+  float* apart;                    // per tile: arg-max partial {max, second, idx, count}
+  float* ybuf;                     // per graph: [2][64] virtual-node embedding after iteration 2
   int* pend;                       // per node slot: host-queued actions
   int* tr_action;                  // per node slot: removal order
   int* tr_rank;                    // per node slot: LMCC after each removal
   int* tr_stat;                    // per node slot x 4: n_live, m0, m1, ntie per prediction
   float* tr_q;                     // per node slot x 2: qmax, gap per prediction
   const float* node_w;             // degree cost: [2][total nodes] static features, else null
-  unsigned* bar;                   // per team barrier counter (zeroed per launch)
-  int* team_graph;                 // per team: graph being processed
-  int* queue;                      // work-queue head (zeroed per launch)
-  const int* glist;                // graphs to process this launch
+  unsigned* bar;                   // grid barrier counter (zeroed per launch)
+  const int* glist;                // graphs processed by this launch (<= G_CAP)
   int nglist;
-  int team_size;
   int run_mode;                    // RUN_*
   int host_select;                 // 1: every prediction goes to the host (step > 1)
-  int lds_mcc_cap;                 // max nodes whose MCC fits the LDS scratch
   int* err;                        // device error word (nonzero = failure code)
+  unsigned long long* prof;        // optional phase timestamps of workgroup 0 (wall clock)
+  int prof_cap;                    // steps of 16 timestamp slots available in prof
 };
 
 }  // namespace md

@@ -1,20 +1,22 @@
 // md_kernels.hip — gfx950 (MI355X, CDNA4) kernels of the MultiDismantler inference rollout.
 //
-// One persistent kernel runs whole rollouts.  A "team" of workgroups owns one graph at a
-// time (team = whole GPU for a single N=1000 graph, one workgroup per graph for batches);
-// graphs are pulled from a device work queue.  Per removal step the team runs four phases
-// separated by team barriers:
-//   A  (team leader only) apply the chosen node (U/mvc_env.py:74-87), mutual-LMCC cascade
-//      by union-find in LDS (U/Mcc.py:30-38), residual degrees, ascending live-node list,
-//      aux features (U/PrepareBatchGraph.py:35-101), first-layer embedding table.
-//   1,2 message passing iterations (U/MultiDismantler_net_graphsage.py:288-321): CSR
-//      neighbour gather-sum in the reference's in_edges order, the node-update MLP on
-//      v_mfma_f32_16x16x4_f32 (k-ordered fp32 FMA chain == MKL's sgemm order), ReLU, row
-//      L2 norm in torch's reduction order; per-workgroup partial virtual-node sums.
-//   3  last iteration + inter-layer attention (U/MRGNN/mutil_layer_weight.py:266-313) +
-//      Q head (net :343-394) on the same rows, per-workgroup arg-max partials.
-// The leader reduces the arg-max partials at the start of the next phase A; exact ties go
-// back to the host (np.argsort tie order, U/MultiDismantler_torch.py:769).
+// One persistent kernel runs whole rollouts of a batch of graphs (1 ... G_CAP per launch).
+// All workgroups of the grid cooperate; per removal step they run four phases separated by
+// grid barriers (placement-independent agent-scope release/acquire):
+//   A  environment, one workgroup per graph: apply the chosen node (U/mvc_env.py:74-87),
+//      mutual-LMCC cascade by union-find over the graph's edges staged in LDS
+//      (U/Mcc.py:30-38), residual degrees, ascending live-node list and aux features
+//      (U/PrepareBatchGraph.py:35-101), first-layer embedding table.
+//   1,2 message passing (U/MultiDismantler_net_graphsage.py:288-321) over 16-row tiles of all
+//      graphs, spread over the grid in contiguous tile ranges: CSR neighbour gather-sum in the
+//      reference's in_edges order, the node-update MLP on v_mfma_f32_16x16x4_f32 (a k-ordered
+//      fp32 FMA chain == MKL's sgemm order), ReLU, row L2 norm in torch's reduction order,
+//      per-tile virtual-node partial sums.
+//   3  last iteration + inter-layer attention (U/MRGNN/mutil_layer_weight.py:266-313) + Q head
+//      (net :343-394) on the same rows, per-tile arg-max partials.
+// Phase A of the next step reduces a graph's arg-max partials in tile order (deterministic,
+// independent of the grid size).  Exact ties go back to the host: the reference breaks them
+// with numpy's unstable argsort (U/MultiDismantler_torch.py:769).
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -24,31 +26,33 @@ namespace md {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-// ------------------------------------------------------------------ LDS layout (floats)
+// ------------------------------------------------------------------ weight image (floats)
 // Weights in MFMA B-fragment order: frag[cb][s][lane] = W[4s + (lane>>4)][16cb + (lane&15)].
-constexpr int L_P1 = 0;                 // 4 x 16 x 64
-constexpr int L_P2 = L_P1 + 4096;
-constexpr int L_P3 = L_P2 + 4096;       // 4 x 32 x 64
-constexpr int L_T = L_P3 + 8192;        // 4 x 16 x 64
-constexpr int L_H1 = L_T + 4096;        // 2 x 16 x 64
-constexpr int L_TB = L_H1 + 2048;       // 64
-constexpr int L_LW = L_TB + 64;         // 64
-constexpr int L_CP = L_LW + 64;         // 64
-constexpr int L_W2 = L_CP + 64;         // 36 (+4)
-constexpr int L_LB = L_W2 + 40;         // 1 (+3)
-constexpr int L_WN = L_LB + 4;          // 128 (w_n2l row-major)
-constexpr int L_WL2 = L_WN + 128;       // 128
-constexpr int L_WEND = L_WL2 + 128;     // end of the weight image (copied from global)
-// per-workgroup persistent area
-constexpr int L_Y0 = L_WEND;            // [64]  virtual-node input embedding (constant)
-constexpr int L_Y = L_Y0 + 64;          // [2][64] virtual-node embedding of the current iteration
-constexpr int L_YS = L_Y + 128;         // [2][64] final graph vector y per layer
-constexpr int L_GS = L_YS + 128;        // graph scalars: mix w0,w1; aux dot per layer (4)
-constexpr int L_SACC = L_GS + 16;       // [3][2][64] partial virtual-node sums of this workgroup
-constexpr int L_MISC = L_SACC + 384;    // 64 words of broadcast scalars
-constexpr int L_GV = L_MISC + 64;       // 32 words: phase-A copy of the graph's GraphVar
-constexpr int L_SCR = L_GV + 32;        // scratch (phase-dependent)
-// scratch, GEMM phases
+constexpr int W_IP1 = 0;                // 4 x 16 x 64
+constexpr int W_IP2 = W_IP1 + 4096;
+constexpr int W_IP3 = W_IP2 + 4096;     // 4 x 32 x 64
+constexpr int W_IT = W_IP3 + 8192;      // 4 x 16 x 64
+constexpr int W_IH1 = W_IT + 4096;      // 2 x 16 x 64
+constexpr int W_ITB = W_IH1 + 2048;     // 64
+constexpr int W_ILW = W_ITB + 64;       // 64
+constexpr int W_ICP = W_ILW + 64;       // 64
+constexpr int W_IW2 = W_ICP + 64;       // 36 (+4)
+constexpr int W_ILB = W_IW2 + 40;       // 1 (+3)
+constexpr int W_IWN = W_ILB + 4;        // 128 (w_n2l row-major)
+constexpr int W_IWL2 = W_IWN + 128;     // 128
+constexpr int W_IEND = W_IWL2 + 128;
+
+// ------------------------------------------------------------------ LDS layout (floats)
+constexpr int L_PREF = 0;                        // int [G_CAP + 4] tile prefix of this step
+constexpr int L_MISC = L_PREF + G_CAP + 4;       // 64 words of broadcast scalars
+constexpr int L_GV = L_MISC + 64;                // 32 words: phase-A copy of a GraphVar
+constexpr int L_Y0 = L_GV + 32;                  // [64] virtual-node input embedding (constant)
+constexpr int L_YW = L_Y0 + 64;                  // [2][64] virtual-node embedding being iterated
+constexpr int L_YS = L_YW + 128;                 // [2][64] final graph vector y per layer
+constexpr int L_GS = L_YS + 128;                 // graph scalars: mix w0,w1; aux per layer
+constexpr int L_W = L_GS + 16;                   // weight image
+constexpr int L_SCR = L_W + W_IEND;              // tile scratch
+// tile scratch (offsets from L_SCR)
 constexpr int LDT = 17;                 // transposed tile: At[k][row], 16 rows + 1 pad
 constexpr int S_P = 0;                  // [2][64][17] gathered neighbour sums
 constexpr int S_X = S_P + 2 * 64 * LDT; // [2][64][17] own embedding
@@ -63,14 +67,15 @@ constexpr int S_ROW = S_Q + 32;             // [16] node id per tile row (int)
 constexpr int S_YP = S_ROW + 16;            // [2][4][128] virtual-node GEMV partials
 constexpr int S_YM = S_YP + 1024;           // [2][128]
 constexpr int S_END = S_YM + 256;
-constexpr int L_TOTAL = L_SCR + S_END;      // floats of LDS per workgroup
-// scratch, phase A: union-find parents [2][n] then a temp area at the end of the scratch
-constexpr int A_TMP = S_END - 1024;         // 1024 words: scan / reduction temps
-constexpr int LDS_MCC_CAP = A_TMP / 2;      // nodes whose MCC fits in LDS
+constexpr int L_TOTAL = L_SCR + S_END;      // floats of dynamic LDS per workgroup
+// phase A uses [L_W, L_TOTAL) (weights are reloaded afterwards)
+constexpr int A_WORDS = L_TOTAL - L_W;
+constexpr int A_TMP_WORDS = 1024;
 
-static_assert(L_SCR % 4 == 0, "scratch must be 16-byte aligned");
+static_assert(L_W % 4 == 0 && L_SCR % 4 == 0, "16-byte aligned regions");
 static_assert(sizeof(GraphVar) <= 32 * 4, "GraphVar must fit its LDS slot");
-static_assert(L_TOTAL * 4 <= 163840, "LDS budget");
+static_assert(L_TOTAL * 4 + 1024 <= 163840, "LDS budget");
+static_assert(S_END >= 64 * 128 + 128 + 4 + 256, "scratch must hold w_layer1 for the graph head");
 
 constexpr float NEG_INF = -__builtin_huge_valf();
 constexpr unsigned long long BARRIER_TIMEOUT_TICKS = 400000000ull;  // 4 s at 100 MHz
@@ -86,13 +91,12 @@ __device__ __forceinline__ f4 mfma16(float a, float b, f4 c) {
 
 // Weight element W[k][c] of a [K][64] matrix stored in B-fragment order at `base`.
 __device__ __forceinline__ float wget(const float* base, int ksteps, int k, int c) {
-  // frag[cb][s][lane]: cb = c>>4, s = k>>2, lane = (k&3)*16 + (c&15)
   return base[((c >> 4) * ksteps + (k >> 2)) * 64 + ((k & 3) << 4) + (c & 15)];
 }
 
-// torch's CPU L2 norm reduction order for a 64-wide row (verified against
-// torch.linalg.vector_norm here): 8 accumulators, element c -> accumulator c % 8 as a
-// k-ascending FMA chain, then acc0 + acc1 + ... + acc7, then sqrt.
+// torch's CPU L2 norm reduction order for a 64-wide row (checked against
+// torch.linalg.vector_norm on the build host): element c -> accumulator c % 8 as an FMA
+// chain in ascending c, then acc0 + acc1 + ... + acc7, then sqrt.
 __device__ __forceinline__ float sumsq8_finish(const float* acc8) {
   float s = acc8[0];
 #pragma unroll
@@ -109,7 +113,7 @@ __device__ __forceinline__ float wave_norm64(float x) {
   for (int i = 0; i < 8; ++i) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float v = __shfl(x, 8 * i + j, 64);
+      const float v = __shfl(x, 8 * i + j, 64);
       acc[j] = fmaf(v, v, acc[j]);
     }
   }
@@ -118,24 +122,20 @@ __device__ __forceinline__ float wave_norm64(float x) {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
 
-// ------------------------------------------------------------------ team barrier
-// Monotonic per-team counter; placement-independent agent-scope release/acquire
-// (cdna_hip_programming.md §6 Guideline 16).  Bounded spin: on timeout the error word is
-// set and every later barrier falls through so the grid drains.
-__device__ __forceinline__ void team_sync(const Params& p, unsigned* ctr, unsigned& target) {
-  if (p.team_size == 1) {
-    __syncthreads();
-    return;
-  }
+// ------------------------------------------------------------------ grid barrier
+// Monotonic counter; agent-scope release before the arrival and acquire after the wait
+// (cdna_hip_programming.md §6 Guideline 16).  Bounded spin: on timeout the error word is set
+// and every later barrier falls through, so the grid drains.
+__device__ __forceinline__ void grid_sync(const Params& p, unsigned& target) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  target += (unsigned)p.team_size;
+  target += gridDim.x;
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    __hip_atomic_fetch_add(p.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long t0 = wall_clock64();
+    while (__hip_atomic_load(p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       if (__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
       __builtin_amdgcn_s_sleep(1);
       if (wall_clock64() - t0 > BARRIER_TIMEOUT_TICKS) {
@@ -151,6 +151,9 @@ __device__ __forceinline__ void team_sync(const Params& p, unsigned* ctr, unsign
 
 __device__ __forceinline__ int load_err(const Params& p) {
   return __hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void set_err(const Params& p, int code) {
+  __hip_atomic_store(p.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------ block reductions
@@ -192,10 +195,10 @@ __device__ __forceinline__ long long block_sum_ll(long long v, long long* tmp) {
 
 // Exclusive scan over the block (thread order); returns this thread's offset, total in *tot.
 __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* tot) {
-  int lane = lane_id(), w = wave_id();
+  const int lane = lane_id(), w = wave_id();
   int x = v;
   for (int o = 1; o < 64; o <<= 1) {
-    int y = __shfl_up(x, o, 64);
+    const int y = __shfl_up(x, o, 64);
     if (lane >= o) x += y;
   }
   __syncthreads();
@@ -214,308 +217,581 @@ __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* tot) {
 // ------------------------------------------------------------------ union-find
 // Parents always point to smaller ids, so the root of a component is its minimum node id
 // (the canonical label compared across layers).  Lock-free hooking with atomicCAS.
-template <bool GLOBAL>
+template <bool GL>
 __device__ __forceinline__ int uf_load(int* par, int i) {
-  if constexpr (GLOBAL) {
+  if constexpr (GL) {
     return __hip_atomic_load(par + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
     return *((volatile int*)(par + i));
   }
 }
-template <bool GLOBAL>
+template <bool GL>
 __device__ __forceinline__ void uf_store(int* par, int i, int v) {
-  if constexpr (GLOBAL) {
+  if constexpr (GL) {
     __hip_atomic_store(par + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
     *((volatile int*)(par + i)) = v;
   }
 }
-template <bool GLOBAL>
-__device__ int uf_find(int* par, int v) {
-  int cur = uf_load<GLOBAL>(par, v);
+template <bool GL>
+__device__ __forceinline__ int uf_find(int* par, int v) {
+  int cur = uf_load<GL>(par, v);
   if (cur != v) {
     int prev = v, next;
-    while (cur > (next = uf_load<GLOBAL>(par, cur))) {
-      uf_store<GLOBAL>(par, prev, next);  // path halving; benign race (values only shrink)
+    while (cur > (next = uf_load<GL>(par, cur))) {
+      uf_store<GL>(par, prev, next);  // path halving; benign race (values only shrink)
       prev = cur;
       cur = next;
     }
   }
   return cur;
 }
-template <bool GLOBAL>
-__device__ void uf_unite(int* par, int a, int b) {
+template <bool GL>
+__device__ __forceinline__ void uf_unite(int* par, int a, int b) {
   while (true) {
-    a = uf_find<GLOBAL>(par, a);
-    b = uf_find<GLOBAL>(par, b);
+    a = uf_find<GL>(par, a);
+    b = uf_find<GL>(par, b);
     if (a == b) return;
-    if (a > b) { int t = a; a = b; b = t; }
-    int old = atomicCAS(par + b, b, a);
+    if (a > b) { const int t = a; a = b; b = t; }
+    const int old = atomicCAS(par + b, b, a);
     if (old == b) return;
   }
 }
 
-// ------------------------------------------------------------------ phase A pieces
-struct GraphCtx {
-  GraphInfo gi;
-  int g;
-};
+// Phase-A sub-step timestamps of workgroup 0 (diagnostics; step index stashed in LDS misc[60]).
+#define MD_PROF_A(slot)                                                                          \
+  do {                                                                                           \
+    if (p.prof != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {                              \
+      const int ps_ = ((volatile int*)(lds_base + L_MISC))[60];                                  \
+      if (ps_ < p.prof_cap) p.prof[(size_t)ps_ * 16 + (slot)] = wall_clock64();                  \
+    }                                                                                            \
+  } while (0)
 
-// Cover node a in both layers (U/mvc_env.py:74-85): alive incident edges become
-// "covered"; numCoveredEdges grows by their count.
-__device__ void apply_action(const Params& p, const GraphCtx& G, int a, int* tmp, int* cnt_out) {
-  const GraphInfo& gi = G.gi;
-  int c[2] = {0, 0};
-  for (int l = 0; l < 2; ++l) {
-    const int rb = p.rowptr[l][gi.roff[l] + a], re = p.rowptr[l][gi.roff[l] + a + 1];
-    for (int e = rb + (int)threadIdx.x; e < re; e += NTHREADS) {
-      int ed = p.ceid[l][gi.coff[l] + e];
-      uint8_t* st = p.estate[l] + gi.eoff[l] + ed;
-      if (*st == E_ALIVE) {
-        *st = E_COVERED;
-        c[l]++;
-      }
+// ------------------------------------------------------------------ phase A (environment)
+// Edge arrays of one graph: LDS-staged (u16 endpoints) or the global arrays themselves.
+template <bool GL>
+struct EnvView {
+  const GraphInfo* gi;
+  int e0, et;                   // edges of layer 0, both layers
+  const uint16_t* u16;          // LDS mode: endpoints [et]
+  const uint16_t* v16;
+  uint8_t* st;                  // LDS mode: edge states [et]
+  uint8_t* st_old;              // LDS mode: edge states at the start of phase A
+  const int* gu[2];             // global mode
+  const int* gv[2];
+  uint8_t* gst[2];
+  int *par0, *par1, *deg0, *deg1;
+  int* tmp;
+  uint8_t* calive[2];
+  const int* epos[2];
+
+  __device__ __forceinline__ int layer_of(int e) const { return e < e0 ? 0 : 1; }
+  __device__ __forceinline__ int local(int e) const { return e < e0 ? e : e - e0; }
+  __device__ __forceinline__ int u(int e) const {
+    if constexpr (GL) return gu[layer_of(e)][local(e)]; else return u16[e];
+  }
+  __device__ __forceinline__ int v(int e) const {
+    if constexpr (GL) return gv[layer_of(e)][local(e)]; else return v16[e];
+  }
+  __device__ __forceinline__ uint8_t state(int e) const {
+    if constexpr (GL) return gst[layer_of(e)][local(e)]; else return st[e];
+  }
+  // alive -> dead transition (the LDS mode writes back at the end of phase A)
+  __device__ __forceinline__ void kill(int e, uint8_t s) const {
+    if constexpr (GL) {
+      const int l = layer_of(e), k = local(e);
+      gst[l][k] = s;
+      calive[l][epos[l][2 * k]] = 0;
+      calive[l][epos[l][2 * k + 1]] = 0;
+    } else {
+      st[e] = s;
     }
   }
-  __syncthreads();
-  cnt_out[0] = block_sum_int(c[0], tmp);
-  cnt_out[1] = block_sum_int(c[1], tmp);
-  if (threadIdx.x == 0) p.covered[gi.node_off + a] = 1;
-  __syncthreads();
-}
+};
 
-// Mutual-LMCC fixed point (U/Mcc.py:30-38) on the alive edges.  Both layers' components
-// are found simultaneously; while the partitions differ, every alive edge of one layer
-// that crosses the other layer's partition is pruned (both layers per round).  The fixed
-// point (the coarsest partition connected in both layers) and the pruned-edge set equal
-// the reference's alternating order.  Returns LMCC size; pruned counts in pr[2].
-template <bool GLOBAL>
-__device__ int mcc_fixed_point(const Params& p, const GraphCtx& G, int* par0, int* par1, int* tmp, int* pr) {
-  const GraphInfo& gi = G.gi;
-  const int n = gi.n;
-  const int e0 = gi.e[0], e1 = gi.e[1];
-  const int* eu0 = p.eu[0] + gi.eoff[0];
-  const int* ev0 = p.ev[0] + gi.eoff[0];
-  const int* eu1 = p.eu[1] + gi.eoff[1];
-  const int* ev1 = p.ev[1] + gi.eoff[1];
-  uint8_t* st0 = p.estate[0] + gi.eoff[0];
-  uint8_t* st1 = p.estate[1] + gi.eoff[1];
+// Mutual-LMCC fixed point (U/Mcc.py:30-38) on the alive edges.  Both layers' components are
+// found simultaneously; while the partitions differ, every alive edge of a layer that crosses
+// the other layer's partition is pruned (both layers per round).  The fixed point (the
+// coarsest partition connected in both layers) and the pruned-edge set equal the reference's
+// alternating order.  Returns the LMCC size (over non-covered nodes); pruned counts in pr[2].
+template <bool GL>
+__device__ int mcc_fixed_point(const EnvView<GL>& E, const uint8_t* cov, int* pr) {
+  const int n = E.gi->n;
   int pruned0 = 0, pruned1 = 0;
   while (true) {
-    for (int v = threadIdx.x; v < n; v += NTHREADS) {
-      uf_store<GLOBAL>(par0, v, v);
-      uf_store<GLOBAL>(par1, v, v);
+    for (int x = threadIdx.x; x < n; x += NTHREADS) {
+      uf_store<GL>(E.par0, x, x);
+      uf_store<GL>(E.par1, x, x);
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < e0 + e1; e += NTHREADS) {
-      if (e < e0) {
-        if (st0[e] == E_ALIVE) uf_unite<GLOBAL>(par0, eu0[e], ev0[e]);
-      } else {
-        int f = e - e0;
-        if (st1[f] == E_ALIVE) uf_unite<GLOBAL>(par1, eu1[f], ev1[f]);
-      }
-    }
+    for (int e = threadIdx.x; e < E.et; e += NTHREADS)
+      if (E.state(e) == E_ALIVE) uf_unite<GL>(e < E.e0 ? E.par0 : E.par1, E.u(e), E.v(e));
     __syncthreads();
     int diff = 0;
-    for (int v = threadIdx.x; v < n; v += NTHREADS) {
-      int r0 = uf_find<GLOBAL>(par0, v);
-      int r1 = uf_find<GLOBAL>(par1, v);
-      uf_store<GLOBAL>(par0, v, r0);
-      uf_store<GLOBAL>(par1, v, r1);
+    for (int x = threadIdx.x; x < n; x += NTHREADS) {
+      const int r0 = uf_find<GL>(E.par0, x), r1 = uf_find<GL>(E.par1, x);
+      uf_store<GL>(E.par0, x, r0);
+      uf_store<GL>(E.par1, x, r1);
       diff |= (r0 != r1);
     }
-    if (GLOBAL) __threadfence_block();
     diff = __syncthreads_or(diff);
     if (!diff) break;
-    // roots are final (every node points at its root) -> labels; prune crossing edges
     int c0 = 0, c1 = 0;
-    for (int e = threadIdx.x; e < e0 + e1; e += NTHREADS) {
-      if (e < e0) {
-        if (st0[e] == E_ALIVE && uf_load<GLOBAL>(par1, eu0[e]) != uf_load<GLOBAL>(par1, ev0[e])) {
-          st0[e] = E_PRUNED;
-          c0++;
-        }
-      } else {
-        int f = e - e0;
-        if (st1[f] == E_ALIVE && uf_load<GLOBAL>(par0, eu1[f]) != uf_load<GLOBAL>(par0, ev1[f])) {
-          st1[f] = E_PRUNED;
-          c1++;
-        }
+    for (int e = threadIdx.x; e < E.et; e += NTHREADS) {
+      if (E.state(e) != E_ALIVE) continue;
+      int* other = e < E.e0 ? E.par1 : E.par0;  // layer-0 edges are pruned by layer-1 components
+      if (uf_load<GL>(other, E.u(e)) != uf_load<GL>(other, E.v(e))) {
+        E.kill(e, E_PRUNED);
+        if (e < E.e0) c0++; else c1++;
       }
     }
-    pruned0 += block_sum_int(c0, tmp);
-    pruned1 += block_sum_int(c1, tmp);
+    pruned0 += block_sum_int(c0, E.tmp);
+    pruned1 += block_sum_int(c1, E.tmp);
   }
   pr[0] = pruned0;
   pr[1] = pruned1;
-  // component sizes over non-covered nodes (covered nodes are not in the reference graphs)
-  for (int v = threadIdx.x; v < n; v += NTHREADS) uf_store<GLOBAL>(par1, v, 0);
-  if (GLOBAL) __threadfence_block();
+  for (int x = threadIdx.x; x < n; x += NTHREADS) uf_store<GL>(E.par1, x, 0);
   __syncthreads();
-  const uint8_t* cov = p.covered + gi.node_off;
-  for (int v = threadIdx.x; v < n; v += NTHREADS)
-    if (!cov[v]) atomicAdd(par1 + uf_load<GLOBAL>(par0, v), 1);
-  if (GLOBAL) __threadfence_block();
+  for (int x = threadIdx.x; x < n; x += NTHREADS)
+    if (!cov[x]) atomicAdd(E.par1 + uf_load<GL>(E.par0, x), 1);
   __syncthreads();
   int best = 0;
-  for (int v = threadIdx.x; v < n; v += NTHREADS) best = max(best, uf_load<GLOBAL>(par1, v));
-  return block_max_int(best, tmp);
+  for (int x = threadIdx.x; x < n; x += NTHREADS) best = max(best, uf_load<GL>(E.par1, x));
+  return block_max_int(best, E.tmp);
 }
 
-// Residual degrees, ascending live list, per-layer aggregates, first-layer table.
-// Returns 0 on success, an ERR_* code otherwise.
-__device__ int compute_features(const Params& p, const GraphCtx& G, GraphVar& gv, float* lds, int* tmp) {
-  const GraphInfo& gi = G.gi;
-  const int n = gi.n;
+// Everything phase A does for one graph once the actions to apply are known.
+// Returns 0 or an ERR_* code.
+template <bool GL>
+__device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, float* area, int pend_n,
+                        int pend_first, const float* lds_base) {
+  const int n = gi.n, e0 = gi.e[0], e1 = gi.e[1], et = e0 + e1;
+  EnvView<GL> E;
+  E.gi = &gi;
+  E.e0 = e0;
+  E.et = et;
+  for (int l = 0; l < 2; ++l) {
+    E.gu[l] = p.eu[l] + gi.eoff[l];
+    E.gv[l] = p.ev[l] + gi.eoff[l];
+    E.gst[l] = p.estate[l] + gi.eoff[l];
+    E.calive[l] = p.calive[l] + gi.coff[l];
+    E.epos[l] = p.epos[l] + 2 * (size_t)gi.eoff[l];
+  }
+  int* ia = (int*)area;
+  if constexpr (GL) {
+    int* gs = p.gscr + 4 * (size_t)gi.node_off;
+    E.par0 = gs;
+    E.par1 = gs + n;
+    E.deg0 = gs + 2 * n;
+    E.deg1 = gs + 3 * n;
+    E.tmp = ia;
+  } else {
+    E.par0 = ia;
+    E.par1 = ia + n;
+    E.deg0 = ia + 2 * n;
+    E.deg1 = ia + 3 * n;
+    E.tmp = ia + 4 * n;
+    uint16_t* u16 = (uint16_t*)(ia + 4 * n + A_TMP_WORDS);
+    uint16_t* v16 = u16 + ((et + 7) & ~7);
+    uint8_t* st = (uint8_t*)(v16 + ((et + 7) & ~7));
+    uint8_t* st_old = st + ((et + 15) & ~15);
+    E.u16 = u16;
+    E.v16 = v16;
+    E.st = st;
+    E.st_old = st_old;
+    // batched so every thread keeps 8 independent loads in flight
+    for (int e0b = 0; e0b < et; e0b += 8 * NTHREADS) {
+      int uu[8], vv[8];
+      uint8_t ss[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = e0b + k * NTHREADS + threadIdx.x;
+        if (e < et) {
+          const int l = e < e0 ? 0 : 1, kk = e < e0 ? e : e - e0;
+          uu[k] = E.gu[l][kk];
+          vv[k] = E.gv[l][kk];
+          ss[k] = E.gst[l][kk];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = e0b + k * NTHREADS + threadIdx.x;
+        if (e < et) {
+          u16[e] = (uint16_t)uu[k];
+          v16[e] = (uint16_t)vv[k];
+          st[e] = ss[k];
+          st_old[e] = ss[k];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  MD_PROF_A(1);
+  uint8_t* cov = p.covered + gi.node_off;
+  int err = 0;
+  for (int k = 0; k < pend_n; ++k) {
+    if (gv.alive[0] == 0 || gv.alive[1] == 0) break;  // terminal between queued actions
+    const int a = k == 0 && pend_first >= 0 ? pend_first : p.pend[gi.node_off + k];
+    if (a < 0 || a >= n) { err = ERR_BADNODE; break; }
+    if (cov[a]) { err = ERR_COVERED; break; }
+    // cover a in both layers (U/mvc_env.py:74-85): its alive edges become "covered"
+    int c0 = 0, c1 = 0;
+    for (int e = threadIdx.x; e < et; e += NTHREADS) {
+      if (E.state(e) == E_ALIVE && (E.u(e) == a || E.v(e) == a)) {
+        E.kill(e, E_COVERED);
+        if (e < e0) c0++; else c1++;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) cov[a] = 1;
+    c0 = block_sum_int(c0, E.tmp);
+    c1 = block_sum_int(c1, E.tmp);
+    __syncthreads();
+    int pr[2];
+    const int lm = mcc_fixed_point<GL>(E, cov, pr);
+    if (threadIdx.x == 0) {
+      gv.counter[0] += c0;
+      gv.counter[1] += c1;
+      gv.removed[0] += pr[0];
+      gv.removed[1] += pr[1];
+      gv.alive[0] -= c0 + pr[0];
+      gv.alive[1] -= c1 + pr[1];
+      gv.n_cov += 1;
+      gv.lmcc = lm;
+      p.tr_action[gi.node_off + gv.steps] = a;
+      p.tr_rank[gi.node_off + gv.steps] = lm;
+      gv.steps += 1;
+    }
+    __syncthreads();
+  }
+  if (!gv.s0_done && !err) {
+    int pr[2];
+    const int lm = mcc_fixed_point<GL>(E, cov, pr);
+    if (threadIdx.x == 0) {
+      gv.removed[0] += pr[0];
+      gv.removed[1] += pr[1];
+      gv.max_rank = lm;
+      gv.lmcc = lm;
+      gv.s0_done = 1;
+    }
+  }
+  MD_PROF_A(2);
+  // residual degrees by edge-parallel atomics
+  for (int x = threadIdx.x; x < n; x += NTHREADS) {
+    uf_store<GL>(E.deg0, x, 0);
+    uf_store<GL>(E.deg1, x, 0);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < et; e += NTHREADS) {
+    if (E.state(e) != E_ALIVE) continue;
+    int* d = e < e0 ? E.deg0 : E.deg1;
+    atomicAdd(d + E.u(e), 1);
+    atomicAdd(d + E.v(e), 1);
+  }
+  __syncthreads();
+  // live list (ascending ids), per-layer aggregates (U/PrepareBatchGraph.py:35-74)
   const int chunk = (n + NTHREADS - 1) / NTHREADS;
-  const int v0 = min(n, (int)threadIdx.x * chunk), v1 = min(n, v0 + chunk);
-  int nlive = 0, dmax0 = 0, dmax1 = 0, sd0 = 0, sd1 = 0, bad = 0;
+  const int x0 = min(n, (int)threadIdx.x * chunk), x1 = min(n, x0 + chunk);
+  int nlive = 0, dm0 = 0, dm1 = 0, sd0 = 0, sd1 = 0, bad = 0;
   long long th0 = 0, th1 = 0;
   float* q = p.q + gi.node_off;
-  for (int v = v0; v < v1; ++v) {
-    int d[2];
-    for (int l = 0; l < 2; ++l) {
-      const int rb = p.rowptr[l][gi.roff[l] + v], re = p.rowptr[l][gi.roff[l] + v + 1];
-      const int* ce = p.ceid[l] + gi.coff[l];
-      const uint8_t* st = p.estate[l] + gi.eoff[l];
-      int c = 0;
-      for (int e = rb; e < re; ++e) c += (st[ce[e]] == E_ALIVE);
-      d[l] = c;
-      p.deg[l][gi.node_off + v] = c;
-    }
-    bad |= ((d[0] > 0) != (d[1] > 0));
-    if (d[0] > 0) {
+  int* gdeg0 = p.deg[0] + gi.node_off;
+  int* gdeg1 = p.deg[1] + gi.node_off;
+  for (int x = x0; x < x1; ++x) {
+    const int d0 = uf_load<GL>(E.deg0, x), d1 = uf_load<GL>(E.deg1, x);
+    gdeg0[x] = d0;
+    gdeg1[x] = d1;
+    q[x] = NEG_INF;
+    bad |= ((d0 > 0) != (d1 > 0));
+    if (d0 > 0) {
       nlive++;
-      dmax0 = max(dmax0, d[0]);
-      dmax1 = max(dmax1, d[1]);
-      th0 += (long long)d[0] * (d[0] - 1) / 2;
-      th1 += (long long)d[1] * (d[1] - 1) / 2;
+      dm0 = max(dm0, d0);
+      dm1 = max(dm1, d1);
+      th0 += (long long)d0 * (d0 - 1) / 2;
+      th1 += (long long)d1 * (d1 - 1) / 2;
     }
-    sd0 += d[0];
-    sd1 += d[1];
-    q[v] = NEG_INF;
+    sd0 += d0;
+    sd1 += d1;
   }
   int tot = 0;
-  int base = block_excl_scan(nlive, tmp, &tot);
+  const int base = block_excl_scan(nlive, E.tmp, &tot);
   {
     int k = base;
     int* lv = p.live + gi.node_off;
-    for (int v = v0; v < v1; ++v)
-      if (p.deg[0][gi.node_off + v] > 0) lv[k++] = v;
+    for (int x = x0; x < x1; ++x)
+      if (uf_load<GL>(E.deg0, x) > 0) lv[k++] = x;
   }
-  int dm0 = block_max_int(dmax0, tmp);
-  int dm1 = block_max_int(dmax1, tmp);
-  int a0 = block_sum_int(sd0, tmp) / 2;
-  int a1 = block_sum_int(sd1, tmp) / 2;
-  long long t0 = block_sum_ll(th0, (long long*)tmp);
-  long long t1 = block_sum_ll(th1, (long long*)tmp);
+  dm0 = block_max_int(dm0, E.tmp);
+  dm1 = block_max_int(dm1, E.tmp);
+  sd0 = block_sum_int(sd0, E.tmp);
+  sd1 = block_sum_int(sd1, E.tmp);
+  th0 = block_sum_ll(th0, (long long*)E.tmp);
+  th1 = block_sum_ll(th1, (long long*)E.tmp);
   bad = __syncthreads_or(bad);
-  gv.n_live = tot;
-  gv.dmax[0] = dm0;
-  gv.dmax[1] = dm1;
-  gv.alive[0] = a0;
-  gv.alive[1] = a1;
-  gv.twohop[0] = t0;
-  gv.twohop[1] = t1;
-  if (bad) return ERR_LIVE_MISMATCH;
-  // First-layer embedding by degree (unit cost): X = [d/dmax, d/dmax] (net :252-261),
-  // normalize(relu(X . w_n2l)) with the 2-term FMA chain of MKL's sgemm.
-  if (p.node_w == nullptr) {
-    const float* wn = lds + L_WN;
-    const int lane = lane_id();
-    for (int l = 0; l < 2; ++l) {
-      const int dm = l ? dm1 : dm0;
-      // degrees are <= n-1, so the table of graph g fits rows [node_off, node_off + n)
-      float* tab = p.h0tab[l] + (size_t)gi.node_off * EMB;
-      for (int d = 1 + wave_id(); d <= dm; d += NTHREADS / 64) {
-        float f = (float)d / (float)dm;
-        float x = fmaf(f, wn[64 + lane], fmaf(f, wn[lane], 0.f));
-        x = fmaxf(x, 0.f);
-        float nr = wave_norm64(x);
-        tab[(size_t)d * EMB + lane] = x / fmaxf(nr, 1e-12f);
+  if (bad && !err) err = ERR_LIVE_MISMATCH;
+  if (threadIdx.x == 0) {
+    gv.n_live = tot;
+    gv.dmax[0] = dm0;
+    gv.dmax[1] = dm1;
+    gv.alive[0] = sd0 / 2;
+    gv.alive[1] = sd1 / 2;
+    gv.twohop[0] = th0;
+    gv.twohop[1] = th1;
+  }
+  if constexpr (!GL) {
+    // write back edge states; dead edges drop out of the gather's CSR view
+    for (int e = threadIdx.x; e < et; e += NTHREADS) {
+      const int l = e < e0 ? 0 : 1, k = e < e0 ? e : e - e0;
+      const uint8_t s = E.st[e];
+      if (s != E.st_old[e]) {
+        E.gst[l][k] = s;
+        E.calive[l][E.epos[l][2 * k]] = 0;
+        E.calive[l][E.epos[l][2 * k + 1]] = 0;
       }
     }
   }
-  return 0;
+  __syncthreads();
+  MD_PROF_A(14);
+  // First-layer embedding by degree (unit cost): X = [d/dmax, d/dmax] (net :252-261),
+  // normalize(relu(X . w_n2l)) with the 2-term FMA chain of MKL's sgemm; rows d = 1..dmax,
+  // 64 rows at a time in LDS.
+  if (p.node_w == nullptr) {
+    float* xs = area;             // [64][65]
+    float* red = area + 64 * 65;  // [64][8]
+    const float* wn = p.w + W_N2L;
+    const int c = threadIdx.x & 63, r8 = threadIdx.x >> 6;
+    const float w0 = wn[c], w1 = wn[64 + c];
+    for (int l = 0; l < 2; ++l) {
+      const int dm = l ? dm1 : dm0;
+      float* tab = p.h0tab[l] + (size_t)gi.node_off * EMB;  // degrees <= n-1 fit the graph's rows
+      for (int d0 = 1; d0 <= dm; d0 += 64) {
+        for (int r = r8; r < 64; r += NTHREADS / 64) {
+          const int d = d0 + r;
+          float x = 0.f;
+          if (d <= dm) {
+            const float f = (float)d / (float)dm;
+            x = fmaxf(fmaf(f, w1, fmaf(f, w0, 0.f)), 0.f);
+          }
+          xs[r * 65 + c] = x;
+        }
+        __syncthreads();
+        {
+          const int r = threadIdx.x >> 3, j = threadIdx.x & 7;
+          float acc = 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float v = xs[r * 65 + 8 * i + j];
+            acc = fmaf(v, v, acc);
+          }
+          red[r * 8 + j] = acc;
+        }
+        __syncthreads();
+        for (int r = r8; r < 64; r += NTHREADS / 64) {
+          const int d = d0 + r;
+          if (d > dm) break;
+          const float den = fmaxf(sqrtf(sumsq8_finish(red + r * 8)), 1e-12f);
+          tab[(size_t)d * EMB + c] = xs[r * 65 + c] / den;
+        }
+        __syncthreads();
+      }
+    }
+  }
+  MD_PROF_A(15);
+  return err;
 }
 
-// ------------------------------------------------------------------ GEMM tile pieces
-// Gather for one tile: waves 0-3 layer 0, 4-7 layer 1; wave handles rows 4*(w&3)..+3.
-// it == 1: previous embedding = first-layer table (unit cost) or static per-node input.
-__device__ void gather_tile(const Params& p, const GraphInfo& gi, int it, const int* rows, float* scr) {
+// Must agree with the staging layout of env_step<false>: par/deg 4n words, temp, u16/v16
+// endpoints, edge states and their phase-start copy.
+__host__ __device__ inline bool phase_a_fits_lds(int n, int et) {
+  const size_t bytes = 4 * (4 * (size_t)n + A_TMP_WORDS) + (size_t)((et + 7) & ~7) * 4 + 2 * (size_t)((et + 15) & ~15) + 64;
+  return bytes <= 4 * (size_t)A_WORDS && n <= 65535;
+}
+
+// Phase A of one graph: reduce the previous prediction, then apply / MCC / features.
+__device__ __noinline__ void phase_a(const Params& p, int g, bool have_q, float* lds) {
+  GraphVar& gv = *(GraphVar*)(lds + L_GV);
+  int* misc = (int*)(lds + L_MISC);
+  const GraphInfo gi = p.ginfo[g];
+  if (threadIdx.x == 0) gv = p.gvar[g];
+  __syncthreads();
+  if (gv.status != ST_RUN) return;
+  int pend_n = 0, pend_first = -1;
+  bool stop = false;
+  if (have_q) {
+    if (threadIdx.x == 0) {
+      // arg-max over the graph's tile partials, in tile order
+      float bm = NEG_INF, bs = NEG_INF;
+      int bi = 0x7fffffff, bc = 0;
+      const int nt = (gv.n_live + TILE - 1) / TILE;
+      for (int j = 0; j < nt; ++j) {
+        const float* ap = p.apart + (size_t)(gi.tile_off + j) * 4;
+        const float m = ap[0], s = ap[1];
+        const int i = __float_as_int(ap[2]), c = __float_as_int(ap[3]);
+        if (c == 0) continue;
+        if (m > bm) {
+          bs = fmaxf(bm, s);
+          bm = m;
+          bi = i;
+          bc = c;
+        } else if (m == bm) {
+          bc += c;
+          bi = min(bi, i);
+          bs = fmaxf(bs, s);
+        } else {
+          bs = fmaxf(bs, m);
+        }
+      }
+      const int t = gv.npred;
+      if (t < gi.n) {
+        int* ts = p.tr_stat + (size_t)(gi.node_off + t) * 4;
+        ts[0] = gv.n_live;
+        ts[1] = gv.alive[0];
+        ts[2] = gv.alive[1];
+        ts[3] = bc;
+        p.tr_q[(size_t)(gi.node_off + t) * 2 + 0] = bm;
+        p.tr_q[(size_t)(gi.node_off + t) * 2 + 1] = bm - bs;
+      }
+      gv.npred = t + 1;
+      gv.ntie = bc;
+      gv.qmax = bm;
+      gv.gap = bm - bs;
+      gv.argmax = bc == 1 ? bi : -1;
+      misc[1] = bi;
+      misc[2] = bc;
+    }
+    __syncthreads();
+    if (p.run_mode == RUN_PREDICT) {
+      if (threadIdx.x == 0) gv.status = ST_PAUSED;
+      stop = true;
+    } else if (p.host_select || misc[2] != 1) {
+      if (threadIdx.x == 0) gv.status = ST_NEED_HOST;
+      stop = true;
+    } else {
+      pend_n = 1;
+      pend_first = misc[1];
+    }
+  } else {
+    pend_n = gv.npend;
+  }
+  __syncthreads();
+  if (!stop) {
+    const int et = gi.e[0] + gi.e[1];
+    const bool fits = phase_a_fits_lds(gi.n, et);
+    float* area = lds + L_W;
+    const int err = fits ? env_step<false>(p, gi, gv, area, pend_n, pend_first, lds)
+                         : env_step<true>(p, gi, gv, area, pend_n, pend_first, lds);
+    if (threadIdx.x == 0) {
+      gv.npend = 0;
+      if (err) set_err(p, err);
+      const bool term = gv.alive[0] == 0 || gv.alive[1] == 0;
+      if (term) gv.status = ST_TERMINAL;
+      else if (p.run_mode == RUN_STEP) gv.status = ST_PAUSED;
+      else gv.status = ST_RUN;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) p.gvar[g] = gv;
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------ tile pieces
+// Gather for one tile: waves 0-3 layer 0, 4-7 layer 1; each wave handles rows 4*(w&3)..+3
+// concurrently, one 16-lane group per row, every lane owning 4 features (float4 loads).
+// it == 1: previous embedding = first-layer table (by degree, unit cost) or static input.
+__device__ __noinline__ void gather_tile(const Params& p, const GraphInfo& gi, int it, const int* rows, float* scr) {
   const int w = wave_id(), l = w >> 2, lane = lane_id();
+  const int grp = lane >> 4, qd = lane & 15;
   const int* rp = p.rowptr[l] + gi.roff[l];
   const int* adj = p.adj[l] + gi.coff[l];
-  const int* ce = p.ceid[l] + gi.coff[l];
-  const uint8_t* st = p.estate[l] + gi.eoff[l];
+  const uint8_t* ca = p.calive[l] + gi.coff[l];
   const int* deg = p.deg[l] + gi.node_off;
   const float* hp;
   bool table = false;
   if (it == 1) {
-    // unit cost: table indexed by residual degree; degree cost: static per-node input
     hp = p.h0tab[l] + (size_t)gi.node_off * EMB;
     table = p.node_w == nullptr;
   } else {
     hp = p.H[l][(it - 2) & 1] + (size_t)gi.node_off * EMB;
   }
-  float* atp = scr + S_P + l * 64 * LDT;
-  float* atx = scr + S_X + l * 64 * LDT;
-  for (int rr = 0; rr < 4; ++rr) {
-    const int r = 4 * (w & 3) + rr;
-    const int v = rows[r];
-    float own = 0.f, acc = 0.f;
-    if (v >= 0) {
-      const int ov = table ? deg[v] : v;
-      own = hp[(size_t)ov * EMB + lane];
-      const int rb = rp[v], re = rp[v + 1];
-      for (int e0 = rb; e0 < re; e0 += 64) {
-        const int e = e0 + lane;
-        int nb = -1;
-        if (e < re && st[ce[e]] == E_ALIVE) nb = adj[e];
-        if (table && nb >= 0) nb = deg[nb];
-        unsigned long long m = __ballot(nb >= 0);
-        // sum the alive neighbours in CSR order (== reference in_edges order)
-        while (m) {
-          int b0 = __builtin_ctzll(m);
-          m &= m - 1;
-          int j0 = __shfl(nb, b0, 64);
-          int b1 = -1, j1 = -1, b2 = -1, j2 = -1, b3 = -1, j3 = -1;
-          if (m) { b1 = __builtin_ctzll(m); m &= m - 1; j1 = __shfl(nb, b1, 64); }
-          if (m) { b2 = __builtin_ctzll(m); m &= m - 1; j2 = __shfl(nb, b2, 64); }
-          if (m) { b3 = __builtin_ctzll(m); m &= m - 1; j3 = __shfl(nb, b3, 64); }
-          float x0 = hp[(size_t)j0 * EMB + lane];
-          float x1 = j1 >= 0 ? hp[(size_t)j1 * EMB + lane] : 0.f;
-          float x2 = j2 >= 0 ? hp[(size_t)j2 * EMB + lane] : 0.f;
-          float x3 = j3 >= 0 ? hp[(size_t)j3 * EMB + lane] : 0.f;
-          acc = acc + x0;
-          if (j1 >= 0) acc = acc + x1;
-          if (j2 >= 0) acc = acc + x2;
-          if (j3 >= 0) acc = acc + x3;
+  const float4* hp4 = (const float4*)hp;
+  const int r = 4 * (w & 3) + grp;
+  const int v = rows[r];
+  int rb = 0, re = 0;
+  float4 own = {0.f, 0.f, 0.f, 0.f}, acc = {0.f, 0.f, 0.f, 0.f};
+  if (v >= 0) {
+    rb = rp[v];
+    re = rp[v + 1];
+    const int ov = table ? deg[v] : v;
+    own = hp4[(size_t)ov * 16 + qd];
+  }
+  int nch = (re - rb + 15) >> 4;
+  nch = max(nch, __shfl_xor(nch, 16, 64));
+  nch = max(nch, __shfl_xor(nch, 32, 64));
+  for (int ch = 0; ch < nch; ++ch) {
+    const int e = rb + 16 * ch + qd;
+    int nb = -1;
+    if (e < re && ca[e]) nb = adj[e];
+    if (table && nb >= 0) nb = deg[nb];
+    const unsigned long long m = __ballot(nb >= 0);
+    unsigned gm = (unsigned)(m >> (16 * grp)) & 0xFFFFu;
+    // the alive neighbours in CSR order (== reference in_edges order), 4 rows x 4 loads in flight
+    while (__any(gm != 0)) {
+      int j[4] = {-1, -1, -1, -1};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (gm) {
+          const int b = __builtin_ctz(gm);
+          gm &= gm - 1;
+          j[k] = b;
+        }
+      }
+      int src[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) src[k] = __shfl(nb, 16 * grp + (j[k] < 0 ? 0 : j[k]), 64);
+      float4 x[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) x[k] = j[k] >= 0 ? hp4[(size_t)src[k] * 16 + qd] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (j[k] >= 0) {
+          acc.x = acc.x + x[k].x;
+          acc.y = acc.y + x[k].y;
+          acc.z = acc.z + x[k].z;
+          acc.w = acc.w + x[k].w;
         }
       }
     }
-    atp[lane * LDT + r] = acc;
-    atx[lane * LDT + r] = own;
   }
+  float* atp = scr + S_P + l * 64 * LDT;
+  float* atx = scr + S_X + l * 64 * LDT;
+  const int c = 4 * qd;
+  atp[(c + 0) * LDT + r] = acc.x;
+  atp[(c + 1) * LDT + r] = acc.y;
+  atp[(c + 2) * LDT + r] = acc.z;
+  atp[(c + 3) * LDT + r] = acc.w;
+  atx[(c + 0) * LDT + r] = own.x;
+  atx[(c + 1) * LDT + r] = own.y;
+  atx[(c + 2) * LDT + r] = own.z;
+  atx[(c + 3) * LDT + r] = own.w;
 }
 
-// Node update for one tile: H' = normalize(relu([P.P1 | X.P2] . P3)), written to S_E.
-__device__ void update_tile(const float* lds, float* scr) {
+// Node update for one tile: H' = relu([P.P1 | X.P2] . P3) into S_E (normalised separately).
+__device__ __noinline__ void update_tile(const float* wi, float* scr) {
   const int w = wave_id(), l = w >> 2, cb = w & 3, lane = lane_id();
   const int ar = lane & 15, ak = lane >> 4;
   const float* atp = scr + S_P + l * 64 * LDT;
   const float* atx = scr + S_X + l * 64 * LDT;
   float* atm = scr + S_M + l * 128 * LDT;
-  const float* p1 = lds + L_P1 + cb * 16 * 64;
-  const float* p2 = lds + L_P2 + cb * 16 * 64;
-  const float* p3 = lds + L_P3 + cb * 32 * 64;
+  const float* p1 = wi + W_IP1 + cb * 16 * 64;
+  const float* p2 = wi + W_IP2 + cb * 16 * 64;
+  const float* p3 = wi + W_IP3 + cb * 32 * 64;
   f4 a1 = {0.f, 0.f, 0.f, 0.f}, a2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
   for (int s = 0; s < 16; ++s) {
     a1 = mfma16(atp[(4 * s + ak) * LDT + ar], p1[s * 64 + lane], a1);
     a2 = mfma16(atx[(4 * s + ak) * LDT + ar], p2[s * 64 + lane], a2);
   }
-  const int col = 16 * cb + ar;  // output column held by this lane
+  const int col = 16 * cb + ar;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     atm[col * LDT + 4 * ak + r] = a1[r];
@@ -531,7 +807,7 @@ __device__ void update_tile(const float* lds, float* scr) {
 }
 
 // Row-normalise the [2][64][16] transposed tile at `at` in place (torch reduction order).
-__device__ void normalize_tile(float* at, float* scr) {
+__device__ __noinline__ void normalize_tile(float* at, float* scr) {
   float* red = scr + S_RED;
   const int t = threadIdx.x;
   if (t < 256) {
@@ -540,7 +816,7 @@ __device__ void normalize_tile(float* at, float* scr) {
     float acc = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      float v = a[(8 * i + j) * LDT + row];
+      const float v = a[(8 * i + j) * LDT + row];
       acc = fmaf(v, v, acc);
     }
     red[(l * 16 + row) * 8 + j] = acc;
@@ -558,18 +834,32 @@ __device__ void normalize_tile(float* at, float* scr) {
 }
 
 // ------------------------------------------------------------------ virtual node (1 row)
-// out[c] = sum_k in[k] W[k][c] for a [K][64] B-fragment weight, computed by the 4 waves of
-// the layer group as 4 partial FMA chains over K/4 each, summed in order.
-__device__ void vrow_gemv(const float* in, const float* wf, int K, float* part /*[4][64]*/) {
-  const int w = wave_id(), q = w & 3, lane = lane_id();
-  const int ks = K / 4, k0 = q * ks;
-  float acc = 0.f;
-  for (int k = k0; k < k0 + ks; ++k) acc = fmaf(in[k], wget(wf, K / 4, k, lane), acc);
-  part[q * 64 + lane] = acc;
+// Sum of one graph's per-tile partial sums (slot) -> out[2][64]: four threads per output each
+// add a contiguous quarter of the tiles in order, then the quarters are added in order
+// (a fixed order, identical in every workgroup).
+__device__ void graph_sum(const Params& p, const GraphInfo& gi, int nt, int slot, float* out, float* tmp4) {
+  const int o = threadIdx.x & 127, qt = threadIdx.x >> 7;
+  const int per = (nt + 3) >> 2;
+  const int j0 = min(nt, qt * per), j1 = min(nt, j0 + per);
+  const float* sp = p.spart + (size_t)gi.tile_off * 384 + slot * 128 + o;
+  float a = 0.f;
+  for (int jb = j0; jb < j1; jb += 16) {
+    float x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = jb + k < j1 ? sp[(size_t)(jb + k) * 384] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (jb + k < j1) a = a + x[k];
+  }
+  tmp4[qt * 128 + o] = a;
+  __syncthreads();
+  if (threadIdx.x < 128) out[o] = ((tmp4[o] + tmp4[128 + o]) + tmp4[256 + o]) + tmp4[384 + o];
+  __syncthreads();
 }
 
-// One virtual-node iteration for both layers: y' = normalize(relu([s.P1 | y.P2] . P3)).
-__device__ void vrow_update(const float* lds, float* scr, const float* s /*[2][64]*/, float* y /*[2][64]*/) {
+// One virtual-node iteration for both layers: y' = normalize(relu([s.P1 | y.P2] . P3)),
+// computed by the 4 waves of each layer group as 4 partial chains summed in order.
+__device__ __noinline__ void vrow_update(const float* wi, float* scr, const float* s /*[2][64]*/, float* y /*[2][64]*/) {
   const int w = wave_id(), l = w >> 2, q = w & 3, lane = lane_id();
   float* yp = scr + S_YP + l * 512;
   float* ym = scr + S_YM + l * 128;
@@ -577,8 +867,8 @@ __device__ void vrow_update(const float* lds, float* scr, const float* s /*[2][6
     const int k0 = q * 16;
     float a1 = 0.f, a2 = 0.f;
     for (int k = k0; k < k0 + 16; ++k) {
-      a1 = fmaf(s[l * 64 + k], wget(lds + L_P1, 16, k, lane), a1);
-      a2 = fmaf(y[l * 64 + k], wget(lds + L_P2, 16, k, lane), a2);
+      a1 = fmaf(s[l * 64 + k], wget(wi + W_IP1, 16, k, lane), a1);
+      a2 = fmaf(y[l * 64 + k], wget(wi + W_IP2, 16, k, lane), a2);
     }
     yp[q * 128 + lane] = a1;
     yp[q * 128 + 64 + lane] = a2;
@@ -592,21 +882,21 @@ __device__ void vrow_update(const float* lds, float* scr, const float* s /*[2][6
   {
     const int k0 = q * 32;
     float a = 0.f;
-    for (int k = k0; k < k0 + 32; ++k) a = fmaf(ym[k], wget(lds + L_P3, 32, k, lane), a);
+    for (int k = k0; k < k0 + 32; ++k) a = fmaf(ym[k], wget(wi + W_IP3, 32, k, lane), a);
     yp[q * 128 + lane] = a;
   }
   __syncthreads();
   if (q == 0) {
     float o = ((yp[lane] + yp[128 + lane]) + yp[256 + lane]) + yp[384 + lane];
     o = fmaxf(o, 0.f);
-    float nr = wave_norm64(o);
+    const float nr = wave_norm64(o);
     y[l * 64 + lane] = o / fmaxf(nr, 1e-12f);
   }
   __syncthreads();
 }
 
 // Attention gate of one row (U/MRGNN/mutil_layer_weight.py:266-285, LogisticVector :304-313):
-// weight of the OTHER layer for target layer l, from dots d00=F0.F0.lw, d11, d01.
+// weight of the OTHER layer for target layer l, from dots d00 = F0F0.lw, d11, d01.
 __device__ __forceinline__ float other_gate(int l, float d00, float d11, float d01, float lb) {
   float a0, a1;
   if (l == 0) {
@@ -622,52 +912,55 @@ __device__ __forceinline__ float other_gate(int l, float d00, float d11, float d
   return l == 0 ? e1 * inv : e0 * inv;
 }
 
-// Graph rows: y_l from the final virtual-node embeddings E_l = Y3_l (both layers),
-// then the layer-mix weights softmax(relu(y_l.WL1).WL2) and the aux dot per layer.
-__device__ void graph_head(const Params& p, float* lds, float* scr, const GraphInfo& gi, const GraphVar& gv) {
+// Graph rows: y_l from the final virtual-node embeddings E_l = Y3_l (in L_YW), the layer-mix
+// weights softmax(relu(y_l.WL1).WL2) and the aux features (U/PrepareBatchGraph.py:92-101).
+__device__ __noinline__ void graph_head(const Params& p, float* lds, float* scr, const GraphInfo& gi,
+                                        const GraphVar& gv) {
   const int w = wave_id(), l = w >> 2, q = w & 3, lane = lane_id();
+  const float* wi = lds + L_W;
   float* gs = lds + L_GS;
   float* ys = lds + L_YS;
-  const float* y = lds + L_Y;
-  float* f = scr + S_YM;  // [2][64] tanh features
-  float* dots = scr + S_YP;  // [4]
+  const float* y = lds + L_YW;
+  float* wl1 = scr;                 // [64][128] staged w_layer1
+  float* f = scr + 64 * 128;        // [2][64] tanh features
+  float* dots = f + 128;            // [4]
+  float* zh = dots + 4;             // [2][128]
+  for (int i = threadIdx.x; i < 64 * 128 / 4; i += NTHREADS)
+    ((float4*)wl1)[i] = ((const float4*)(p.w + W_WL1))[i];
   if (q == 0) {
-    // F = tanh(E.T + b): graph row is part of the reference's [n+1,64] sgemm -> FMA chain
+    // F = tanh(E.T + b): the graph row is part of the reference's [n+1, 64] sgemm -> FMA chain
     float a = 0.f;
-    for (int k = 0; k < 64; ++k) a = fmaf(y[l * 64 + k], wget(lds + L_T, 16, k, lane), a);
-    f[l * 64 + lane] = tanhf(a + lds[L_TB + lane]);
+    for (int k = 0; k < 64; ++k) a = fmaf(y[l * 64 + k], wget(wi + W_IT, 16, k, lane), a);
+    f[l * 64 + lane] = tanhf(a + wi[W_ITB + lane]);
   }
   __syncthreads();
   if (w == 0 && lane < 3) {
     const float* fa = f + (lane == 1 ? 64 : 0);
     const float* fb = f + (lane == 0 ? 0 : 64);
     float a = 0.f;
-    for (int c = 0; c < 64; ++c) a = fmaf(fa[c] * fb[c], lds[L_LW + c], a);
+    for (int c = 0; c < 64; ++c) a = fmaf(fa[c] * fb[c], wi[W_ILW + c], a);
     dots[lane] = a;  // 0: F0F0, 1: F1F1, 2: F0F1
   }
   __syncthreads();
   if (q == 0) {
-    const float g = other_gate(l, dots[0], dots[1], dots[2], lds[L_LB]);
-    const float self = f[l * 64 + lane], oth = f[(1 - l) * 64 + lane];
-    const float m = self + g * oth;
+    const float g = other_gate(l, dots[0], dots[1], dots[2], wi[W_ILB]);
+    const float m = f[l * 64 + lane] + g * f[(1 - l) * 64 + lane];
     const float nr = wave_norm64(m);
     ys[l * 64 + lane] = m / fmaxf(nr, 1e-12f);
   }
   __syncthreads();
-  // z_l = relu(y_l . WL1) . WL2 (WL1 read from global, [64][128] row-major)
-  if (q < 2) {
-    const int j = q * 64 + lane;
-    const float* wl1 = p.w + W_WL1;
+  if (threadIdx.x < 256) {
+    const int ll = threadIdx.x >> 7, j = threadIdx.x & 127;
     float a = 0.f;
-    for (int k = 0; k < 64; ++k) a = fmaf(ys[l * 64 + k], wl1[k * 128 + j], a);
-    scr[S_YP + 8 + l * 128 + j] = fmaxf(a, 0.f);
+    for (int k = 0; k < 64; ++k) a = fmaf(ys[ll * 64 + k], wl1[k * 128 + j], a);
+    zh[ll * 128 + j] = fmaxf(a, 0.f);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     float z[2];
     for (int ll = 0; ll < 2; ++ll) {
       float a = 0.f;
-      for (int j = 0; j < 128; ++j) a = fmaf(scr[S_YP + 8 + ll * 128 + j], lds[L_WL2 + j], a);
+      for (int j = 0; j < 128; ++j) a = fmaf(zh[ll * 128 + j], wi[W_IWL2 + j], a);
       z[ll] = a;
     }
     const float m = fmaxf(z[0], z[1]);
@@ -675,7 +968,7 @@ __device__ void graph_head(const Params& p, float* lds, float* scr, const GraphI
     const float inv = 1.f / (e0 + e1);
     gs[0] = e0 * inv;
     gs[1] = e1 * inv;
-    // aux features (U/PrepareBatchGraph.py:92-101), fp64 division then fp32 as torch.tensor
+    // aux features: fp64 division, then fp32 as torch.tensor(...).type(FloatTensor)
     const double N = (double)gi.n;
     for (int ll = 0; ll < 2; ++ll) {
       gs[4 + ll * 4 + 0] = (float)((double)gv.n_cov / N);
@@ -688,21 +981,22 @@ __device__ void graph_head(const Params& p, float* lds, float* scr, const GraphI
 }
 
 // Attention + Q head for one tile whose final embeddings are in S_E (both layers).
-// Writes q for valid rows; returns nothing (argmax partial updated by thread 0).
-__device__ void attention_q_tile(const Params& p, const float* lds, float* scr, const GraphInfo& gi, const int* rows,
-                                 float* amax /*[4] in LDS misc*/) {
+// Writes q for valid rows and this tile's arg-max partial.
+__device__ __noinline__ void attention_q_tile(const Params& p, const float* lds, float* scr, const GraphInfo& gi,
+                                              const int* rows, float* apart_out) {
+  const float* wi = lds + L_W;
   const int w = wave_id(), l = w >> 2, cb = w & 3, lane = lane_id();
   const int ar = lane & 15, ak = lane >> 4;
   const int col = 16 * cb + ar;
   float* ate = scr + S_E + l * 64 * LDT;
   float* atf = scr + S_F + l * 64 * LDT;
-  // F_l = tanh(E_l . T + b)
   {
-    const float* tf = lds + L_T + cb * 16 * 64;
+    // F_l = tanh(E_l . T + b)
+    const float* tf = wi + W_IT + cb * 16 * 64;
     f4 a = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
     for (int s = 0; s < 16; ++s) a = mfma16(ate[(4 * s + ak) * LDT + ar], tf[s * 64 + lane], a);
-    const float b = lds[L_TB + col];
+    const float b = wi[W_ITB + col];
 #pragma unroll
     for (int r = 0; r < 4; ++r) atf[col * LDT + 4 * ak + r] = tanhf(a[r] + b);
   }
@@ -713,7 +1007,7 @@ __device__ void attention_q_tile(const Params& p, const float* lds, float* scr, 
     const float* fa = scr + S_F + (kind == 1 ? 64 * LDT : 0);
     const float* fb = scr + S_F + (kind == 0 ? 0 : 64 * LDT);
     float a = 0.f;
-    for (int c = 0; c < 64; ++c) a = fmaf(fa[c * LDT + row] * fb[c * LDT + row], lds[L_LW + c], a);
+    for (int c = 0; c < 64; ++c) a = fmaf(fa[c * LDT + row] * fb[c * LDT + row], wi[W_ILW + c], a);
     dot[row * 4 + kind] = a;
   }
   __syncthreads();
@@ -722,28 +1016,31 @@ __device__ void attention_q_tile(const Params& p, const float* lds, float* scr, 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 4 * ak + r;
-      const float g = other_gate(l, dot[row * 4 + 0], dot[row * 4 + 1], dot[row * 4 + 2], lds[L_LB]);
+      const float g = other_gate(l, dot[row * 4 + 0], dot[row * 4 + 1], dot[row * 4 + 2], wi[W_ILB]);
       ate[col * LDT + row] = atf[col * LDT + row] + g * oth[col * LDT + row];
     }
   }
   __syncthreads();
   normalize_tile(scr + S_E, scr);
   __syncthreads();
-  // e[a] = sum_b (h[a] * y[b]) * cp[b]  (outer product then x cross_product, net :356-363)
   {
+    // e[a] = sum_b (h[a] * y[b]) * cp[b]: the reference's outer product then x cross_product
+    // (net :356-363), a batched [64,64]x[64,1] matmul = an FMA chain over b.
     const float* ys = lds + L_YS;
     for (int idx = threadIdx.x; idx < 2 * 16 * 64; idx += NTHREADS) {
       const int ll = idx >> 10, row = (idx >> 6) & 15, a = idx & 63;
       const float h = scr[S_E + ll * 64 * LDT + a * LDT + row];
+      const float* yy = ys + ll * 64;
       float acc = 0.f;
-      for (int b = 0; b < 64; ++b) acc = fmaf(h * ys[ll * 64 + b], lds[L_CP + b], acc);
+#pragma unroll 8
+      for (int b = 0; b < 64; ++b) acc = fmaf(h * yy[b], wi[W_ICP + b], acc);
       scr[S_F + ll * 64 * LDT + a * LDT + row] = acc;
     }
   }
   __syncthreads();
   float* hid = scr + S_HID;
   if (cb < 2) {
-    const float* hf = lds + L_H1 + cb * 16 * 64;
+    const float* hf = wi + W_IH1 + cb * 16 * 64;
     f4 a = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
     for (int s = 0; s < 16; ++s) a = mfma16(atf[(4 * s + ak) * LDT + ar], hf[s * 64 + lane], a);
@@ -756,15 +1053,15 @@ __device__ void attention_q_tile(const Params& p, const float* lds, float* scr, 
     const int ll = threadIdx.x >> 4, row = threadIdx.x & 15;
     const float* gs = lds + L_GS;
     float a = 0.f;
-    for (int k = 0; k < 32; ++k) a = fmaf(hid[(ll * 16 + row) * 33 + k], lds[L_W2 + k], a);
-    for (int k = 0; k < 4; ++k) a = fmaf(gs[4 + ll * 4 + k], lds[L_W2 + 32 + k], a);
+    for (int k = 0; k < 32; ++k) a = fmaf(hid[(ll * 16 + row) * 33 + k], wi[W_IW2 + k], a);
+    for (int k = 0; k < 4; ++k) a = fmaf(gs[4 + ll * 4 + k], wi[W_IW2 + 32 + k], a);
     ql[ll * 16 + row] = a;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     const float* gs = lds + L_GS;
-    float bm = amax[0], bs = amax[1];
-    int bi = __float_as_int(amax[2]), bc = __float_as_int(amax[3]);
+    float bm = NEG_INF, bs = NEG_INF;
+    int bi = 0x7fffffff, bc = 0;
     float* qg = p.q + gi.node_off;
     for (int row = 0; row < 16; ++row) {
       const int v = rows[row];
@@ -772,7 +1069,7 @@ __device__ void attention_q_tile(const Params& p, const float* lds, float* scr, 
       const float qq = gs[0] * ql[row] + gs[1] * ql[16 + row];
       qg[v] = qq;
       if (qq > bm) {
-        bs = bm;  // old max becomes a candidate for second
+        bs = bm;
         bm = qq;
         bi = v;
         bc = 1;
@@ -783,320 +1080,181 @@ __device__ void attention_q_tile(const Params& p, const float* lds, float* scr, 
         bs = qq;
       }
     }
-    amax[0] = bm;
-    amax[1] = bs;
-    amax[2] = __int_as_float(bi);
-    amax[3] = __int_as_float(bc);
+    apart_out[0] = bm;
+    apart_out[1] = bs;
+    apart_out[2] = __int_as_float(bi);
+    apart_out[3] = __int_as_float(bc);
   }
   __syncthreads();
+}
+
+// Phase timestamps of workgroup 0 (diagnostics only; p.prof == nullptr in normal runs).
+#define MD_PROF(slot)                                                                            \
+  do {                                                                                           \
+    if (p.prof != nullptr && blockIdx.x == 0 && threadIdx.x == 0 && pstep < p.prof_cap)          \
+      p.prof[(size_t)pstep * 16 + (slot)] = wall_clock64();                                      \
+  } while (0)
+
+__device__ __forceinline__ void load_weights(float* dst, const float* src) {
+  constexpr int N4 = W_IEND / 4, K = (N4 + NTHREADS - 1) / NTHREADS;
+  const float4* s4 = (const float4*)src;
+  float4* d4 = (float4*)dst;
+  float4 t[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int i = k * NTHREADS + threadIdx.x;
+    if (i < N4) t[k] = s4[i];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int i = k * NTHREADS + threadIdx.x;
+    if (i < N4) d4[i] = t[k];
+  }
+}
+static_assert(W_IEND % 4 == 0, "weight image is copied as float4");
+
+// Graph-list index of global tile t (prefix in LDS, ng + 1 entries).
+__device__ __forceinline__ int tile_graph(const int* pref, int ng, int t) {
+  int lo = 0, hi = ng - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (pref[mid] <= t) lo = mid; else hi = mid - 1;
+  }
+  return lo;
 }
 
 // ------------------------------------------------------------------ the kernel
 __global__ void __launch_bounds__(NTHREADS, 1) md_rollout_kernel(Params p, const float* __restrict__ wimg) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* scr = lds + L_SCR;
-  int* misc = (int*)(lds + L_MISC);
-  float* miscf = lds + L_MISC;
+  int* pref = (int*)(lds + L_PREF);
+  int* rows = (int*)(scr + S_ROW);
 
-  // weight image -> LDS (pre-permuted on the host into fragment order)
-  {
-    const float4* src = (const float4*)wimg;
-    float4* dst = (float4*)lds;
-    for (int i = threadIdx.x; i < L_WEND / 4; i += NTHREADS) dst[i] = src[i];
-  }
+  load_weights(lds + L_W, wimg);
   __syncthreads();
-  // constant virtual-node input: normalize(relu([1,1] . w_n2l))  (net :247,272-283)
   if (wave_id() == 0) {
+    // constant virtual-node input: normalize(relu([1,1] . w_n2l))  (net :247,272-283)
     const int lane = lane_id();
-    float x = fmaf(1.f, lds[L_WN + 64 + lane], fmaf(1.f, lds[L_WN + lane], 0.f));
-    x = fmaxf(x, 0.f);
+    const float x = fmaxf(fmaf(1.f, lds[L_W + W_IWN + 64 + lane], fmaf(1.f, lds[L_W + W_IWN + lane], 0.f)), 0.f);
     const float nr = wave_norm64(x);
     lds[L_Y0 + lane] = x / fmaxf(nr, 1e-12f);
   }
   __syncthreads();
 
-  const int tsz = p.team_size;
-  const int team = blockIdx.x / tsz, trank = blockIdx.x % tsz;
-  unsigned* bar = p.bar + team;
   unsigned target = 0;
-  int* rows = (int*)(scr + S_ROW);
-
+  int pstep = 0;
+  bool have_q = false;
+  const int ng = p.nglist;
   while (true) {
-    if (trank == 0 && threadIdx.x == 0) {
-      int k = atomicAdd(p.queue, 1);
-      p.team_graph[team] = k < p.nglist ? p.glist[k] : -1;
+    // ---------------- phase A: one workgroup per graph
+    MD_PROF(0);
+    if (threadIdx.x == 0) ((int*)(lds + L_MISC))[60] = pstep;
+    __syncthreads();
+    bool wdirty = false;
+    for (int gi = blockIdx.x; gi < ng; gi += gridDim.x) {
+      phase_a(p, p.glist[gi], have_q, lds);
+      wdirty = true;
     }
-    team_sync(p, bar, target);
-    if (threadIdx.x == 0) misc[0] = load_err(p) ? -1 : p.team_graph[team];
+    if (wdirty) load_weights(lds + L_W, wimg);
+    MD_PROF(3);
+    grid_sync(p, target);
+    MD_PROF(4);
+    if (load_err(p)) break;
+    // ---------------- tile prefix over the launch's graphs
+    for (int i = threadIdx.x; i < ng; i += NTHREADS) {
+      const GraphVar* gv = p.gvar + p.glist[i];
+      pref[i + 1] = gv->status == ST_RUN ? (gv->n_live + TILE - 1) / TILE : 0;
+    }
     __syncthreads();
-    const int g = misc[0];
+    if (threadIdx.x == 0) {
+      pref[0] = 0;
+      for (int i = 0; i < ng; ++i) pref[i + 1] += pref[i];
+    }
     __syncthreads();
-    if (g < 0) break;
-    GraphCtx G;
-    G.gi = p.ginfo[g];
-    G.g = g;
-    const GraphInfo& gi = G.gi;
-    bool have_q = false;
+    const int ttot = pref[ng];
+    if (ttot == 0) break;
+    const int per = (ttot + gridDim.x - 1) / gridDim.x;
+    const int t0 = min(ttot, (int)blockIdx.x * per), t1 = min(ttot, t0 + per);
 
-    while (true) {
-      // ---------------- phase A (team leader)
-      if (trank == 0) {
-        GraphVar& gv = *(GraphVar*)(lds + L_GV);
-        if (threadIdx.x == 0) gv = p.gvar[g];
-        __syncthreads();
-        int* tmp = (int*)(scr + A_TMP);
-        bool stop = false;
-        int pend_n = 0;
-        int pend_a = -1;
-        if (have_q) {
-          if (threadIdx.x == 0) {
-            float bm = NEG_INF, bs = NEG_INF;
-            int bi = 0x7fffffff, bc = 0;
-            for (int r = 0; r < tsz; ++r) {
-              const float* ap = p.apart + (size_t)(team * tsz + r) * 4;
-              const float m = ap[0], s = ap[1];
-              const int i = __float_as_int(ap[2]), c = __float_as_int(ap[3]);
-              if (c == 0) continue;
-              if (m > bm) {
-                bs = fmaxf(bm, s);
-                bm = m;
-                bi = i;
-                bc = c;
-              } else if (m == bm) {
-                bc += c;
-                bi = min(bi, i);
-                bs = fmaxf(bs, s);
-              } else {
-                bs = fmaxf(bs, m);
-              }
-            }
-            const int t = gv.npred;
-            if (t < gi.n) {
-              int* ts = p.tr_stat + (size_t)(gi.node_off + t) * 4;
-              ts[0] = gv.n_live;
-              ts[1] = gv.alive[0];
-              ts[2] = gv.alive[1];
-              ts[3] = bc;
-              p.tr_q[(size_t)(gi.node_off + t) * 2 + 0] = bm;
-              p.tr_q[(size_t)(gi.node_off + t) * 2 + 1] = bm - bs;
-            }
-            gv.npred = t + 1;
-            gv.ntie = bc;
-            gv.qmax = bm;
-            gv.gap = bm - bs;
-            gv.argmax = bc == 1 ? bi : -1;
-            misc[1] = bi;
-            misc[2] = bc;
-          }
-          __syncthreads();
-          if (p.run_mode == RUN_PREDICT) {
-            if (threadIdx.x == 0) gv.status = ST_PAUSED;
-            stop = true;
-          } else if (p.host_select || misc[2] != 1) {
-            if (threadIdx.x == 0) gv.status = ST_NEED_HOST;
-            stop = true;
-          } else {
-            pend_n = 1;
-            pend_a = misc[1];
-          }
-        } else {
-          pend_n = gv.npend;
-        }
-        __syncthreads();
-        if (!stop) {
-          int* par0;
-          int* par1;
-          const bool lds_mcc = gi.n <= p.lds_mcc_cap;
-          if (lds_mcc) {
-            par0 = (int*)scr;
-            par1 = par0 + gi.n;
-          } else {
-            par0 = p.gpar + 2 * (size_t)gi.node_off;
-            par1 = par0 + gi.n;
-          }
-          for (int k = 0; k < pend_n; ++k) {
-            const int a = have_q ? pend_a : p.pend[gi.node_off + k];
-            if (gv.alive[0] == 0 || gv.alive[1] == 0) break;  // terminal between queued actions
-            if (a < 0 || a >= gi.n || p.covered[gi.node_off + a]) {
-              if (threadIdx.x == 0) atomicExch(p.err, a < 0 || a >= gi.n ? ERR_BADNODE : ERR_COVERED);
-              break;
-            }
-            int cnt[2], pr[2];
-            apply_action(p, G, a, tmp, cnt);
-            const int lm = lds_mcc ? mcc_fixed_point<false>(p, G, par0, par1, tmp, pr)
-                                   : mcc_fixed_point<true>(p, G, par0, par1, tmp, pr);
-            if (threadIdx.x == 0) {
-              gv.counter[0] += cnt[0];
-              gv.counter[1] += cnt[1];
-              gv.removed[0] += pr[0];
-              gv.removed[1] += pr[1];
-              gv.alive[0] -= cnt[0] + pr[0];
-              gv.alive[1] -= cnt[1] + pr[1];
-              gv.n_cov += 1;
-              gv.lmcc = lm;
-              p.tr_action[gi.node_off + gv.steps] = a;
-              p.tr_rank[gi.node_off + gv.steps] = lm;
-              gv.steps += 1;
-            }
-            __syncthreads();
-          }
-          if (!gv.s0_done) {
-            int pr[2];
-            const int lm = lds_mcc ? mcc_fixed_point<false>(p, G, par0, par1, tmp, pr)
-                                   : mcc_fixed_point<true>(p, G, par0, par1, tmp, pr);
-            if (threadIdx.x == 0) {
-              gv.removed[0] += pr[0];
-              gv.removed[1] += pr[1];
-              gv.max_rank = lm;
-              gv.lmcc = lm;
-              gv.s0_done = 1;
-            }
-          }
-          if (threadIdx.x == 0) gv.npend = 0;
-          __syncthreads();
-          GraphVar loc = gv;
-          __syncthreads();
-          const int ferr = compute_features(p, G, loc, lds, tmp);
-          if (threadIdx.x == 0) {
-            gv.n_live = loc.n_live;
-            gv.dmax[0] = loc.dmax[0];
-            gv.dmax[1] = loc.dmax[1];
-            gv.alive[0] = loc.alive[0];
-            gv.alive[1] = loc.alive[1];
-            gv.twohop[0] = loc.twohop[0];
-            gv.twohop[1] = loc.twohop[1];
-            if (ferr) atomicExch(p.err, ferr);
-            const bool term = gv.alive[0] == 0 || gv.alive[1] == 0;
-            if (term) gv.status = ST_TERMINAL;
-            else if (p.run_mode == RUN_STEP) gv.status = ST_PAUSED;
-            else gv.status = ST_RUN;
-          }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) p.gvar[g] = gv;
-        __syncthreads();
-      }
-      team_sync(p, bar, target);
-      if (threadIdx.x == 0) {
-        const GraphVar* gvp = p.gvar + g;
-        misc[3] = load_err(p) ? ST_TERMINAL : gvp->status;
-        misc[4] = gvp->n_live;
-      }
-      __syncthreads();
-      if (misc[3] != ST_RUN) break;
-      const int n_live = misc[4];
-      const int ntiles = (n_live + TILE - 1) / TILE;
-      const int per = (ntiles + tsz - 1) / tsz;
-      const int t0 = min(ntiles, trank * per), t1 = min(ntiles, t0 + per);
-      if (threadIdx.x == 0) {
-        GraphVar gvl = p.gvar[g];
-        // stash what phase 3 needs
-        misc[8] = gvl.n_cov;
-        misc[9] = gvl.counter[0];
-        misc[10] = gvl.counter[1];
-        ((long long*)(misc + 12))[0] = gvl.twohop[0];
-        ((long long*)(misc + 12))[1] = gvl.twohop[1];
-      }
-      __syncthreads();
-
-      // ---------------- phases 1..3
-      for (int it = 1; it <= BP_ITERS; ++it) {
-        float* sacc = lds + L_SACC;
-        if (threadIdx.x < 384) sacc[threadIdx.x] = 0.f;
-        if (it == 3) {
-          // partial arg-max of this workgroup
-          if (threadIdx.x == 0) {
-            miscf[16] = NEG_INF;
-            miscf[17] = NEG_INF;
-            miscf[18] = __int_as_float(0x7fffffff);
-            miscf[19] = __int_as_float(0);
-          }
-        }
-        __syncthreads();
-        if (it >= 2) {
-          // virtual-node sums of all team workgroups, in workgroup order
-          const int nsum = it == 2 ? 2 : 1;  // it==2: S0,S1 ; it==3: S2
-          float* sbuf = scr + S_HID;          // [2 sums][2 layers][64]
-          for (int idx = threadIdx.x; idx < nsum * 128; idx += NTHREADS) {
-            const int si = idx >> 7, lc = idx & 127;
-            const int which = it == 2 ? si : 2;
-            float a = 0.f;
-            for (int r = 0; r < tsz; ++r) a = a + p.spart[((size_t)(team * tsz + r) * 3 + which) * 128 + lc];
-            sbuf[si * 128 + lc] = a;
-          }
-          __syncthreads();
-          float* y = lds + L_Y;
+    for (int it = 1; it <= BP_ITERS; ++it) {
+      MD_PROF(10 + it);
+      int cur = -1;  // graph-list index whose virtual node / graph head is loaded
+      for (int t = t0; t < t1; ++t) {
+        const int gl = tile_graph(pref, ng, t);
+        const int g = p.glist[gl];
+        const GraphInfo gi = p.ginfo[g];
+        const int j = t - pref[gl];  // tile within the graph
+        if (it >= 2 && gl != cur) {
+          // virtual-node chain of this graph (identical in every workgroup that needs it)
+          const GraphVar gv = p.gvar[g];
+          const int nt = (gv.n_live + TILE - 1) / TILE;
+          float* sbuf = scr + S_HID;  // [2][64]
+          float* yw = lds + L_YW;
           if (it == 2) {
-            if (threadIdx.x < 128) y[threadIdx.x] = lds[L_Y0 + (threadIdx.x & 63)];
-            __syncthreads();
-            vrow_update(lds, scr, sbuf, y);          // Y1 from S0
-            vrow_update(lds, scr, sbuf + 128, y);    // Y2 from S1
+            if (threadIdx.x < 128) yw[threadIdx.x] = lds[L_Y0 + (threadIdx.x & 63)];
+            graph_sum(p, gi, nt, 0, sbuf, scr + S_YP);
+            vrow_update(lds + L_W, scr, sbuf, yw);  // Y1 from S0
+            graph_sum(p, gi, nt, 1, sbuf, scr + S_YP);
+            vrow_update(lds + L_W, scr, sbuf, yw);  // Y2 from S1
+            if (threadIdx.x < 128) p.ybuf[(size_t)g * 128 + threadIdx.x] = yw[threadIdx.x];
           } else {
-            vrow_update(lds, scr, sbuf, y);          // Y3 from S2
-            GraphVar gvs;
-            gvs.n_cov = misc[8];
-            gvs.counter[0] = misc[9];
-            gvs.counter[1] = misc[10];
-            gvs.twohop[0] = ((long long*)(misc + 12))[0];
-            gvs.twohop[1] = ((long long*)(misc + 12))[1];
-            graph_head(p, lds, scr, gi, gvs);
+            if (threadIdx.x < 128) yw[threadIdx.x] = p.ybuf[(size_t)g * 128 + threadIdx.x];
+            graph_sum(p, gi, nt, 2, sbuf, scr + S_YP);
+            vrow_update(lds + L_W, scr, sbuf, yw);  // Y3 from S2
+            graph_head(p, lds, scr, gi, gv);
           }
+          cur = gl;
         }
-        for (int t = t0; t < t1; ++t) {
-          if (threadIdx.x < TILE) {
-            const int r = t * TILE + threadIdx.x;
-            rows[threadIdx.x] = r < n_live ? p.live[gi.node_off + r] : -1;
-          }
-          __syncthreads();
-          gather_tile(p, gi, it, rows, scr);
-          __syncthreads();
-          update_tile(lds, scr);
-          __syncthreads();
-          normalize_tile(scr + S_E, scr);
-          __syncthreads();
-          // partial virtual-node sums (rows in ascending compact order) and H store
-          if (threadIdx.x < 128) {
-            const int l = threadIdx.x >> 6, c = threadIdx.x & 63;
-            const float* ate = scr + S_E + l * 64 * LDT + c * LDT;
-            const float* atx = scr + S_X + l * 64 * LDT + c * LDT;
-            float s_new = sacc[(it == 1 ? 1 : 2) * 128 + l * 64 + c];
-            float s_old = sacc[l * 64 + c];
-            for (int r = 0; r < TILE; ++r) {
-              if (rows[r] < 0) break;
-              s_new = s_new + ate[r];
-              if (it == 1) s_old = s_old + atx[r];
-            }
-            sacc[(it == 1 ? 1 : 2) * 128 + l * 64 + c] = s_new;
-            if (it == 1) sacc[l * 64 + c] = s_old;
-          }
-          if (it < 3) {
-            // H_it -> global (buffer (it-1)&1), one row per wave pass, 256 B coalesced
-            const int w = wave_id(), l = w >> 2, lane = lane_id();
-            float* hb = p.H[l][(it - 1) & 1] + (size_t)gi.node_off * EMB;
-            for (int r = 4 * (w & 3); r < 4 * (w & 3) + 4; ++r) {
-              const int v = rows[r];
-              if (v >= 0) hb[(size_t)v * EMB + lane] = scr[S_E + l * 64 * LDT + lane * LDT + r];
-            }
-          }
-          __syncthreads();
-          if (it == 3) attention_q_tile(p, lds, scr, gi, rows, miscf + 16);
+        if (threadIdx.x < TILE) {
+          const int r = j * TILE + threadIdx.x;
+          const GraphVar* gvp = p.gvar + g;
+          rows[threadIdx.x] = r < gvp->n_live ? p.live[gi.node_off + r] : -1;
         }
         __syncthreads();
-        if (it < 3) {
-          // publish partial sums: it==1 -> S0 (slot 0), S1 (slot 1); it==2 -> S2 (slot 2)
-          float* sp = p.spart + (size_t)blockIdx.x * 3 * 128;
-          if (it == 1) {
-            if (threadIdx.x < 256) sp[threadIdx.x] = sacc[threadIdx.x];
-          } else {
-            if (threadIdx.x < 128) sp[256 + threadIdx.x] = sacc[256 + threadIdx.x];
+        gather_tile(p, gi, it, rows, scr);
+        __syncthreads();
+        update_tile(lds + L_W, scr);
+        __syncthreads();
+        normalize_tile(scr + S_E, scr);
+        __syncthreads();
+        if (threadIdx.x < 128) {
+          // tile partial sums of the virtual node (rows in ascending compact order from 0)
+          const int l = threadIdx.x >> 6, c = threadIdx.x & 63;
+          const float* ate = scr + S_E + l * 64 * LDT + c * LDT;
+          const float* atx = scr + S_X + l * 64 * LDT + c * LDT;
+          float s_new = 0.f, s_old = 0.f;
+          for (int r = 0; r < TILE; ++r) {
+            if (rows[r] < 0) break;
+            s_new = s_new + ate[r];
+            s_old = s_old + atx[r];
           }
-        } else {
-          if (threadIdx.x < 4) p.apart[(size_t)blockIdx.x * 4 + threadIdx.x] = miscf[16 + threadIdx.x];
+          float* sp = p.spart + (size_t)(gi.tile_off + j) * 384;
+          if (it == 1) {
+            sp[l * 64 + c] = s_old;        // S0 (first-layer input)
+            sp[128 + l * 64 + c] = s_new;  // S1
+          } else if (it == 2) {
+            sp[256 + l * 64 + c] = s_new;  // S2
+          }
         }
-        team_sync(p, bar, target);
+        if (it < 3) {
+          const int w = wave_id(), l = w >> 2, lane = lane_id();
+          float* hb = p.H[l][(it - 1) & 1] + (size_t)gi.node_off * EMB;
+          for (int r = 4 * (w & 3); r < 4 * (w & 3) + 4; ++r) {
+            const int v = rows[r];
+            if (v >= 0) hb[(size_t)v * EMB + lane] = scr[S_E + l * 64 * LDT + lane * LDT + r];
+          }
+        }
+        __syncthreads();
+        if (it == 3) attention_q_tile(p, lds, scr, gi, rows, p.apart + (size_t)(gi.tile_off + j) * 4);
       }
-      have_q = true;
+      MD_PROF(3 + 2 * it);
+      grid_sync(p, target);
+      MD_PROF(4 + 2 * it);
+      if (load_err(p)) break;
     }
+    if (load_err(p)) break;
+    have_q = true;
+    pstep++;
   }
 }
 
@@ -1110,8 +1268,10 @@ __global__ void md_reset_kernel(Params p) {
     p.covered[gi.node_off + v] = 0;
     p.q[gi.node_off + v] = NEG_INF;
   }
-  for (int l = 0; l < 2; ++l)
+  for (int l = 0; l < 2; ++l) {
     for (int e = threadIdx.x; e < gi.e[l]; e += blockDim.x) p.estate[l][gi.eoff[l] + e] = E_ALIVE;
+    for (int e = threadIdx.x; e < 2 * gi.e[l]; e += blockDim.x) p.calive[l][gi.coff[l] + e] = 1;
+  }
   if (threadIdx.x == 0) {
     GraphVar v = {};
     v.status = ST_RUN;
@@ -1125,8 +1285,8 @@ __global__ void md_reset_kernel(Params p) {
 // ------------------------------------------------------------------ launch wrappers (C++)
 namespace md {
 int lds_bytes() { return L_TOTAL * 4; }
-int lds_mcc_cap() { return LDS_MCC_CAP; }
-int weight_image_floats() { return L_WEND; }
+int weight_image_floats() { return W_IEND; }
+bool phase_a_fits_lds_host(int n, int et) { return phase_a_fits_lds(n, et); }
 
 // Host-side permutation of the reference-layout weight blob into the LDS image.
 void build_weight_image(const float* w, float* img) {
@@ -1138,27 +1298,27 @@ void build_weight_image(const float* w, float* img) {
           img[dst + (cb * (K / 4) + s) * 64 + lane] = w[src + k * 64 + c];
         }
   };
-  for (int i = 0; i < L_WEND; ++i) img[i] = 0.f;
-  frag(L_P1, W_P1, 64);
-  frag(L_P2, W_P2, 64);
-  frag(L_P3, W_P3, 128);
-  frag(L_T, W_T, 64);
+  for (int i = 0; i < W_IEND; ++i) img[i] = 0.f;
+  frag(W_IP1, W_P1, 64);
+  frag(W_IP2, W_P2, 64);
+  frag(W_IP3, W_P3, 128);
+  frag(W_IT, W_T, 64);
   for (int cb = 0; cb < 2; ++cb)
     for (int s = 0; s < 16; ++s)
       for (int lane = 0; lane < 64; ++lane) {
         const int k = 4 * s + (lane >> 4), c = 16 * cb + (lane & 15);
-        img[L_H1 + (cb * 16 + s) * 64 + lane] = w[W_H1 + k * 32 + c];
+        img[W_IH1 + (cb * 16 + s) * 64 + lane] = w[W_H1 + k * 32 + c];
       }
   for (int i = 0; i < 64; ++i) {
-    img[L_TB + i] = w[W_TB + i];
-    img[L_LW + i] = w[W_LW + i];
-    img[L_CP + i] = w[W_CP + i];
+    img[W_ITB + i] = w[W_TB + i];
+    img[W_ILW + i] = w[W_LW + i];
+    img[W_ICP + i] = w[W_CP + i];
   }
-  for (int i = 0; i < 36; ++i) img[L_W2 + i] = w[W_W2 + i];
-  img[L_LB] = w[W_LB];
+  for (int i = 0; i < 36; ++i) img[W_IW2 + i] = w[W_W2 + i];
+  img[W_ILB] = w[W_LB];
   for (int i = 0; i < 128; ++i) {
-    img[L_WN + i] = w[W_N2L + i];
-    img[L_WL2 + i] = w[W_WL2 + i];
+    img[W_IWN + i] = w[W_N2L + i];
+    img[W_IWL2 + i] = w[W_WL2 + i];
   }
 }
 

@@ -1,0 +1,56 @@
+"""On-GPU phase profile of the rollout kernel (workgroup-0 wall-clock stamps)."""
+import os, sys, time
+import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mdcommunity_amd import _lib
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+W = _lib.pack_weights(dict(np.load(os.path.join(ROOT, "mdcommunity_amd/weights/unit_g0.5_iter100000.npz"))))
+NAMES = ["A:mcc", "A:feat", "A:end", "barA", "p1", "bar1", "p2", "bar2", "p3", "bar3"]
+
+def prof(name, team):
+    z = np.load(os.path.join(ROOT, f"tests/golden/rollout_{name}.npz"))
+    eng = _lib.Engine(W)
+    eng.set_team_size(team)
+    n = int(z["n_nodes"])
+    eng.load_graphs([(n, z["edges0"], z["edges1"])])
+    eng.reset()
+    eng.rollout()  # warm
+    eng.reset()
+    eng.profile(512)
+    t0 = time.time(); out = eng.rollout(); dt = time.time() - t0
+    ms, nl = eng.last_timing()
+    P = eng.profile_read().astype(np.int64)
+    eng.profile(0)
+    # slots: 0 startA,1 after mcc,2 after feat,3 endA,4 afterbarA,11 p1 tiles start,5 end p1,6 after bar1,12,7,8,13,9,10
+    full = P[(P[:, 10] > 0)]
+    d = lambda a, b: np.median((full[:, b] - full[:, a])) * 10 / 1000.0  # us
+    seg = [("A:stage", 0, 1), ("A:apply+mcc", 1, 2), ("A:feat", 2, 14), ("A:h0", 14, 15), ("A:wreload", 15, 3), ("barA", 3, 4), ("pref", 4, 11), ("p1", 11, 5), ("bar1", 5, 6), ("p2", 12, 7),
+           ("bar2", 7, 8), ("p3", 13, 9), ("bar3", 9, 10)]
+    tot = np.median(full[:, 10] - full[:, 0]) * 10 / 1000.0
+    print(f"{name} team={team}: removals {len(out[0][0])} wall {dt*1e3:.2f} ms kernel {ms:.2f} ms launches {nl}; "
+          f"steps profiled {len(full)} median step {tot:.1f} us", flush=True)
+    print("   " + "  ".join(f"{s}={d(a,b):.1f}" for s, a, b in seg), flush=True)
+    eng.close()
+
+def batch(nb, team):
+    gs = []
+    for name in ["gmm1000_s0", "gmm1000_s1", "gmm1000_s2", "er1000"]:
+        z = np.load(os.path.join(ROOT, f"tests/golden/rollout_{name}.npz"))
+        gs.append((int(z["n_nodes"]), z["edges0"], z["edges1"], len(z["seq"])))
+    eng = _lib.Engine(W)
+    eng.set_team_size(team)
+    sel = [gs[i % 4] for i in range(nb)]
+    eng.load_graphs([g[:3] for g in sel])
+    eng.reset(); eng.rollout(); eng.reset()
+    t0 = time.time(); out = eng.rollout(); dt = time.time() - t0
+    ms, nl = eng.last_timing()
+    rem = sum(len(o[0]) for o in out)
+    print(f"batch {nb} team={team}: removals {rem} wall {dt*1e3:.1f} ms kernel {ms:.1f} ms launches {nl} -> {rem/dt:.0f} rem/s", flush=True)
+    eng.close()
+
+if __name__ == "__main__":
+    for team in [int(x) for x in sys.argv[1].split(",")]:
+        prof("gmm1000_s0", team)
+    if len(sys.argv) > 2:
+        for nb in [int(x) for x in sys.argv[2].split(",")]:
+            batch(nb, 0)
