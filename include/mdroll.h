@@ -133,10 +133,13 @@ md_status md_set_team_size(md_ctx* ctx, int team_size);
  * events on the context's stream, and the number of launches they took. */
 md_status md_last_timing(md_ctx* ctx, double* kernel_ms, int32_t* launches);
 
-/* Diagnostics: record device wall-clock (100 MHz) phase timestamps of workgroup 0, 16 slots
- * per removal step, for up to `steps` steps per launch of the following calls (0 disables).
+/* Diagnostics: record device wall-clock (100 MHz) phase timestamps of workgroup 0,
+ * MD_PROF_SLOTS slots per removal step (0-15 timestamps, 16-31 accumulated sub-phase
+ * durations and counters of the environment step), for up to `steps` steps per launch of the
+ * following calls (0 disables).
  * md_profile_read copies the timestamps accumulated since md_profile was called and returns
  * the number of steps recorded in *n_steps. */
+#define MD_PROF_SLOTS 32
 md_status md_profile(md_ctx* ctx, int steps);
 md_status md_profile_read(md_ctx* ctx, uint64_t* out, int capacity_steps, int32_t* n_steps);
 

@@ -18,6 +18,8 @@ MD_WEIGHT_FLOATS = 31205
 STATUS_NAMES = {1: "MD_EINVAL", 2: "MD_EHIP", 3: "MD_EOOM", 4: "MD_ESTATE", 5: "MD_ETIMEOUT", 6: "MD_ECALLBACK"}
 
 # Every symbol include/mdroll.h declares (checked by tests/test_abi.py).
+PROF_SLOTS = 32  # MD_PROF_SLOTS in include/mdroll.h
+
 EXPORTS = ("md_create", "md_destroy", "md_last_error", "md_set_weights", "md_load_graphs", "md_reset",
            "md_predict", "md_step", "md_rollout", "md_rollout_trace", "md_get_state", "md_set_state",
            "md_set_team_size", "md_last_timing", "md_profile", "md_profile_read", "md_version")
@@ -220,7 +222,7 @@ class Engine:
         self._check(self.lib.md_profile(self.h, int(steps)))
 
     def profile_read(self, cap=4096):
-        out = np.zeros((cap, 16), np.uint64)
+        out = np.zeros((cap, PROF_SLOTS), np.uint64)
         k = ctypes.c_int32()
         self._check(self.lib.md_profile_read(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), cap,
                                              ctypes.byref(k)))

@@ -10,6 +10,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <string>
 #include <unordered_set>
 #include <vector>
@@ -60,6 +61,8 @@ struct md_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::string err;
   int team_size_req = 0;
+  int env_mode = 1;  // 1: dedicated environment workgroups for small batches
+  int variant = 0;   // diagnostics knob (MD_VARIANT)
   double last_ms = 0.0;
   int last_launches = 0;
 
@@ -75,7 +78,9 @@ struct md_ctx {
   DevBuf<int> rowptr[2], adj[2], epos[2], eu[2], ev[2];
   DevBuf<uint8_t> estate[2], calive[2], covered;
   DevBuf<int> deg[2], live, gscr, pend, tr_action, tr_rank, tr_stat, glist, ctl;
-  DevBuf<float> H[2][2], h0tab[2], q, spart, apart, ybuf, tr_q, node_w;
+  DevBuf<float> H[2][2], h0tab[2], q, spart, apart, ybuf, hbuf, tr_q, node_w;
+  DevBuf<unsigned long long> hflag;
+  unsigned launch_seq = 0;
   bool need_gscr = false;
   DevBuf<unsigned long long> prof;
   int prof_cap = 0;
@@ -103,7 +108,7 @@ struct md_ctx {
     }
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
     tr_stat.release(); glist.release(); ctl.release(); q.release(); spart.release();
-    apart.release(); ybuf.release(); tr_q.release(); node_w.release();
+    apart.release(); ybuf.release(); hbuf.release(); hflag.release(); tr_q.release(); node_w.release();
     ng = 0;
     hinfo.clear();
     hvar.clear();
@@ -157,6 +162,8 @@ Params make_params(md_ctx* c) {
   p.spart = c->spart.p;
   p.apart = c->apart.p;
   p.ybuf = c->ybuf.p;
+  p.hbuf = c->hbuf.p;
+  p.hflag = c->hflag.p;
   p.pend = c->pend.p;
   p.tr_action = c->tr_action.p;
   p.tr_rank = c->tr_rank.p;
@@ -191,24 +198,38 @@ md_status push_vars(md_ctx* c) {
   return MD_OK;
 }
 
+// Small batches whose environments fit LDS get dedicated environment workgroups.
+constexpr int DEDICATED_MAX_GRAPHS = 16;
+
+int env_workgroups(md_ctx* c, const std::vector<int>& gl) {
+  if (c->env_mode == 0 || (int)gl.size() > DEDICATED_MAX_GRAPHS || (int)gl.size() * 4 > c->cus) return 0;
+  for (int g : gl)
+    if (!phase_a_fits_lds_host(c->hinfo[g].n, c->hinfo[g].e[0] + c->hinfo[g].e[1])) return 0;
+  return (int)gl.size();
+}
+
 // Workgroups of one launch: enough for every graph's phase A and every 16-row tile, at most
 // one per CU (the kernel is persistent and relies on co-residency for its grid barrier).
-int grid_size(md_ctx* c, const std::vector<int>& gl) {
-  if (c->team_size_req > 0) return std::max(1, std::min(c->team_size_req, c->cus));
+int grid_size(md_ctx* c, const std::vector<int>& gl, int n_env) {
   long tiles = 0;
   for (int g : gl) tiles += (c->hinfo[g].n + TILE - 1) / TILE;
-  const long want = std::max<long>((long)gl.size(), tiles);
-  return (int)std::max<long>(1, std::min<long>(want, c->cus));
+  if (c->team_size_req > 0) tiles = c->team_size_req;
+  const long want = n_env > 0 ? 2 * n_env + std::max<long>(1, tiles) : std::max<long>((long)gl.size(), tiles);
+  return (int)std::max<long>(2 * n_env + 1, std::min<long>(want, c->cus));
 }
 
 // One launch of the persistent kernel over the graphs in gl (<= G_CAP of them).
 md_status launch_chunk(md_ctx* c, const int* gl, int ngl, int run_mode, int host_select) {
   std::vector<int> v(gl, gl + ngl);
-  const int grid = grid_size(c, v);
+  const int n_env = env_workgroups(c, v);
+  const int grid = grid_size(c, v, n_env);
   HIPCHK(c, hipMemcpyAsync(c->glist.p, gl, sizeof(int) * ngl, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->ctl.p, 0, sizeof(int) * CTL_WORDS, c->stream));
   Params p = make_params(c);
   p.nglist = ngl;
+  p.n_env = n_env;
+  p.variant = c->variant;
+  p.launch_seq = ++c->launch_seq;
   p.run_mode = run_mode;
   p.host_select = host_select;
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
@@ -223,11 +244,11 @@ md_status launch_chunk(md_ctx* c, const int* gl, int ngl, int run_mode, int host
   c->last_launches += 1;
   if (dev_err) return fail(c, dev_err == 1 ? MD_ETIMEOUT : MD_EINVAL, "device: %s", err_name(dev_err));
   if (c->prof_cap > 0) {
-    std::vector<unsigned long long> tmp((size_t)c->prof_cap * 16);
+    std::vector<unsigned long long> tmp((size_t)c->prof_cap * PROF_SLOTS);
     HIPCHK(c, hipMemcpy(tmp.data(), c->prof.p, sizeof(unsigned long long) * tmp.size(), hipMemcpyDeviceToHost));
     for (int s = 0; s < c->prof_cap; ++s) {
-      if (tmp[(size_t)s * 16] == 0) break;
-      c->prof_host.insert(c->prof_host.end(), tmp.begin() + (size_t)s * 16, tmp.begin() + (size_t)s * 16 + 16);
+      if (tmp[(size_t)s * PROF_SLOTS] == 0) break;
+      c->prof_host.insert(c->prof_host.end(), tmp.begin() + (size_t)s * PROF_SLOTS, tmp.begin() + (size_t)s * PROF_SLOTS + PROF_SLOTS);
     }
     HIPCHK(c, hipMemset(c->prof.p, 0, sizeof(unsigned long long) * tmp.size()));
   }
@@ -278,6 +299,8 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   md_ctx* c = new md_ctx();
   c->device = device;
   c->cost_mode = cost_mode;
+  if (const char* v = std::getenv("MD_VARIANT")) c->variant = std::atoi(v);
+  if (const char* v = std::getenv("MD_ENV_MODE")) c->env_mode = std::atoi(v);
   md_status st = MD_OK;
   do {
     if (hipSetDevice(device) != hipSuccess) { st = MD_EHIP; break; }
@@ -319,6 +342,10 @@ md_status md_set_weights(md_ctx* c, const float* weights, size_t n_floats) {
       for (size_t v = 0; v < c->tot_n; ++v) host_first_layer(weights, &nw[l * c->tot_n + v], &tab[v * EMB]);
       HIPCHK(c, hipMemcpy(c->h0tab[l].p, tab.data(), sizeof(float) * tab.size(), hipMemcpyHostToDevice));
     }
+  } else if (c->ng > 0) {
+    // unit cost: the per-graph degree tables were built from the old weights
+    for (auto& v : c->hvar) v.hdmax[0] = v.hdmax[1] = 0;
+    return push_vars(c);
   }
   return MD_OK;
 }
@@ -448,6 +475,9 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->spart.alloc(tt * 384));
   HIPCHK(c, c->apart.alloc(tt * 4));
   HIPCHK(c, c->ybuf.alloc((size_t)n_graphs * 128));
+  HIPCHK(c, c->hbuf.alloc((size_t)n_graphs * 144));
+  HIPCHK(c, c->hflag.alloc((size_t)n_graphs));
+  HIPCHK(c, hipMemset(c->hflag.p, 0, sizeof(unsigned long long) * n_graphs));
   HIPCHK(c, hipMemcpyAsync(c->ginfo.p, info.data(), sizeof(GraphInfo) * n_graphs, hipMemcpyHostToDevice, c->stream));
   if (c->cost_mode == MD_COST_DEGREE) {
     HIPCHK(c, c->node_w.alloc(2 * tn));
@@ -692,6 +722,7 @@ md_status md_set_state(md_ctx* c, int graph, const uint8_t* covered, const uint8
   v.npend = 0;
   v.status = ST_RUN;
   v.n_live = 1;  // recomputed by the next prediction's phase A
+  v.hdmax[0] = v.hdmax[1] = 0;
   return push_vars(c);
 }
 
@@ -702,8 +733,8 @@ md_status md_profile(md_ctx* c, int steps) {
   c->prof_cap = 0;
   c->prof_host.clear();
   if (steps > 0) {
-    HIPCHK(c, c->prof.alloc((size_t)steps * 16));
-    HIPCHK(c, hipMemset(c->prof.p, 0, sizeof(unsigned long long) * (size_t)steps * 16));
+    HIPCHK(c, c->prof.alloc((size_t)steps * PROF_SLOTS));
+    HIPCHK(c, hipMemset(c->prof.p, 0, sizeof(unsigned long long) * (size_t)steps * PROF_SLOTS));
     c->prof_cap = steps;
   }
   return MD_OK;
@@ -711,9 +742,9 @@ md_status md_profile(md_ctx* c, int steps) {
 
 md_status md_profile_read(md_ctx* c, uint64_t* out, int capacity_steps, int32_t* n_steps) {
   if (!c || capacity_steps < 0) return MD_EINVAL;
-  const int have = (int)(c->prof_host.size() / 16);
+  const int have = (int)(c->prof_host.size() / PROF_SLOTS);
   const int k = std::min(have, capacity_steps);
-  if (out) std::memcpy(out, c->prof_host.data(), sizeof(uint64_t) * 16 * (size_t)k);
+  if (out) std::memcpy(out, c->prof_host.data(), sizeof(uint64_t) * PROF_SLOTS * (size_t)k);
   if (n_steps) *n_steps = k;
   return MD_OK;
 }

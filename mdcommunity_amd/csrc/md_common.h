@@ -14,7 +14,8 @@ constexpr int AUX_DIM = 4;       // aux_dim, :64
 constexpr int BP_ITERS = 3;      // max_bp_iter, :62
 constexpr int NTHREADS = 512;    // 8 waves: waves 0-3 work on layer 0, waves 4-7 on layer 1
 constexpr int TILE = 16;         // node rows per MFMA tile (v_mfma_f32_16x16x4_f32)
-constexpr int G_CAP = 512;       // graphs per kernel launch (the host chunks larger batches)
+constexpr int G_CAP = 512;
+constexpr int PROF_SLOTS = 32;   // MD_PROF_SLOTS (include/mdroll.h)       // graphs per kernel launch (the host chunks larger batches)
 
 // Offsets (floats) of each tensor in the packed weight blob (see include/mdroll.h).
 enum WOff : int {
@@ -61,6 +62,7 @@ struct GraphVar {            // mutable per-graph state
   int argmax;                // last prediction: best node (-1 when tied / none)
   int ntie;                  // last prediction: nodes tied at the max
   float qmax, gap;           // last prediction: best Q and top-2 gap
+  int hdmax[2];              // dmax the unit-cost first-layer table was built for (0 = none)
 };
 
 struct Params {
@@ -84,6 +86,8 @@ struct Params {
   float* spart;                    // per tile: [3 sums][2 layers][64] virtual-node partial sums
   float* apart;                    // per tile: arg-max partial {max, second, idx, count}
   float* ybuf;                     // per graph: [2][64] virtual-node embedding after iteration 2
+  float* hbuf;                     // per graph: [144] graph-head hand-off (y, mix, aux)
+  unsigned long long* hflag;       // per graph: step tag of the published graph head
   int* pend;                       // per node slot: host-queued actions
   int* tr_action;                  // per node slot: removal order
   int* tr_rank;                    // per node slot: LMCC after each removal
@@ -93,6 +97,9 @@ struct Params {
   unsigned* bar;                   // grid barrier counter (zeroed per launch)
   const int* glist;                // graphs processed by this launch (<= G_CAP)
   int nglist;
+  int n_env;                       // dedicated environment workgroups (0 = shared mode)
+  unsigned launch_seq;             // launches of this context so far (tags hand-offs)
+  int variant;                     // diagnostics: algorithm variant (MD_VARIANT env, 0 = default)
   int run_mode;                    // RUN_*
   int host_select;                 // 1: every prediction goes to the host (step > 1)
   int* err;                        // device error word (nonzero = failure code)

@@ -1,0 +1,673 @@
+// md_env.h — phase A of the rollout kernel: the MvcEnv step of one graph on one workgroup
+// (cover the chosen node U/mvc_env.py:74-85, the mutual-LMCC fixed point U/Mcc.py:30-38, and
+// the per-step graph features of U/PrepareBatchGraph.py:35-74).  Included by md_kernels.hip.
+//
+// Two storage modes share the code: LDS mode (the graph's edges, states, union-find and
+// degree arrays staged in LDS; every graph of the reference's synthetic sizes) and global mode
+// (arrays in HBM scratch, for graphs too large for one workgroup's LDS).  LDS-mode accesses go
+// through address-space-3 pointers so they compile to ds_* instructions, and edge passes read
+// eight edges per vector load.
+#pragma once
+
+typedef __attribute__((address_space(3))) int lds_i32;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v2u lds_u2;
+typedef __attribute__((address_space(3))) v4u lds_u4;
+
+// Phase-A sub-step timestamps of workgroup 0 (diagnostics; step index stashed in LDS misc[60]).
+#define MD_PROF_A(slot)                                                                          \
+  do {                                                                                           \
+    if (p.prof != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {                              \
+      const int ps_ = ((volatile int*)(lds_base + L_MISC))[60];                                  \
+      if (ps_ < p.prof_cap) p.prof[(size_t)ps_ * PROF_SLOTS + (slot)] = wall_clock64();          \
+    }                                                                                            \
+  } while (0)
+
+// Profile accumulators (slots 16.. of a profiled step; workgroup 0, thread 0 writes).
+enum { PA_ROUNDS = 0, PA_UNITE = 1, PA_LABEL = 2, PA_PRUNE = 3, PA_COUNT = 4, PA_CALLS = 5, PA_COVER = 6 };
+#define PACC(acc, slot, t0)                                                          \
+  do {                                                                               \
+    if ((acc) != nullptr && threadIdx.x == 0) (acc)[slot] += wall_clock64() - (t0);  \
+  } while (0)
+
+// ------------------------------------------------------------------ union-find
+// Parents always point to smaller ids, so the root of a tree is its minimum node id (the
+// canonical label compared across layers).  Lock-free hooking of roots with compare-and-swap.
+template <bool GL>
+__device__ __forceinline__ int uf_load(int* a, int i) {
+  if constexpr (GL) return __hip_atomic_load(a + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return __hip_atomic_load((lds_i32*)(a + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <bool GL>
+__device__ __forceinline__ void uf_store(int* a, int i, int v) {
+  if constexpr (GL) __hip_atomic_store(a + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else __hip_atomic_store((lds_i32*)(a + i), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <bool GL>
+__device__ __forceinline__ int uf_cas(int* a, int i, int expect, int v) {
+  if constexpr (GL) {
+    return atomicCAS(a + i, expect, v);
+  } else {
+    __hip_atomic_compare_exchange_strong((lds_i32*)(a + i), &expect, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+    return expect;
+  }
+}
+template <bool GL>
+__device__ __forceinline__ void uf_add(int* a, int i, int v) {
+  if constexpr (GL) __hip_atomic_fetch_add(a + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else __hip_atomic_fetch_add((lds_i32*)(a + i), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <bool GL>
+__device__ __forceinline__ int uf_find(int* par, int v) {
+  int cur = uf_load<GL>(par, v);
+  if (cur != v) {
+    int prev = v, next;
+    while (cur > (next = uf_load<GL>(par, cur))) {
+      uf_store<GL>(par, prev, next);  // path halving; benign race (values only shrink)
+      prev = cur;
+      cur = next;
+    }
+  }
+  return cur;
+}
+template <bool GL>
+__device__ __forceinline__ void uf_unite(int* par, int a, int b) {
+  while (true) {
+    a = uf_find<GL>(par, a);
+    b = uf_find<GL>(par, b);
+    if (a == b) return;
+    if (a > b) { const int t = a; a = b; b = t; }
+    if (uf_cas<GL>(par, b, b, a) == b) return;
+  }
+}
+
+// ------------------------------------------------------------------ layout and view
+// LDS layout of a graph's environment (words from the start of the phase-A area): the edge
+// region first (u16 endpoints, state, state at the last write-back, covered flags) so a
+// dedicated environment workgroup keeps it across steps, then union-find / degree arrays,
+// the reduction temp and the first-layer-table scratch.
+struct EnvLayout {
+  int ew;                        // words of the edge region
+  int cov;                       // byte offset of the covered flags
+  int par0, par1, deg0, deg1, tmp, total;
+};
+__host__ __device__ inline EnvLayout env_layout(int n, int et) {
+  EnvLayout L;
+  const int e8 = (et + 7) & ~7, e16 = (et + 15) & ~15;
+  L.cov = 4 * e8 + 2 * e16;
+  const int eb = L.cov + ((n + 15) & ~15);
+  L.ew = ((eb + 15) / 16) * 4;
+  L.par0 = L.ew;
+  L.par1 = L.par0 + n;
+  L.deg0 = L.par1 + n;
+  L.deg1 = L.deg0 + n;
+  L.tmp = ((L.deg1 + n + 3) / 4) * 4;
+  L.total = L.tmp + A_TMP_WORDS;
+  return L;
+}
+__host__ __device__ inline bool phase_a_fits_lds(int n, int et) {
+  return env_layout(n, et).total <= A_WORDS && n <= 65535;
+}
+
+// Edge arrays of one graph: LDS-staged (u16 endpoints) or the global arrays themselves.
+template <bool GL>
+struct EnvView {
+  const GraphInfo* gi;
+  int e0, et;                   // edges of layer 0, both layers
+  int variant;
+  lds_u16* u16;                 // LDS mode: endpoints [et]
+  lds_u16* v16;
+  lds_u8* st;                   // LDS mode: edge states [et]
+  lds_u8* st_old;               // LDS mode: edge states at the last write-back
+  lds_u8* cov8;                 // LDS mode: covered flags [n]
+  const int* gu[2];             // global mode
+  const int* gv[2];
+  uint8_t* gst[2];
+  uint8_t* gcov;                // covered flags in HBM (both modes keep them current)
+  int *par0, *par1, *deg0, *deg1;
+  int* tmp;                     // always LDS
+  uint8_t* calive[2];
+  const int* epos[2];
+
+  __device__ __forceinline__ int layer_of(int e) const { return e < e0 ? 0 : 1; }
+  __device__ __forceinline__ int local(int e) const { return e < e0 ? e : e - e0; }
+  __device__ __forceinline__ int u(int e) const {
+    if constexpr (GL) return gu[layer_of(e)][local(e)]; else return u16[e];
+  }
+  __device__ __forceinline__ int v(int e) const {
+    if constexpr (GL) return gv[layer_of(e)][local(e)]; else return v16[e];
+  }
+  __device__ __forceinline__ int state(int e) const {
+    if constexpr (GL) return gst[layer_of(e)][local(e)]; else return st[e];
+  }
+  __device__ __forceinline__ int covered(int x) const {
+    if constexpr (GL) return gcov[x]; else return cov8[x];
+  }
+  // alive -> dead transition (the LDS mode writes back at the end of phase A)
+  __device__ __forceinline__ void kill(int e, uint8_t s) const {
+    if constexpr (GL) {
+      const int l = layer_of(e), k = local(e);
+      gst[l][k] = s;
+      calive[l][epos[l][2 * k]] = 0;
+      calive[l][epos[l][2 * k + 1]] = 0;
+    } else {
+      st[e] = s;
+    }
+  }
+};
+
+__device__ __forceinline__ unsigned sel4(const v4u& w, int i) {
+  return i == 0 ? w.x : i == 1 ? w.y : i == 2 ? w.z : w.w;
+}
+
+// Visits this thread's edges: f(e, u, v, state).  LDS mode reads eight edges per vector load
+// (edge groups g = tid, tid + NTHREADS, ...).
+template <bool GL, class F>
+__device__ __forceinline__ void for_each_edge(const EnvView<GL>& E, F&& f) {
+  if constexpr (GL) {
+    for (int e = threadIdx.x; e < E.et; e += NTHREADS) f(e, E.u(e), E.v(e), E.state(e));
+  } else {
+    const int ng = (E.et + 7) >> 3;
+    for (int g = threadIdx.x; g < ng; g += NTHREADS) {
+      const v4u U = ((const lds_u4*)E.u16)[g];
+      const v4u V = ((const lds_u4*)E.v16)[g];
+      const v2u S = ((const lds_u2*)E.st)[g];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = 8 * g + k;
+        if (e >= E.et) break;
+        const unsigned uw = sel4(U, k >> 1), vw = sel4(V, k >> 1), sw = k < 4 ? S.x : S.y;
+        f(e, (int)((uw >> (16 * (k & 1))) & 0xffffu), (int)((vw >> (16 * (k & 1))) & 0xffffu),
+          (int)((sw >> (8 * (k & 3))) & 0xffu));
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ block reductions (fused)
+// Sums of two ints over the block.  Leading barrier only: the caller must pass another
+// __syncthreads before tmp is written again (every helper here starts with one).
+__device__ __forceinline__ int2 block_sum2(int a, int b, int* tmp) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  __syncthreads();
+  lds_i32* t = (lds_i32*)tmp;
+  if (lane_id() == 0) {
+    t[2 * wave_id()] = a;
+    t[2 * wave_id() + 1] = b;
+  }
+  __syncthreads();
+  int2 r = make_int2(0, 0);
+#pragma unroll
+  for (int w = 0; w < NTHREADS / 64; ++w) {
+    r.x += t[2 * w];
+    r.y += t[2 * w + 1];
+  }
+  return r;
+}
+
+// ------------------------------------------------------------------ unions
+// Union of every alive edge (both layers) into par0 / par1, four unions in flight per thread:
+// each iteration loads the parents of all current endpoints (eight independent LDS loads),
+// then every union advances one hop with path splitting, stops when both ends meet, or hooks
+// root hi -> lo with compare-and-swap (a failed CAS re-reads next iteration).
+template <bool GL>
+__device__ void unite_lockstep(const EnvView<GL>& E) {
+  constexpr int K = 4;
+  int gcur = (int)threadIdx.x - NTHREADS, kk = 8, ge = threadIdx.x;
+  v4u U = (v4u)(0u), V = U;
+  v2u S = (v2u)(0u);
+  const int ngr = (E.et + 7) >> 3;
+  auto feed = [&](int& a, int& b, int& l) -> bool {
+    if constexpr (GL) {
+      while (ge < E.et) {
+        const int e = ge;
+        ge += NTHREADS;
+        if (E.state(e) == E_ALIVE) {
+          a = E.u(e);
+          b = E.v(e);
+          l = e < E.e0 ? 0 : 1;
+          return true;
+        }
+      }
+      return false;
+    } else {
+      while (true) {
+        if (kk == 8) {
+          gcur += NTHREADS;
+          if (gcur >= ngr) return false;
+          U = ((const lds_u4*)E.u16)[gcur];
+          V = ((const lds_u4*)E.v16)[gcur];
+          S = ((const lds_u2*)E.st)[gcur];
+          kk = 0;
+        }
+        const int k = kk++;
+        const int e = 8 * gcur + k;
+        if (e >= E.et) {
+          kk = 8;
+          continue;
+        }
+        const unsigned sw = k < 4 ? S.x : S.y;
+        if (((sw >> (8 * (k & 3))) & 0xffu) != E_ALIVE) continue;
+        const unsigned uw = sel4(U, k >> 1), vw = sel4(V, k >> 1);
+        a = (int)((uw >> (16 * (k & 1))) & 0xffffu);
+        b = (int)((vw >> (16 * (k & 1))) & 0xffffu);
+        l = e < E.e0 ? 0 : 1;
+        return true;
+      }
+    }
+  };
+  int x[K], y[K], xp[K], yp[K], lay[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    int l = -1;
+    lay[k] = feed(x[k], y[k], l) ? l : -1;
+    xp[k] = yp[k] = -1;
+  }
+  while (lay[0] >= 0 || lay[1] >= 0 || lay[2] >= 0 || lay[3] >= 0) {
+    int fx[K], fy[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (lay[k] >= 0) {
+        int* par = lay[k] ? E.par1 : E.par0;
+        fx[k] = uf_load<GL>(par, x[k]);
+        fy[k] = uf_load<GL>(par, y[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (lay[k] < 0) continue;
+      int* par = lay[k] ? E.par1 : E.par0;
+      const bool rx = fx[k] == x[k], ry = fy[k] == y[k];
+      if (!rx) {
+        if (xp[k] >= 0) uf_store<GL>(par, xp[k], fx[k]);  // path splitting
+        xp[k] = x[k];
+        x[k] = fx[k];
+      }
+      if (!ry) {
+        if (yp[k] >= 0) uf_store<GL>(par, yp[k], fy[k]);
+        yp[k] = y[k];
+        y[k] = fy[k];
+      }
+      bool done = x[k] == y[k];
+      if (!done && rx && ry) {
+        const int hi = max(x[k], y[k]), lo = min(x[k], y[k]);
+        done = uf_cas<GL>(par, hi, hi, lo) == hi;
+      }
+      if (done) {
+        int l = -1;
+        lay[k] = feed(x[k], y[k], l) ? l : -1;
+        xp[k] = yp[k] = -1;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ mutual LMCC
+// Mutual-LMCC fixed point (U/Mcc.py:30-38) on the alive edges.  Both layers' components are
+// found simultaneously; while the partitions differ, every alive edge of a layer that crosses
+// the other layer's partition is pruned (both layers per round).  The fixed point (the
+// coarsest partition connected in both layers) and the pruned-edge set equal the reference's
+// alternating order.  Returns the LMCC size (over non-covered nodes); pruned counts in pr[2].
+// Component labels (root ids) go to the degree arrays, free until after the fixed point: a
+// path-halving find may rewrite a parent slot with a non-root ancestor after its owner stored
+// the root, so the parent array itself is not a label map.
+template <bool GL>
+__device__ int mcc_fixed_point(const EnvView<GL>& E, int* pr, unsigned long long* acc) {
+  const int n = E.gi->n;
+  int pruned0 = 0, pruned1 = 0;
+  if (acc != nullptr && threadIdx.x == 0) acc[PA_CALLS] += 1;
+  while (true) {
+    unsigned long long tp = wall_clock64();
+    if (acc != nullptr && threadIdx.x == 0) acc[PA_ROUNDS] += 1;
+    for (int x = threadIdx.x; x < n; x += NTHREADS) {
+      uf_store<GL>(E.par0, x, x);
+      uf_store<GL>(E.par1, x, x);
+    }
+    __syncthreads();
+    if (E.variant & 1) {
+      unite_lockstep<GL>(E);  // experimental (measured slower on gfx950 so far)
+    } else {
+      for_each_edge<GL>(E, [&](int e, int u, int v, int s) {
+        if (s == E_ALIVE) uf_unite<GL>(e < E.e0 ? E.par0 : E.par1, u, v);
+      });
+    }
+    __syncthreads();
+    PACC(acc, PA_UNITE, tp);
+    tp = wall_clock64();
+    int diff = 0;
+    for (int x = threadIdx.x; x < n; x += NTHREADS) {
+      const int r0 = uf_find<GL>(E.par0, x), r1 = uf_find<GL>(E.par1, x);
+      uf_store<GL>(E.deg0, x, r0);
+      uf_store<GL>(E.deg1, x, r1);
+      diff |= (r0 != r1);
+    }
+    diff = __syncthreads_or(diff);
+    PACC(acc, PA_LABEL, tp);
+    tp = wall_clock64();
+    if (!diff) break;
+    int c0 = 0, c1 = 0;
+    for_each_edge<GL>(E, [&](int e, int u, int v, int s) {
+      if (s != E_ALIVE) return;
+      int* other = e < E.e0 ? E.deg1 : E.deg0;  // layer-0 edges are pruned by layer-1 components
+      if (uf_load<GL>(other, u) != uf_load<GL>(other, v)) {
+        E.kill(e, E_PRUNED);
+        if (e < E.e0) c0++; else c1++;
+      }
+    });
+    const int2 c = block_sum2(c0, c1, E.tmp);
+    pruned0 += c.x;
+    pruned1 += c.y;
+    PACC(acc, PA_PRUNE, tp);
+  }
+  const unsigned long long tc = wall_clock64();
+  pr[0] = pruned0;
+  pr[1] = pruned1;
+  for (int x = threadIdx.x; x < n; x += NTHREADS) uf_store<GL>(E.par1, x, 0);
+  __syncthreads();
+  for (int x = threadIdx.x; x < n; x += NTHREADS)
+    if (!E.covered(x)) uf_add<GL>(E.par1, uf_load<GL>(E.deg0, x), 1);
+  __syncthreads();
+  int best = 0;
+  for (int x = threadIdx.x; x < n; x += NTHREADS) best = max(best, uf_load<GL>(E.par1, x));
+  best = block_max_int(best, E.tmp);
+  PACC(acc, PA_COUNT, tc);
+  return best;
+}
+
+// ------------------------------------------------------------------ the environment step
+// Everything phase A does for one graph once the actions to apply are known: cover each
+// queued node and run the fixed point (s0 first if not done), then residual degrees, the
+// ascending live-node list and the per-layer aggregates, the write-back of edge states and
+// the unit-cost first-layer table.  Returns 0 or an ERR_* code.
+template <bool GL>
+__device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, float* area, int pend_n,
+                        int pend_first, const float* lds_base, bool staged) {
+  const int n = gi.n, e0 = gi.e[0], e1 = gi.e[1], et = e0 + e1;
+  EnvView<GL> E;
+  E.gi = &gi;
+  E.e0 = e0;
+  E.et = et;
+  E.variant = p.variant;
+  for (int l = 0; l < 2; ++l) {
+    E.gu[l] = p.eu[l] + gi.eoff[l];
+    E.gv[l] = p.ev[l] + gi.eoff[l];
+    E.gst[l] = p.estate[l] + gi.eoff[l];
+    E.calive[l] = p.calive[l] + gi.coff[l];
+    E.epos[l] = p.epos[l] + 2 * (size_t)gi.eoff[l];
+  }
+  E.gcov = p.covered + gi.node_off;
+  int* ia = (int*)area;
+  if constexpr (GL) {
+    int* gs = p.gscr + 4 * (size_t)gi.node_off;
+    E.par0 = gs;
+    E.par1 = gs + n;
+    E.deg0 = gs + 2 * n;
+    E.deg1 = gs + 3 * n;
+    E.tmp = ia;
+  } else {
+    const EnvLayout L = env_layout(n, et);
+    E.par0 = ia + L.par0;
+    E.par1 = ia + L.par1;
+    E.deg0 = ia + L.deg0;
+    E.deg1 = ia + L.deg1;
+    E.tmp = ia + L.tmp;
+    lds_u8* base8 = (lds_u8*)(uint8_t*)ia;
+    E.u16 = (lds_u16*)base8;
+    E.v16 = E.u16 + ((et + 7) & ~7);
+    E.st = base8 + 4 * ((et + 7) & ~7);
+    E.st_old = E.st + ((et + 15) & ~15);
+    E.cov8 = base8 + L.cov;
+    if (!staged) {
+      // batched so every thread keeps 8 independent global loads in flight
+      for (int e0b = 0; e0b < et; e0b += 8 * NTHREADS) {
+        int uu[8], vv[8], ss[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int e = e0b + k * NTHREADS + threadIdx.x;
+          if (e < et) {
+            const int l = e < e0 ? 0 : 1, kk = e < e0 ? e : e - e0;
+            uu[k] = E.gu[l][kk];
+            vv[k] = E.gv[l][kk];
+            ss[k] = E.gst[l][kk];
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int e = e0b + k * NTHREADS + threadIdx.x;
+          if (e < et) {
+            E.u16[e] = (uint16_t)uu[k];
+            E.v16[e] = (uint16_t)vv[k];
+            E.st[e] = (uint8_t)ss[k];
+            E.st_old[e] = (uint8_t)ss[k];
+          }
+        }
+      }
+      for (int x = threadIdx.x; x < n; x += NTHREADS) E.cov8[x] = E.gcov[x];
+    }
+    __syncthreads();
+  }
+  MD_PROF_A(1);
+  unsigned long long* acc = nullptr;
+  if (p.prof != nullptr && blockIdx.x == 0) {
+    const int ps = ((volatile int*)(lds_base + L_MISC))[60];
+    if (ps < p.prof_cap) acc = p.prof + (size_t)ps * PROF_SLOTS + 16;
+  }
+  int err = 0;
+  for (int k = 0; k < pend_n; ++k) {
+    if (gv.alive[0] == 0 || gv.alive[1] == 0) break;  // terminal between queued actions
+    const int a = k == 0 && pend_first >= 0 ? pend_first : p.pend[gi.node_off + k];
+    if (a < 0 || a >= n) { err = ERR_BADNODE; break; }
+    if (E.covered(a)) { err = ERR_COVERED; break; }
+    // cover a in both layers (U/mvc_env.py:74-85): its alive edges become "covered"
+    const unsigned long long tcv = wall_clock64();
+    int c0 = 0, c1 = 0;
+    for_each_edge<GL>(E, [&](int e, int u, int v, int s) {
+      if (s == E_ALIVE && (u == a || v == a)) {
+        E.kill(e, E_COVERED);
+        if (e < e0) c0++; else c1++;
+      }
+    });
+    const int2 c = block_sum2(c0, c1, E.tmp);
+    if (threadIdx.x == 0) {
+      E.gcov[a] = 1;
+      if constexpr (!GL) E.cov8[a] = 1;
+    }
+    __syncthreads();
+    PACC(acc, PA_COVER, tcv);
+    int pr[2];
+    const int lm = mcc_fixed_point<GL>(E, pr, acc);
+    if (threadIdx.x == 0) {
+      gv.counter[0] += c.x;
+      gv.counter[1] += c.y;
+      gv.removed[0] += pr[0];
+      gv.removed[1] += pr[1];
+      gv.alive[0] -= c.x + pr[0];
+      gv.alive[1] -= c.y + pr[1];
+      gv.n_cov += 1;
+      gv.lmcc = lm;
+      p.tr_action[gi.node_off + gv.steps] = a;
+      p.tr_rank[gi.node_off + gv.steps] = lm;
+      gv.steps += 1;
+    }
+    __syncthreads();
+  }
+  if (!gv.s0_done && !err) {
+    int pr[2];
+    const int lm = mcc_fixed_point<GL>(E, pr, acc);
+    if (threadIdx.x == 0) {
+      gv.removed[0] += pr[0];
+      gv.removed[1] += pr[1];
+      gv.max_rank = lm;
+      gv.lmcc = lm;
+      gv.s0_done = 1;
+    }
+  }
+  MD_PROF_A(2);
+  // residual degrees by edge-parallel atomics
+  for (int x = threadIdx.x; x < n; x += NTHREADS) {
+    uf_store<GL>(E.deg0, x, 0);
+    uf_store<GL>(E.deg1, x, 0);
+  }
+  __syncthreads();
+  for_each_edge<GL>(E, [&](int e, int u, int v, int s) {
+    if (s != E_ALIVE) return;
+    int* d = e < e0 ? E.deg0 : E.deg1;
+    uf_add<GL>(d, u, 1);
+    uf_add<GL>(d, v, 1);
+  });
+  __syncthreads();
+  // live list (ascending ids), per-layer aggregates (U/PrepareBatchGraph.py:35-74): one
+  // fused block exchange for the scan and all reductions
+  const int chunk = (n + NTHREADS - 1) / NTHREADS;
+  const int x0 = min(n, (int)threadIdx.x * chunk), x1 = min(n, x0 + chunk);
+  int nlive = 0, dm0 = 0, dm1 = 0, sd0 = 0, sd1 = 0, bad = 0;
+  long long th0 = 0, th1 = 0;
+  float* q = p.q + gi.node_off;
+  int* gdeg0 = p.deg[0] + gi.node_off;
+  int* gdeg1 = p.deg[1] + gi.node_off;
+  for (int x = x0; x < x1; ++x) {
+    const int d0 = uf_load<GL>(E.deg0, x), d1 = uf_load<GL>(E.deg1, x);
+    gdeg0[x] = d0;
+    gdeg1[x] = d1;
+    q[x] = NEG_INF;
+    bad |= ((d0 > 0) != (d1 > 0));
+    if (d0 > 0) {
+      nlive++;
+      dm0 = max(dm0, d0);
+      dm1 = max(dm1, d1);
+      th0 += (long long)d0 * (d0 - 1) / 2;
+      th1 += (long long)d1 * (d1 - 1) / 2;
+    }
+    sd0 += d0;
+    sd1 += d1;
+  }
+  int tot = 0, base = 0;
+  {
+    const int lane = lane_id(), w = wave_id();
+    int incl = nlive;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    int r_nl = nlive, r_m0 = dm0, r_m1 = dm1, r_s0 = sd0, r_s1 = sd1, r_bad = bad;
+    long long r_t0 = th0, r_t1 = th1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      r_nl += __shfl_xor(r_nl, o, 64);
+      r_m0 = max(r_m0, __shfl_xor(r_m0, o, 64));
+      r_m1 = max(r_m1, __shfl_xor(r_m1, o, 64));
+      r_s0 += __shfl_xor(r_s0, o, 64);
+      r_s1 += __shfl_xor(r_s1, o, 64);
+      r_bad |= __shfl_xor(r_bad, o, 64);
+      r_t0 += __shfl_xor(r_t0, o, 64);
+      r_t1 += __shfl_xor(r_t1, o, 64);
+    }
+    __syncthreads();
+    lds_i32* t = (lds_i32*)E.tmp;  // 12 words per wave
+    if (lane == 0) {
+      t[12 * w + 0] = r_nl;
+      t[12 * w + 1] = r_m0;
+      t[12 * w + 2] = r_m1;
+      t[12 * w + 3] = r_s0;
+      t[12 * w + 4] = r_s1;
+      t[12 * w + 5] = r_bad;
+      t[12 * w + 6] = (int)(r_t0 & 0xffffffffll);
+      t[12 * w + 7] = (int)(r_t0 >> 32);
+      t[12 * w + 8] = (int)(r_t1 & 0xffffffffll);
+      t[12 * w + 9] = (int)(r_t1 >> 32);
+    }
+    __syncthreads();
+    dm0 = dm1 = sd0 = sd1 = bad = 0;
+    th0 = th1 = 0;
+    int before = 0;
+#pragma unroll
+    for (int i = 0; i < NTHREADS / 64; ++i) {
+      const int nl_i = t[12 * i];
+      if (i < w) before += nl_i;
+      tot += nl_i;
+      dm0 = max(dm0, (int)t[12 * i + 1]);
+      dm1 = max(dm1, (int)t[12 * i + 2]);
+      sd0 += t[12 * i + 3];
+      sd1 += t[12 * i + 4];
+      bad |= t[12 * i + 5];
+      th0 += (long long)(((unsigned long long)(unsigned)t[12 * i + 7] << 32) | (unsigned)t[12 * i + 6]);
+      th1 += (long long)(((unsigned long long)(unsigned)t[12 * i + 9] << 32) | (unsigned)t[12 * i + 8]);
+    }
+    base = before + incl - nlive;
+  }
+  {
+    int k = base;
+    int* lv = p.live + gi.node_off;
+    for (int x = x0; x < x1; ++x)
+      if (uf_load<GL>(E.deg0, x) > 0) lv[k++] = x;
+  }
+  if (bad && !err) err = ERR_LIVE_MISMATCH;
+  const int hd0 = gv.hdmax[0], hd1 = gv.hdmax[1];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    gv.n_live = tot;
+    gv.dmax[0] = dm0;
+    gv.dmax[1] = dm1;
+    gv.alive[0] = sd0 / 2;
+    gv.alive[1] = sd1 / 2;
+    gv.twohop[0] = th0;
+    gv.twohop[1] = th1;
+  }
+  if constexpr (!GL) {
+    // write back changed edge states; dead edges drop out of the gather's CSR view
+    const int ng8 = (et + 7) >> 3;
+    for (int g = threadIdx.x; g < ng8; g += NTHREADS) {
+      const v2u S = ((const lds_u2*)E.st)[g], O = ((const lds_u2*)E.st_old)[g];
+      if (S.x == O.x && S.y == O.y) continue;
+      ((lds_u2*)E.st_old)[g] = S;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = 8 * g + k;
+        const unsigned s = ((k < 4 ? S.x : S.y) >> (8 * (k & 3))) & 0xffu;
+        const unsigned o = ((k < 4 ? O.x : O.y) >> (8 * (k & 3))) & 0xffu;
+        if (e < et && s != o) {
+          const int l = e < e0 ? 0 : 1, kk = e < e0 ? e : e - e0;
+          E.gst[l][kk] = (uint8_t)s;
+          E.calive[l][E.epos[l][2 * kk]] = 0;
+          E.calive[l][E.epos[l][2 * kk + 1]] = 0;
+        }
+      }
+    }
+  }
+  MD_PROF_A(14);
+  // First-layer embedding by degree (unit cost): X = [d/dmax, d/dmax] (net :252-261),
+  // normalize(relu(X . w_n2l)) with the 2-term FMA chain of MKL's sgemm; one wave per row
+  // d = 1..dmax.  The table depends on dmax only, so it is rebuilt only when dmax changed.
+  if (p.node_w == nullptr) {
+    const float* wn = p.w + W_N2L;
+    const int lane = lane_id(), w = wave_id();
+    const float w0 = wn[lane], w1 = wn[64 + lane];
+    for (int l = 0; l < 2; ++l) {
+      const int dm = l ? dm1 : dm0;
+      if (dm == (l ? hd1 : hd0)) continue;
+      float* tab = p.h0tab[l] + (size_t)gi.node_off * EMB;  // degrees <= n-1 fit the graph's rows
+      for (int d = 1 + w; d <= dm; d += NTHREADS / 64) {
+        const float f = (float)d / (float)dm;
+        const float x = fmaxf(fmaf(f, w1, fmaf(f, w0, 0.f)), 0.f);
+        const float nr = wave_norm64(x);
+        tab[(size_t)d * EMB + lane] = x / fmaxf(nr, 1e-12f);
+      }
+    }
+    if (threadIdx.x == 0) {
+      gv.hdmax[0] = dm0;
+      gv.hdmax[1] = dm1;
+    }
+  }
+  __syncthreads();
+  MD_PROF_A(15);
+  return err;
+}

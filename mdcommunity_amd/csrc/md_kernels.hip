@@ -214,433 +214,60 @@ __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* tot) {
   return base + x - v;
 }
 
-// ------------------------------------------------------------------ union-find
-// Parents always point to smaller ids, so the root of a component is its minimum node id
-// (the canonical label compared across layers).  Lock-free hooking with atomicCAS.
-template <bool GL>
-__device__ __forceinline__ int uf_load(int* par, int i) {
-  if constexpr (GL) {
-    return __hip_atomic_load(par + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#include "md_env.h"
+
+// Merge arg-max partial (m2, s2, i2, c2) into (bm, bs, bi, bc); c = 0 marks an empty partial.
+__device__ __forceinline__ void argmax_combine(float& bm, float& bs, int& bi, int& bc, float m2, float s2,
+                                               int i2, int c2) {
+  if (bc == 0) {
+    bm = m2; bs = s2; bi = i2; bc = c2;
+  } else if (m2 > bm) {
+    bs = fmaxf(bm, s2);
+    bm = m2; bi = i2; bc = c2;
+  } else if (m2 == bm) {
+    bc += c2;
+    bi = min(bi, i2);
+    bs = fmaxf(bs, s2);
   } else {
-    return *((volatile int*)(par + i));
+    bs = fmaxf(bs, m2);
   }
-}
-template <bool GL>
-__device__ __forceinline__ void uf_store(int* par, int i, int v) {
-  if constexpr (GL) {
-    __hip_atomic_store(par + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    *((volatile int*)(par + i)) = v;
-  }
-}
-template <bool GL>
-__device__ __forceinline__ int uf_find(int* par, int v) {
-  int cur = uf_load<GL>(par, v);
-  if (cur != v) {
-    int prev = v, next;
-    while (cur > (next = uf_load<GL>(par, cur))) {
-      uf_store<GL>(par, prev, next);  // path halving; benign race (values only shrink)
-      prev = cur;
-      cur = next;
-    }
-  }
-  return cur;
-}
-template <bool GL>
-__device__ __forceinline__ void uf_unite(int* par, int a, int b) {
-  while (true) {
-    a = uf_find<GL>(par, a);
-    b = uf_find<GL>(par, b);
-    if (a == b) return;
-    if (a > b) { const int t = a; a = b; b = t; }
-    const int old = atomicCAS(par + b, b, a);
-    if (old == b) return;
-  }
-}
-
-// Phase-A sub-step timestamps of workgroup 0 (diagnostics; step index stashed in LDS misc[60]).
-#define MD_PROF_A(slot)                                                                          \
-  do {                                                                                           \
-    if (p.prof != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {                              \
-      const int ps_ = ((volatile int*)(lds_base + L_MISC))[60];                                  \
-      if (ps_ < p.prof_cap) p.prof[(size_t)ps_ * 16 + (slot)] = wall_clock64();                  \
-    }                                                                                            \
-  } while (0)
-
-// ------------------------------------------------------------------ phase A (environment)
-// Edge arrays of one graph: LDS-staged (u16 endpoints) or the global arrays themselves.
-template <bool GL>
-struct EnvView {
-  const GraphInfo* gi;
-  int e0, et;                   // edges of layer 0, both layers
-  const uint16_t* u16;          // LDS mode: endpoints [et]
-  const uint16_t* v16;
-  uint8_t* st;                  // LDS mode: edge states [et]
-  uint8_t* st_old;              // LDS mode: edge states at the start of phase A
-  const int* gu[2];             // global mode
-  const int* gv[2];
-  uint8_t* gst[2];
-  int *par0, *par1, *deg0, *deg1;
-  int* tmp;
-  uint8_t* calive[2];
-  const int* epos[2];
-
-  __device__ __forceinline__ int layer_of(int e) const { return e < e0 ? 0 : 1; }
-  __device__ __forceinline__ int local(int e) const { return e < e0 ? e : e - e0; }
-  __device__ __forceinline__ int u(int e) const {
-    if constexpr (GL) return gu[layer_of(e)][local(e)]; else return u16[e];
-  }
-  __device__ __forceinline__ int v(int e) const {
-    if constexpr (GL) return gv[layer_of(e)][local(e)]; else return v16[e];
-  }
-  __device__ __forceinline__ uint8_t state(int e) const {
-    if constexpr (GL) return gst[layer_of(e)][local(e)]; else return st[e];
-  }
-  // alive -> dead transition (the LDS mode writes back at the end of phase A)
-  __device__ __forceinline__ void kill(int e, uint8_t s) const {
-    if constexpr (GL) {
-      const int l = layer_of(e), k = local(e);
-      gst[l][k] = s;
-      calive[l][epos[l][2 * k]] = 0;
-      calive[l][epos[l][2 * k + 1]] = 0;
-    } else {
-      st[e] = s;
-    }
-  }
-};
-
-// Mutual-LMCC fixed point (U/Mcc.py:30-38) on the alive edges.  Both layers' components are
-// found simultaneously; while the partitions differ, every alive edge of a layer that crosses
-// the other layer's partition is pruned (both layers per round).  The fixed point (the
-// coarsest partition connected in both layers) and the pruned-edge set equal the reference's
-// alternating order.  Returns the LMCC size (over non-covered nodes); pruned counts in pr[2].
-template <bool GL>
-__device__ int mcc_fixed_point(const EnvView<GL>& E, const uint8_t* cov, int* pr) {
-  const int n = E.gi->n;
-  int pruned0 = 0, pruned1 = 0;
-  while (true) {
-    for (int x = threadIdx.x; x < n; x += NTHREADS) {
-      uf_store<GL>(E.par0, x, x);
-      uf_store<GL>(E.par1, x, x);
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < E.et; e += NTHREADS)
-      if (E.state(e) == E_ALIVE) uf_unite<GL>(e < E.e0 ? E.par0 : E.par1, E.u(e), E.v(e));
-    __syncthreads();
-    int diff = 0;
-    for (int x = threadIdx.x; x < n; x += NTHREADS) {
-      const int r0 = uf_find<GL>(E.par0, x), r1 = uf_find<GL>(E.par1, x);
-      uf_store<GL>(E.par0, x, r0);
-      uf_store<GL>(E.par1, x, r1);
-      diff |= (r0 != r1);
-    }
-    diff = __syncthreads_or(diff);
-    if (!diff) break;
-    int c0 = 0, c1 = 0;
-    for (int e = threadIdx.x; e < E.et; e += NTHREADS) {
-      if (E.state(e) != E_ALIVE) continue;
-      int* other = e < E.e0 ? E.par1 : E.par0;  // layer-0 edges are pruned by layer-1 components
-      if (uf_load<GL>(other, E.u(e)) != uf_load<GL>(other, E.v(e))) {
-        E.kill(e, E_PRUNED);
-        if (e < E.e0) c0++; else c1++;
-      }
-    }
-    pruned0 += block_sum_int(c0, E.tmp);
-    pruned1 += block_sum_int(c1, E.tmp);
-  }
-  pr[0] = pruned0;
-  pr[1] = pruned1;
-  for (int x = threadIdx.x; x < n; x += NTHREADS) uf_store<GL>(E.par1, x, 0);
-  __syncthreads();
-  for (int x = threadIdx.x; x < n; x += NTHREADS)
-    if (!cov[x]) atomicAdd(E.par1 + uf_load<GL>(E.par0, x), 1);
-  __syncthreads();
-  int best = 0;
-  for (int x = threadIdx.x; x < n; x += NTHREADS) best = max(best, uf_load<GL>(E.par1, x));
-  return block_max_int(best, E.tmp);
-}
-
-// Everything phase A does for one graph once the actions to apply are known.
-// Returns 0 or an ERR_* code.
-template <bool GL>
-__device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, float* area, int pend_n,
-                        int pend_first, const float* lds_base) {
-  const int n = gi.n, e0 = gi.e[0], e1 = gi.e[1], et = e0 + e1;
-  EnvView<GL> E;
-  E.gi = &gi;
-  E.e0 = e0;
-  E.et = et;
-  for (int l = 0; l < 2; ++l) {
-    E.gu[l] = p.eu[l] + gi.eoff[l];
-    E.gv[l] = p.ev[l] + gi.eoff[l];
-    E.gst[l] = p.estate[l] + gi.eoff[l];
-    E.calive[l] = p.calive[l] + gi.coff[l];
-    E.epos[l] = p.epos[l] + 2 * (size_t)gi.eoff[l];
-  }
-  int* ia = (int*)area;
-  if constexpr (GL) {
-    int* gs = p.gscr + 4 * (size_t)gi.node_off;
-    E.par0 = gs;
-    E.par1 = gs + n;
-    E.deg0 = gs + 2 * n;
-    E.deg1 = gs + 3 * n;
-    E.tmp = ia;
-  } else {
-    E.par0 = ia;
-    E.par1 = ia + n;
-    E.deg0 = ia + 2 * n;
-    E.deg1 = ia + 3 * n;
-    E.tmp = ia + 4 * n;
-    uint16_t* u16 = (uint16_t*)(ia + 4 * n + A_TMP_WORDS);
-    uint16_t* v16 = u16 + ((et + 7) & ~7);
-    uint8_t* st = (uint8_t*)(v16 + ((et + 7) & ~7));
-    uint8_t* st_old = st + ((et + 15) & ~15);
-    E.u16 = u16;
-    E.v16 = v16;
-    E.st = st;
-    E.st_old = st_old;
-    // batched so every thread keeps 8 independent loads in flight
-    for (int e0b = 0; e0b < et; e0b += 8 * NTHREADS) {
-      int uu[8], vv[8];
-      uint8_t ss[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int e = e0b + k * NTHREADS + threadIdx.x;
-        if (e < et) {
-          const int l = e < e0 ? 0 : 1, kk = e < e0 ? e : e - e0;
-          uu[k] = E.gu[l][kk];
-          vv[k] = E.gv[l][kk];
-          ss[k] = E.gst[l][kk];
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int e = e0b + k * NTHREADS + threadIdx.x;
-        if (e < et) {
-          u16[e] = (uint16_t)uu[k];
-          v16[e] = (uint16_t)vv[k];
-          st[e] = ss[k];
-          st_old[e] = ss[k];
-        }
-      }
-    }
-    __syncthreads();
-  }
-  MD_PROF_A(1);
-  uint8_t* cov = p.covered + gi.node_off;
-  int err = 0;
-  for (int k = 0; k < pend_n; ++k) {
-    if (gv.alive[0] == 0 || gv.alive[1] == 0) break;  // terminal between queued actions
-    const int a = k == 0 && pend_first >= 0 ? pend_first : p.pend[gi.node_off + k];
-    if (a < 0 || a >= n) { err = ERR_BADNODE; break; }
-    if (cov[a]) { err = ERR_COVERED; break; }
-    // cover a in both layers (U/mvc_env.py:74-85): its alive edges become "covered"
-    int c0 = 0, c1 = 0;
-    for (int e = threadIdx.x; e < et; e += NTHREADS) {
-      if (E.state(e) == E_ALIVE && (E.u(e) == a || E.v(e) == a)) {
-        E.kill(e, E_COVERED);
-        if (e < e0) c0++; else c1++;
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) cov[a] = 1;
-    c0 = block_sum_int(c0, E.tmp);
-    c1 = block_sum_int(c1, E.tmp);
-    __syncthreads();
-    int pr[2];
-    const int lm = mcc_fixed_point<GL>(E, cov, pr);
-    if (threadIdx.x == 0) {
-      gv.counter[0] += c0;
-      gv.counter[1] += c1;
-      gv.removed[0] += pr[0];
-      gv.removed[1] += pr[1];
-      gv.alive[0] -= c0 + pr[0];
-      gv.alive[1] -= c1 + pr[1];
-      gv.n_cov += 1;
-      gv.lmcc = lm;
-      p.tr_action[gi.node_off + gv.steps] = a;
-      p.tr_rank[gi.node_off + gv.steps] = lm;
-      gv.steps += 1;
-    }
-    __syncthreads();
-  }
-  if (!gv.s0_done && !err) {
-    int pr[2];
-    const int lm = mcc_fixed_point<GL>(E, cov, pr);
-    if (threadIdx.x == 0) {
-      gv.removed[0] += pr[0];
-      gv.removed[1] += pr[1];
-      gv.max_rank = lm;
-      gv.lmcc = lm;
-      gv.s0_done = 1;
-    }
-  }
-  MD_PROF_A(2);
-  // residual degrees by edge-parallel atomics
-  for (int x = threadIdx.x; x < n; x += NTHREADS) {
-    uf_store<GL>(E.deg0, x, 0);
-    uf_store<GL>(E.deg1, x, 0);
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < et; e += NTHREADS) {
-    if (E.state(e) != E_ALIVE) continue;
-    int* d = e < e0 ? E.deg0 : E.deg1;
-    atomicAdd(d + E.u(e), 1);
-    atomicAdd(d + E.v(e), 1);
-  }
-  __syncthreads();
-  // live list (ascending ids), per-layer aggregates (U/PrepareBatchGraph.py:35-74)
-  const int chunk = (n + NTHREADS - 1) / NTHREADS;
-  const int x0 = min(n, (int)threadIdx.x * chunk), x1 = min(n, x0 + chunk);
-  int nlive = 0, dm0 = 0, dm1 = 0, sd0 = 0, sd1 = 0, bad = 0;
-  long long th0 = 0, th1 = 0;
-  float* q = p.q + gi.node_off;
-  int* gdeg0 = p.deg[0] + gi.node_off;
-  int* gdeg1 = p.deg[1] + gi.node_off;
-  for (int x = x0; x < x1; ++x) {
-    const int d0 = uf_load<GL>(E.deg0, x), d1 = uf_load<GL>(E.deg1, x);
-    gdeg0[x] = d0;
-    gdeg1[x] = d1;
-    q[x] = NEG_INF;
-    bad |= ((d0 > 0) != (d1 > 0));
-    if (d0 > 0) {
-      nlive++;
-      dm0 = max(dm0, d0);
-      dm1 = max(dm1, d1);
-      th0 += (long long)d0 * (d0 - 1) / 2;
-      th1 += (long long)d1 * (d1 - 1) / 2;
-    }
-    sd0 += d0;
-    sd1 += d1;
-  }
-  int tot = 0;
-  const int base = block_excl_scan(nlive, E.tmp, &tot);
-  {
-    int k = base;
-    int* lv = p.live + gi.node_off;
-    for (int x = x0; x < x1; ++x)
-      if (uf_load<GL>(E.deg0, x) > 0) lv[k++] = x;
-  }
-  dm0 = block_max_int(dm0, E.tmp);
-  dm1 = block_max_int(dm1, E.tmp);
-  sd0 = block_sum_int(sd0, E.tmp);
-  sd1 = block_sum_int(sd1, E.tmp);
-  th0 = block_sum_ll(th0, (long long*)E.tmp);
-  th1 = block_sum_ll(th1, (long long*)E.tmp);
-  bad = __syncthreads_or(bad);
-  if (bad && !err) err = ERR_LIVE_MISMATCH;
-  if (threadIdx.x == 0) {
-    gv.n_live = tot;
-    gv.dmax[0] = dm0;
-    gv.dmax[1] = dm1;
-    gv.alive[0] = sd0 / 2;
-    gv.alive[1] = sd1 / 2;
-    gv.twohop[0] = th0;
-    gv.twohop[1] = th1;
-  }
-  if constexpr (!GL) {
-    // write back edge states; dead edges drop out of the gather's CSR view
-    for (int e = threadIdx.x; e < et; e += NTHREADS) {
-      const int l = e < e0 ? 0 : 1, k = e < e0 ? e : e - e0;
-      const uint8_t s = E.st[e];
-      if (s != E.st_old[e]) {
-        E.gst[l][k] = s;
-        E.calive[l][E.epos[l][2 * k]] = 0;
-        E.calive[l][E.epos[l][2 * k + 1]] = 0;
-      }
-    }
-  }
-  __syncthreads();
-  MD_PROF_A(14);
-  // First-layer embedding by degree (unit cost): X = [d/dmax, d/dmax] (net :252-261),
-  // normalize(relu(X . w_n2l)) with the 2-term FMA chain of MKL's sgemm; rows d = 1..dmax,
-  // 64 rows at a time in LDS.
-  if (p.node_w == nullptr) {
-    float* xs = area;             // [64][65]
-    float* red = area + 64 * 65;  // [64][8]
-    const float* wn = p.w + W_N2L;
-    const int c = threadIdx.x & 63, r8 = threadIdx.x >> 6;
-    const float w0 = wn[c], w1 = wn[64 + c];
-    for (int l = 0; l < 2; ++l) {
-      const int dm = l ? dm1 : dm0;
-      float* tab = p.h0tab[l] + (size_t)gi.node_off * EMB;  // degrees <= n-1 fit the graph's rows
-      for (int d0 = 1; d0 <= dm; d0 += 64) {
-        for (int r = r8; r < 64; r += NTHREADS / 64) {
-          const int d = d0 + r;
-          float x = 0.f;
-          if (d <= dm) {
-            const float f = (float)d / (float)dm;
-            x = fmaxf(fmaf(f, w1, fmaf(f, w0, 0.f)), 0.f);
-          }
-          xs[r * 65 + c] = x;
-        }
-        __syncthreads();
-        {
-          const int r = threadIdx.x >> 3, j = threadIdx.x & 7;
-          float acc = 0.f;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const float v = xs[r * 65 + 8 * i + j];
-            acc = fmaf(v, v, acc);
-          }
-          red[r * 8 + j] = acc;
-        }
-        __syncthreads();
-        for (int r = r8; r < 64; r += NTHREADS / 64) {
-          const int d = d0 + r;
-          if (d > dm) break;
-          const float den = fmaxf(sqrtf(sumsq8_finish(red + r * 8)), 1e-12f);
-          tab[(size_t)d * EMB + c] = xs[r * 65 + c] / den;
-        }
-        __syncthreads();
-      }
-    }
-  }
-  MD_PROF_A(15);
-  return err;
-}
-
-// Must agree with the staging layout of env_step<false>: par/deg 4n words, temp, u16/v16
-// endpoints, edge states and their phase-start copy.
-__host__ __device__ inline bool phase_a_fits_lds(int n, int et) {
-  const size_t bytes = 4 * (4 * (size_t)n + A_TMP_WORDS) + (size_t)((et + 7) & ~7) * 4 + 2 * (size_t)((et + 15) & ~15) + 64;
-  return bytes <= 4 * (size_t)A_WORDS && n <= 65535;
 }
 
 // Phase A of one graph: reduce the previous prediction, then apply / MCC / features.
-__device__ __noinline__ void phase_a(const Params& p, int g, bool have_q, float* lds) {
+__device__ __noinline__ bool phase_a(const Params& p, int g, bool have_q, float* lds, bool staged) {
   GraphVar& gv = *(GraphVar*)(lds + L_GV);
   int* misc = (int*)(lds + L_MISC);
   const GraphInfo gi = p.ginfo[g];
-  if (threadIdx.x == 0) gv = p.gvar[g];
+  // a dedicated environment workgroup that already stepped this graph in this launch holds
+  // its current GraphVar in LDS (nobody else writes it during a launch)
+  if (threadIdx.x == 0 && !(staged && p.n_env > 0)) gv = p.gvar[g];
   __syncthreads();
-  if (gv.status != ST_RUN) return;
+  if (gv.status != ST_RUN) return staged;
   int pend_n = 0, pend_first = -1;
   bool stop = false;
   if (have_q) {
-    if (threadIdx.x == 0) {
-      // arg-max over the graph's tile partials, in tile order
-      float bm = NEG_INF, bs = NEG_INF;
-      int bi = 0x7fffffff, bc = 0;
+    float bm = NEG_INF, bs = NEG_INF;
+    int bi = 0x7fffffff, bc = 0;
+    if (threadIdx.x < 64) {
+      // arg-max over the graph's tile partials {max, second, min index at max, count at max}:
+      // lanes combine strided tiles, then a butterfly; every combine step is max / min / sum,
+      // so the result does not depend on the order.
+      const int lane = threadIdx.x;
       const int nt = (gv.n_live + TILE - 1) / TILE;
-      for (int j = 0; j < nt; ++j) {
-        const float* ap = p.apart + (size_t)(gi.tile_off + j) * 4;
-        const float m = ap[0], s = ap[1];
-        const int i = __float_as_int(ap[2]), c = __float_as_int(ap[3]);
+      for (int j = lane; j < nt; j += 64) {
+        const float4 ap = *(const float4*)(p.apart + (size_t)(gi.tile_off + j) * 4);
+        const int c = __float_as_int(ap.w);
         if (c == 0) continue;
-        if (m > bm) {
-          bs = fmaxf(bm, s);
-          bm = m;
-          bi = i;
-          bc = c;
-        } else if (m == bm) {
-          bc += c;
-          bi = min(bi, i);
-          bs = fmaxf(bs, s);
-        } else {
-          bs = fmaxf(bs, m);
-        }
+        argmax_combine(bm, bs, bi, bc, ap.x, ap.y, __float_as_int(ap.z), c);
       }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float m2 = __shfl_xor(bm, o, 64), s2 = __shfl_xor(bs, o, 64);
+        const int i2 = __shfl_xor(bi, o, 64), c2 = __shfl_xor(bc, o, 64);
+        if (c2 != 0) argmax_combine(bm, bs, bi, bc, m2, s2, i2, c2);
+      }
+    }
+    if (threadIdx.x == 0) {
       const int t = gv.npred;
       if (t < gi.n) {
         int* ts = p.tr_stat + (size_t)(gi.node_off + t) * 4;
@@ -678,8 +305,10 @@ __device__ __noinline__ void phase_a(const Params& p, int g, bool have_q, float*
     const int et = gi.e[0] + gi.e[1];
     const bool fits = phase_a_fits_lds(gi.n, et);
     float* area = lds + L_W;
-    const int err = fits ? env_step<false>(p, gi, gv, area, pend_n, pend_first, lds)
-                         : env_step<true>(p, gi, gv, area, pend_n, pend_first, lds);
+    const bool was_staged = staged && fits;
+    staged = fits;
+    const int err = fits ? env_step<false>(p, gi, gv, area, pend_n, pend_first, lds, was_staged)
+                         : env_step<true>(p, gi, gv, area, pend_n, pend_first, lds, false);
     if (threadIdx.x == 0) {
       gv.npend = 0;
       if (err) set_err(p, err);
@@ -692,6 +321,7 @@ __device__ __noinline__ void phase_a(const Params& p, int g, bool have_q, float*
   __syncthreads();
   if (threadIdx.x == 0) p.gvar[g] = gv;
   __syncthreads();
+  return staged;
 }
 
 // ------------------------------------------------------------------ tile pieces
@@ -980,10 +610,70 @@ __device__ __noinline__ void graph_head(const Params& p, float* lds, float* scr,
   __syncthreads();
 }
 
+// ------------------------------------------------------------------ graph-head hand-off
+// Dedicated mode: the graph-head workgroup publishes y (L_YS, 128 floats) and the graph
+// scalars (L_GS, 16) of graph g, then a 64-bit step tag; tile workgroups wait for the tag and
+// copy the 144 floats.  Payload and tag use agent-scope (sc1) stores and loads on both sides,
+// one signalling lane after every storing wave drained and a workgroup barrier
+// (MI355X_MICROARCH.md, inter-workgroup visibility, first table row), so no L2 write-back or
+// L1 invalidate is needed.
+constexpr int HB_FLOATS = 144;
+__device__ __forceinline__ void head_publish(const Params& p, const float* lds, int g, unsigned long long htag) {
+  if (threadIdx.x < HB_FLOATS)
+    __hip_atomic_store(p.hbuf + (size_t)g * HB_FLOATS + threadIdx.x, lds[L_YS + threadIdx.x], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(p.hflag + g, htag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void head_receive(const Params& p, float* lds, int g, unsigned long long htag) {
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = wall_clock64();
+    while (__hip_atomic_load(p.hflag + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != htag) {
+      if (__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > BARRIER_TIMEOUT_TICKS) {
+        __hip_atomic_store(p.err, ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < HB_FLOATS)
+    lds[L_YS + threadIdx.x] =
+        __hip_atomic_load(p.hbuf + (size_t)g * HB_FLOATS + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+}
+
+// One iteration of the graph-head workgroup (dedicated mode) for graph g: it == 2 builds
+// Y1, Y2 from the S0 / S1 tile partials of iteration 1; it == 3 builds Y3 from S2, runs the
+// graph head and publishes it.  Same arithmetic as the shared-mode path in the tile loop.
+__device__ __noinline__ void head_iteration(const Params& p, float* lds, float* scr, int g, int it,
+                                            unsigned long long htag) {
+  const GraphInfo gi = p.ginfo[g];
+  const GraphVar gv = p.gvar[g];
+  if (gv.status != ST_RUN) return;
+  const int nt = (gv.n_live + TILE - 1) / TILE;
+  float* sbuf = scr + S_HID;  // [2][64]
+  float* yw = lds + L_YW;
+  if (it == 2) {
+    if (threadIdx.x < 128) yw[threadIdx.x] = lds[L_Y0 + (threadIdx.x & 63)];
+    graph_sum(p, gi, nt, 0, sbuf, scr + S_YP);
+    vrow_update(lds + L_W, scr, sbuf, yw);  // Y1 from S0
+    graph_sum(p, gi, nt, 1, sbuf, scr + S_YP);
+    vrow_update(lds + L_W, scr, sbuf, yw);  // Y2 from S1
+  } else {
+    graph_sum(p, gi, nt, 2, sbuf, scr + S_YP);
+    vrow_update(lds + L_W, scr, sbuf, yw);  // Y3 from S2
+    graph_head(p, lds, scr, gi, gv);
+    head_publish(p, lds, g, htag);
+  }
+}
+
 // Attention + Q head for one tile whose final embeddings are in S_E (both layers).
 // Writes q for valid rows and this tile's arg-max partial.
-__device__ __noinline__ void attention_q_tile(const Params& p, const float* lds, float* scr, const GraphInfo& gi,
-                                              const int* rows, float* apart_out) {
+__device__ __noinline__ void attention_q_tile(const Params& p, float* lds, float* scr, const GraphInfo& gi, int g,
+                                              const int* rows, float* apart_out, unsigned long long htag) {
   const float* wi = lds + L_W;
   const int w = wave_id(), l = w >> 2, cb = w & 3, lane = lane_id();
   const int ar = lane & 15, ak = lane >> 4;
@@ -1023,6 +713,7 @@ __device__ __noinline__ void attention_q_tile(const Params& p, const float* lds,
   __syncthreads();
   normalize_tile(scr + S_E, scr);
   __syncthreads();
+  if (htag != 0ull) head_receive(p, lds, g, htag);
   {
     // e[a] = sum_b (h[a] * y[b]) * cp[b]: the reference's outer product then x cross_product
     // (net :356-363), a batched [64,64]x[64,1] matmul = an FMA chain over b.
@@ -1092,7 +783,7 @@ __device__ __noinline__ void attention_q_tile(const Params& p, const float* lds,
 #define MD_PROF(slot)                                                                            \
   do {                                                                                           \
     if (p.prof != nullptr && blockIdx.x == 0 && threadIdx.x == 0 && pstep < p.prof_cap)          \
-      p.prof[(size_t)pstep * 16 + (slot)] = wall_clock64();                                      \
+      p.prof[(size_t)pstep * PROF_SLOTS + (slot)] = wall_clock64();                                      \
   } while (0)
 
 __device__ __forceinline__ void load_weights(float* dst, const float* src) {
@@ -1130,32 +821,49 @@ __global__ void __launch_bounds__(NTHREADS, 1) md_rollout_kernel(Params p, const
   int* pref = (int*)(lds + L_PREF);
   int* rows = (int*)(scr + S_ROW);
 
-  load_weights(lds + L_W, wimg);
-  __syncthreads();
-  if (wave_id() == 0) {
-    // constant virtual-node input: normalize(relu([1,1] . w_n2l))  (net :247,272-283)
-    const int lane = lane_id();
-    const float x = fmaxf(fmaf(1.f, lds[L_W + W_IWN + 64 + lane], fmaf(1.f, lds[L_W + W_IWN + lane], 0.f)), 0.f);
-    const float nr = wave_norm64(x);
-    lds[L_Y0 + lane] = x / fmaxf(nr, 1e-12f);
+  // Dedicated mode (p.n_env > 0): workgroup b < n_env owns graph glist[b] and keeps its
+  // environment in LDS across steps; workgroup n_env + b runs graph glist[b]'s virtual-node
+  // chain and graph head while the tiles are computed and hands y / mix / aux to them; the
+  // remaining workgroups own the weight image and do tiles.
+  // Shared mode: every workgroup runs phase A for graphs b, b + grid, ... and then tiles
+  // (the tile workgroups compute the virtual-node chain of the graphs they touch).
+  const bool ded = p.n_env > 0;
+  const bool is_env = ded && (int)blockIdx.x < p.n_env;
+  const bool is_head = ded && !is_env && (int)blockIdx.x < 2 * p.n_env;
+  const int twg0 = ded ? 2 * p.n_env : 0;
+  const int ntw = gridDim.x - twg0;
+  if (!is_env) {
+    load_weights(lds + L_W, wimg);
+    __syncthreads();
+    if (wave_id() == 0) {
+      // constant virtual-node input: normalize(relu([1,1] . w_n2l))  (net :247,272-283)
+      const int lane = lane_id();
+      const float x = fmaxf(fmaf(1.f, lds[L_W + W_IWN + 64 + lane], fmaf(1.f, lds[L_W + W_IWN + lane], 0.f)), 0.f);
+      const float nr = wave_norm64(x);
+      lds[L_Y0 + lane] = x / fmaxf(nr, 1e-12f);
+    }
+    __syncthreads();
   }
-  __syncthreads();
 
   unsigned target = 0;
   int pstep = 0;
-  bool have_q = false;
+  bool have_q = false, staged = false;
   const int ng = p.nglist;
   while (true) {
-    // ---------------- phase A: one workgroup per graph
+    // ---------------- phase A
     MD_PROF(0);
     if (threadIdx.x == 0) ((int*)(lds + L_MISC))[60] = pstep;
     __syncthreads();
-    bool wdirty = false;
-    for (int gi = blockIdx.x; gi < ng; gi += gridDim.x) {
-      phase_a(p, p.glist[gi], have_q, lds);
-      wdirty = true;
+    if (ded) {
+      if (is_env) staged = phase_a(p, p.glist[blockIdx.x], have_q, lds, staged);
+    } else {
+      bool wdirty = false;
+      for (int gi = blockIdx.x; gi < ng; gi += gridDim.x) {
+        phase_a(p, p.glist[gi], have_q, lds, false);
+        wdirty = true;
+      }
+      if (wdirty) load_weights(lds + L_W, wimg);
     }
-    if (wdirty) load_weights(lds + L_W, wimg);
     MD_PROF(3);
     grid_sync(p, target);
     MD_PROF(4);
@@ -1173,18 +881,23 @@ __global__ void __launch_bounds__(NTHREADS, 1) md_rollout_kernel(Params p, const
     __syncthreads();
     const int ttot = pref[ng];
     if (ttot == 0) break;
-    const int per = (ttot + gridDim.x - 1) / gridDim.x;
-    const int t0 = min(ttot, (int)blockIdx.x * per), t1 = min(ttot, t0 + per);
+    const int per = (ttot + ntw - 1) / ntw;
+    const int tb = (int)blockIdx.x - twg0;
+    const bool tiles = !is_env && !is_head;
+    const int t0 = tiles ? min(ttot, tb * per) : 0, t1 = tiles ? min(ttot, t0 + per) : 0;
+    // hand-off tag of this step's graph head (unique per launch and step)
+    const unsigned long long htag = ded ? ((unsigned long long)p.launch_seq << 24) | (unsigned)(pstep + 1) : 0ull;
 
     for (int it = 1; it <= BP_ITERS; ++it) {
       MD_PROF(10 + it);
-      int cur = -1;  // graph-list index whose virtual node / graph head is loaded
+      if (is_head && it >= 2) head_iteration(p, lds, scr, p.glist[blockIdx.x - p.n_env], it, htag);
+      int cur = ded ? 0x7fffffff : -1;  // graph-list index whose virtual node / graph head is loaded
       for (int t = t0; t < t1; ++t) {
         const int gl = tile_graph(pref, ng, t);
         const int g = p.glist[gl];
         const GraphInfo gi = p.ginfo[g];
         const int j = t - pref[gl];  // tile within the graph
-        if (it >= 2 && gl != cur) {
+        if (it >= 2 && gl != cur && cur != 0x7fffffff) {
           // virtual-node chain of this graph (identical in every workgroup that needs it)
           const GraphVar gv = p.gvar[g];
           const int nt = (gv.n_live + TILE - 1) / TILE;
@@ -1245,7 +958,7 @@ __global__ void __launch_bounds__(NTHREADS, 1) md_rollout_kernel(Params p, const
           }
         }
         __syncthreads();
-        if (it == 3) attention_q_tile(p, lds, scr, gi, rows, p.apart + (size_t)(gi.tile_off + j) * 4);
+        if (it == 3) attention_q_tile(p, lds, scr, gi, g, rows, p.apart + (size_t)(gi.tile_off + j) * 4, htag);
       }
       MD_PROF(3 + 2 * it);
       grid_sync(p, target);

@@ -27,9 +27,14 @@ def prof(name, team):
     seg = [("A:stage", 0, 1), ("A:apply+mcc", 1, 2), ("A:feat", 2, 14), ("A:h0", 14, 15), ("A:wreload", 15, 3), ("barA", 3, 4), ("pref", 4, 11), ("p1", 11, 5), ("bar1", 5, 6), ("p2", 12, 7),
            ("bar2", 7, 8), ("p3", 13, 9), ("bar3", 9, 10)]
     tot = np.median(full[:, 10] - full[:, 0]) * 10 / 1000.0
-    print(f"{name} team={team}: removals {len(out[0][0])} wall {dt*1e3:.2f} ms kernel {ms:.2f} ms launches {nl}; "
+    print(f"{name} team={team} variant={os.environ.get('MD_VARIANT', '0')} env_mode={os.environ.get('MD_ENV_MODE', '1')}: removals {len(out[0][0])} wall {dt*1e3:.2f} ms kernel {ms:.2f} ms launches {nl}; "
           f"steps profiled {len(full)} median step {tot:.1f} us", flush=True)
     print("   " + "  ".join(f"{s}={d(a,b):.1f}" for s, a, b in seg), flush=True)
+    acc = full[:, 16:23].astype(np.float64)
+    calls = np.maximum(acc[:, 5], 1)
+    print("   env per step: rounds/call %.2f  cover %.1f  unite %.1f  label %.1f  prune %.1f  count %.1f us" % (
+        np.mean(acc[:, 0] / calls), np.median(acc[:, 6]) / 100, np.median(acc[:, 1]) / 100,
+        np.median(acc[:, 2]) / 100, np.median(acc[:, 3]) / 100, np.median(acc[:, 4]) / 100), flush=True)
     eng.close()
 
 def batch(nb, team):
