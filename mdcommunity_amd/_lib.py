@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmdroll.so")
+# MD_LIB overrides the library path (A/B comparisons of builds on the GPU box)
+LIB_PATH = os.environ.get("MD_LIB") or os.path.join(HERE, "libmdroll.so")
 
 MD_OK, MD_EINVAL, MD_EHIP, MD_EOOM, MD_ESTATE, MD_ETIMEOUT, MD_ECALLBACK = range(7)
 MD_COST_UNIT, MD_COST_DEGREE = 0, 1

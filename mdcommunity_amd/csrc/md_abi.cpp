@@ -13,6 +13,8 @@
 #include <cstdlib>
 #include <string>
 #include <unordered_set>
+#include <thread>
+#include <chrono>
 #include <vector>
 
 #include "../../include/mdroll.h"
@@ -51,6 +53,25 @@ struct DevBuf {
   }
 };
 
+// Mapped, coherent pinned host memory (the in-kernel host selection hand-shake).
+template <class T>
+struct HostBuf {
+  T* h = nullptr;  // host pointer
+  T* d = nullptr;  // device pointer
+  hipError_t alloc(size_t count) {
+    release();
+    if (count == 0) return hipSuccess;
+    hipError_t e = hipHostMalloc((void**)&h, count * sizeof(T), hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) return e;
+    std::memset(h, 0, count * sizeof(T));
+    return hipHostGetDevicePointer((void**)&d, h, 0);
+  }
+  void release() {
+    if (h) (void)hipHostFree(h);
+    h = d = nullptr;
+  }
+};
+
 }  // namespace
 
 struct md_ctx {
@@ -81,6 +102,12 @@ struct md_ctx {
   DevBuf<float> H[2][2], h0tab[2], q, spart, apart, ybuf, hbuf, tr_q, node_w;
   DevBuf<unsigned long long> hflag;
   unsigned launch_seq = 0;
+  // host selection hand-shake
+  int host_mode = 1;
+  int poll_us = 0;    // host poll interval while serving (MD_POLL_US)  // 1: ties / multi-node steps are answered inside the launch (MD_HOST_HANDSHAKE)
+  HostBuf<unsigned> h_req, h_ans;
+  HostBuf<int> h_nact, h_act;
+  HostBuf<float> h_q;
   bool need_gscr = false;
   DevBuf<unsigned long long> prof;
   int prof_cap = 0;
@@ -109,6 +136,7 @@ struct md_ctx {
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
     tr_stat.release(); glist.release(); ctl.release(); q.release(); spart.release();
     apart.release(); ybuf.release(); hbuf.release(); hflag.release(); tr_q.release(); node_w.release();
+    h_req.release(); h_ans.release(); h_nact.release(); h_act.release(); h_q.release();
     ng = 0;
     hinfo.clear();
     hvar.clear();
@@ -184,6 +212,7 @@ const char* err_name(int e) {
     case 2: return "action on an already covered node";
     case 3: return "live node sets differ between layers (U/PrepareBatchGraph.py:73)";
     case 4: return "action out of range";
+    case 5: return "host selection failed";
     default: return "unknown device error";
   }
 }
@@ -219,7 +248,50 @@ int grid_size(md_ctx* c, const std::vector<int>& gl, int n_env) {
 }
 
 // One launch of the persistent kernel over the graphs in gl (<= G_CAP of them).
-md_status launch_chunk(md_ctx* c, const int* gl, int ngl, int run_mode, int host_select) {
+// Host side of the in-kernel selection hand-shake: the callback and what it needs.
+struct Selector {
+  md_select_cb cb = nullptr;
+  void* user = nullptr;
+  int step = 1;
+  std::string err;  // first failure, reported after the launch drained
+};
+
+// Answers graph g's request `tag`: Q row (float, -inf = masked) -> the reference's masked
+// double row, the callback's actions into mapped memory, then the answer tag.
+void serve_request(md_ctx* c, Selector* sel, int g, unsigned tag, std::vector<double>& qd, std::vector<int32_t>& acts) {
+  const GraphInfo& gi = c->hinfo[g];
+  int k = -1;
+  if (!sel->cb) {
+    if (sel->err.empty()) {
+      char b[160];
+      snprintf(b, sizeof b, "graph %d: nodes tie at the max Q and no selection callback was given", g);
+      sel->err = b;
+    }
+  } else {
+    qd.resize(gi.n);
+    const float* hq = c->h_q.h + gi.node_off;
+    for (int i = 0; i < gi.n; ++i) qd[i] = std::isinf(hq[i]) ? QMASK : (double)hq[i];
+    const int nout = std::min(sel->step, gi.n);
+    acts.assign(nout, -1);
+    if (sel->cb(sel->user, g, qd.data(), gi.n, nout, acts.data()) != 0) {
+      if (sel->err.empty()) sel->err = "selection callback failed (graph " + std::to_string(g) + ")";
+    } else {
+      k = 0;
+      for (int i = 0; i < nout; ++i) {
+        if (acts[i] < 0 || acts[i] >= gi.n) {
+          if (sel->err.empty()) sel->err = "callback returned node " + std::to_string(acts[i]) + " out of range";
+          k = -1;
+          break;
+        }
+        c->h_act.h[gi.node_off + k++] = acts[i];
+      }
+    }
+  }
+  c->h_nact.h[g] = k;
+  __atomic_store_n(c->h_ans.h + g, tag, __ATOMIC_RELEASE);
+}
+
+md_status launch_chunk(md_ctx* c, const int* gl, int ngl, int run_mode, int host_select, Selector* sel) {
   std::vector<int> v(gl, gl + ngl);
   const int n_env = env_workgroups(c, v);
   const int grid = grid_size(c, v, n_env);
@@ -232,9 +304,36 @@ md_status launch_chunk(md_ctx* c, const int* gl, int ngl, int run_mode, int host
   p.launch_seq = ++c->launch_seq;
   p.run_mode = run_mode;
   p.host_select = host_select;
+  const bool hs = sel != nullptr && c->host_mode != 0 && c->h_req.d != nullptr;
+  if (hs) {
+    for (int g : v) {
+      __atomic_store_n(c->h_req.h + g, 0u, __ATOMIC_RELAXED);
+      __atomic_store_n(c->h_ans.h + g, 0u, __ATOMIC_RELAXED);
+    }
+    p.h_req = c->h_req.d;
+    p.h_ans = c->h_ans.d;
+    p.h_nact = c->h_nact.d;
+    p.h_act = c->h_act.d;
+    p.h_q = c->h_q.d;
+  }
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   HIPCHK(c, launch_rollout(p, c->wimg.p, grid, c->stream));
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  if (hs) {
+    // serve selection requests while the launch runs
+    std::vector<double> qd;
+    std::vector<int32_t> acts;
+    while (true) {
+      const hipError_t q = hipEventQuery(c->ev1);
+      if (q != hipSuccess && q != hipErrorNotReady) HIPCHK(c, q);
+      for (int g : v) {
+        const unsigned r = __atomic_load_n(c->h_req.h + g, __ATOMIC_ACQUIRE);
+        if (r != 0 && r != __atomic_load_n(c->h_ans.h + g, __ATOMIC_RELAXED)) serve_request(c, sel, g, r, qd, acts);
+      }
+      if (q == hipSuccess) break;
+      if (c->poll_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(c->poll_us));
+    }
+  }
   int dev_err = 0;
   HIPCHK(c, hipMemcpyAsync(&dev_err, c->ctl.p + CTL_ERR, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -242,6 +341,7 @@ md_status launch_chunk(md_ctx* c, const int* gl, int ngl, int run_mode, int host
   HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
   c->last_ms += ms;
   c->last_launches += 1;
+  if (dev_err == 5 && sel != nullptr && !sel->err.empty()) return fail(c, MD_ECALLBACK, "%s", sel->err.c_str());
   if (dev_err) return fail(c, dev_err == 1 ? MD_ETIMEOUT : MD_EINVAL, "device: %s", err_name(dev_err));
   if (c->prof_cap > 0) {
     std::vector<unsigned long long> tmp((size_t)c->prof_cap * PROF_SLOTS);
@@ -255,10 +355,10 @@ md_status launch_chunk(md_ctx* c, const int* gl, int ngl, int run_mode, int host
   return MD_OK;
 }
 
-md_status launch(md_ctx* c, const std::vector<int>& gl, int run_mode, int host_select) {
+md_status launch(md_ctx* c, const std::vector<int>& gl, int run_mode, int host_select, Selector* sel = nullptr) {
   for (size_t i = 0; i < gl.size(); i += G_CAP) {
     const int k = (int)std::min<size_t>(G_CAP, gl.size() - i);
-    md_status st = launch_chunk(c, gl.data() + i, k, run_mode, host_select);
+    md_status st = launch_chunk(c, gl.data() + i, k, run_mode, host_select, sel);
     if (st != MD_OK) return st;
   }
   return pull_vars(c);
@@ -301,6 +401,8 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   c->cost_mode = cost_mode;
   if (const char* v = std::getenv("MD_VARIANT")) c->variant = std::atoi(v);
   if (const char* v = std::getenv("MD_ENV_MODE")) c->env_mode = std::atoi(v);
+  if (const char* v = std::getenv("MD_HOST_HANDSHAKE")) c->host_mode = std::atoi(v);
+  if (const char* v = std::getenv("MD_POLL_US")) c->poll_us = std::atoi(v);
   md_status st = MD_OK;
   do {
     if (hipSetDevice(device) != hipSuccess) { st = MD_EHIP; break; }
@@ -477,6 +579,11 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->ybuf.alloc((size_t)n_graphs * 128));
   HIPCHK(c, c->hbuf.alloc((size_t)n_graphs * 144));
   HIPCHK(c, c->hflag.alloc((size_t)n_graphs));
+  HIPCHK(c, c->h_req.alloc((size_t)n_graphs));
+  HIPCHK(c, c->h_ans.alloc((size_t)n_graphs));
+  HIPCHK(c, c->h_nact.alloc((size_t)n_graphs));
+  HIPCHK(c, c->h_act.alloc(c->tot_n));
+  HIPCHK(c, c->h_q.alloc(c->tot_n));
   HIPCHK(c, hipMemset(c->hflag.p, 0, sizeof(unsigned long long) * n_graphs));
   HIPCHK(c, hipMemcpyAsync(c->ginfo.p, info.data(), sizeof(GraphInfo) * n_graphs, hipMemcpyHostToDevice, c->stream));
   if (c->cost_mode == MD_COST_DEGREE) {
@@ -600,7 +707,11 @@ md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, i
   while (!gl.empty()) {
     md_status st = push_vars(c);
     if (st != MD_OK) return st;
-    st = launch(c, gl, RUN_ROLLOUT, host_select);
+    Selector sel;
+    sel.cb = cb;
+    sel.user = user;
+    sel.step = step;
+    st = launch(c, gl, RUN_ROLLOUT, host_select, &sel);
     if (st != MD_OK) return st;
     std::vector<int> next;
     for (int g : gl) {

@@ -95,6 +95,12 @@ struct Params {
   float* tr_q;                     // per node slot x 2: qmax, gap per prediction
   const float* node_w;             // degree cost: [2][total nodes] static features, else null
   unsigned* bar;                   // grid barrier counter (zeroed per launch)
+  // host selection hand-shake (mapped pinned host memory; null: end the launch instead)
+  unsigned* h_req;                 // per graph: request tag (device writes)
+  unsigned* h_ans;                 // per graph: answer tag (host writes)
+  int* h_nact;                     // per graph: actions answered (-1: abort)
+  int* h_act;                      // per node slot: answered actions
+  float* h_q;                      // per node slot: Q of the request (-inf = masked)
   const int* glist;                // graphs processed by this launch (<= G_CAP)
   int nglist;
   int n_env;                       // dedicated environment workgroups (0 = shared mode)

@@ -8,6 +8,7 @@
 // through address-space-3 pointers so they compile to ds_* instructions, and edge passes read
 // eight edges per vector load.
 #pragma once
+#include <type_traits>
 
 typedef __attribute__((address_space(3))) int lds_i32;
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
@@ -36,52 +37,80 @@ enum { PA_ROUNDS = 0, PA_UNITE = 1, PA_LABEL = 2, PA_PRUNE = 3, PA_COUNT = 4, PA
 // ------------------------------------------------------------------ union-find
 // Parents always point to smaller ids, so the root of a tree is its minimum node id (the
 // canonical label compared across layers).  Lock-free hooking of roots with compare-and-swap.
-template <bool GL>
+// Global-mode arrays are plain (flat) int pointers with agent-scope atomics; LDS-mode arrays
+// are address-space-3 pointers (ds_* instructions, no aperture conversion, and no aliasing
+// with the private stack, so view fields stay in registers).
 __device__ __forceinline__ int uf_load(int* a, int i) {
-  if constexpr (GL) return __hip_atomic_load(a + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else return __hip_atomic_load((lds_i32*)(a + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return __hip_atomic_load(a + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-template <bool GL>
+__device__ __forceinline__ int uf_load(lds_i32* a, int i) {
+  return __hip_atomic_load(a + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 __device__ __forceinline__ void uf_store(int* a, int i, int v) {
-  if constexpr (GL) __hip_atomic_store(a + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else __hip_atomic_store((lds_i32*)(a + i), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_store(a + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-template <bool GL>
-__device__ __forceinline__ int uf_cas(int* a, int i, int expect, int v) {
-  if constexpr (GL) {
-    return atomicCAS(a + i, expect, v);
-  } else {
-    __hip_atomic_compare_exchange_strong((lds_i32*)(a + i), &expect, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_WORKGROUP);
-    return expect;
-  }
+__device__ __forceinline__ void uf_store(lds_i32* a, int i, int v) {
+  __hip_atomic_store(a + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-template <bool GL>
+__device__ __forceinline__ int uf_cas(int* a, int i, int expect, int v) { return atomicCAS(a + i, expect, v); }
+__device__ __forceinline__ int uf_cas(lds_i32* a, int i, int expect, int v) {
+  __hip_atomic_compare_exchange_strong(a + i, &expect, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+  return expect;
+}
 __device__ __forceinline__ void uf_add(int* a, int i, int v) {
-  if constexpr (GL) __hip_atomic_fetch_add(a + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else __hip_atomic_fetch_add((lds_i32*)(a + i), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_fetch_add(a + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-template <bool GL>
-__device__ __forceinline__ int uf_find(int* par, int v) {
-  int cur = uf_load<GL>(par, v);
+__device__ __forceinline__ void uf_add(lds_i32* a, int i, int v) {
+  __hip_atomic_fetch_add(a + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <class P>
+__device__ __forceinline__ int uf_find(P par, int v) {
+  int cur = uf_load(par, v);
   if (cur != v) {
     int prev = v, next;
-    while (cur > (next = uf_load<GL>(par, cur))) {
-      uf_store<GL>(par, prev, next);  // path halving; benign race (values only shrink)
+    while (cur > (next = uf_load(par, cur))) {
+      uf_store(par, prev, next);  // path halving; benign race (values only shrink)
       prev = cur;
       cur = next;
     }
   }
   return cur;
 }
-template <bool GL>
-__device__ __forceinline__ void uf_unite(int* par, int a, int b) {
+template <class P>
+__device__ __forceinline__ void uf_unite(P par, int a, int b) {
   while (true) {
-    a = uf_find<GL>(par, a);
-    b = uf_find<GL>(par, b);
+    a = uf_find(par, a);
+    b = uf_find(par, b);
     if (a == b) return;
     if (a > b) { const int t = a; a = b; b = t; }
-    if (uf_cas<GL>(par, b, b, a) == b) return;
+    if (uf_cas(par, b, b, a) == b) return;
+  }
+}
+
+// Union of the trees holding a and b, climbing both paths in lockstep (two independent LDS
+// loads per hop instead of two dependent find loops), path splitting on the way; stops when
+// the paths meet or after hooking root hi -> lo (a failed compare-and-swap re-reads).
+template <class P>
+__device__ __forceinline__ void uf_unite2(P par, int a, int b) {
+  int ap = -1, bp = -1;
+  while (a != b) {
+    const int na = uf_load(par, a), nb = uf_load(par, b);
+    if (na == a && nb == b) {
+      const int hi = a > b ? a : b, lo = a > b ? b : a;
+      if (uf_cas(par, hi, hi, lo) == hi) return;
+      continue;
+    }
+    if (na != a) {
+      if (ap >= 0) uf_store(par, ap, na);
+      ap = a;
+      a = na;
+    }
+    if (nb != b) {
+      if (bp >= 0) uf_store(par, bp, nb);
+      bp = b;
+      b = nb;
+    }
   }
 }
 
@@ -116,6 +145,7 @@ __host__ __device__ inline bool phase_a_fits_lds(int n, int et) {
 // Edge arrays of one graph: LDS-staged (u16 endpoints) or the global arrays themselves.
 template <bool GL>
 struct EnvView {
+  typedef typename std::conditional<GL, int*, lds_i32*>::type IP;
   const GraphInfo* gi;
   int e0, et;                   // edges of layer 0, both layers
   int variant;
@@ -128,8 +158,8 @@ struct EnvView {
   const int* gv[2];
   uint8_t* gst[2];
   uint8_t* gcov;                // covered flags in HBM (both modes keep them current)
-  int *par0, *par1, *deg0, *deg1;
-  int* tmp;                     // always LDS
+  IP par0, par1, deg0, deg1;    // union-find parents / labels, degrees
+  int* tmp;                     // always LDS (generic pointer for the block helpers)
   uint8_t* calive[2];
   const int* epos[2];
 
@@ -276,36 +306,71 @@ __device__ void unite_lockstep(const EnvView<GL>& E) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       if (lay[k] >= 0) {
-        int* par = lay[k] ? E.par1 : E.par0;
-        fx[k] = uf_load<GL>(par, x[k]);
-        fy[k] = uf_load<GL>(par, y[k]);
+        auto par = lay[k] ? E.par1 : E.par0;
+        fx[k] = uf_load(par, x[k]);
+        fy[k] = uf_load(par, y[k]);
       }
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       if (lay[k] < 0) continue;
-      int* par = lay[k] ? E.par1 : E.par0;
+      auto par = lay[k] ? E.par1 : E.par0;
       const bool rx = fx[k] == x[k], ry = fy[k] == y[k];
       if (!rx) {
-        if (xp[k] >= 0) uf_store<GL>(par, xp[k], fx[k]);  // path splitting
+        if (xp[k] >= 0) uf_store(par, xp[k], fx[k]);  // path splitting
         xp[k] = x[k];
         x[k] = fx[k];
       }
       if (!ry) {
-        if (yp[k] >= 0) uf_store<GL>(par, yp[k], fy[k]);
+        if (yp[k] >= 0) uf_store(par, yp[k], fy[k]);
         yp[k] = y[k];
         y[k] = fy[k];
       }
       bool done = x[k] == y[k];
       if (!done && rx && ry) {
         const int hi = max(x[k], y[k]), lo = min(x[k], y[k]);
-        done = uf_cas<GL>(par, hi, hi, lo) == hi;
+        done = uf_cas(par, hi, hi, lo) == hi;
       }
       if (done) {
         int l = -1;
         lay[k] = feed(x[k], y[k], l) ? l : -1;
         xp[k] = yp[k] = -1;
       }
+    }
+  }
+}
+
+// Union of every alive edge (both layers): per group of eight edges the parents of all
+// sixteen endpoints are loaded at once, edges whose endpoints already share a parent are
+// skipped, the rest start their lockstep climb one hop up.
+template <bool GL>
+__device__ void unite_all(const EnvView<GL>& E) {
+  if constexpr (GL) {
+    for (int e = threadIdx.x; e < E.et; e += NTHREADS)
+      if (E.state(e) == E_ALIVE) uf_unite(e < E.e0 ? E.par0 : E.par1, E.u(e), E.v(e));
+  } else {
+    const int ng = (E.et + 7) >> 3;
+    for (int g = threadIdx.x; g < ng; g += NTHREADS) {
+      const v4u U = ((const lds_u4*)E.u16)[g];
+      const v4u V = ((const lds_u4*)E.v16)[g];
+      const v2u S = ((const lds_u2*)E.st)[g];
+      int pu[8], pv[8];
+      bool al[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = 8 * g + k;
+        const unsigned sw = k < 4 ? S.x : S.y;
+        al[k] = e < E.et && ((sw >> (8 * (k & 3))) & 0xffu) == E_ALIVE;
+        if (al[k]) {
+          auto par = e < E.e0 ? E.par0 : E.par1;
+          const unsigned uw = sel4(U, k >> 1), vw = sel4(V, k >> 1);
+          pu[k] = uf_load(par, (int)((uw >> (16 * (k & 1))) & 0xffffu));
+          pv[k] = uf_load(par, (int)((vw >> (16 * (k & 1))) & 0xffffu));
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (al[k] && pu[k] != pv[k]) uf_unite2(8 * g + k < E.e0 ? E.par0 : E.par1, pu[k], pv[k]);
     }
   }
 }
@@ -320,7 +385,8 @@ __device__ void unite_lockstep(const EnvView<GL>& E) {
 // path-halving find may rewrite a parent slot with a non-root ancestor after its owner stored
 // the root, so the parent array itself is not a label map.
 template <bool GL>
-__device__ int mcc_fixed_point(const EnvView<GL>& E, int* pr, unsigned long long* acc) {
+__device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long long* acc) {
+  const EnvView<GL> E = Ein;  // fields in registers
   const int n = E.gi->n;
   int pruned0 = 0, pruned1 = 0;
   if (acc != nullptr && threadIdx.x == 0) acc[PA_CALLS] += 1;
@@ -328,15 +394,19 @@ __device__ int mcc_fixed_point(const EnvView<GL>& E, int* pr, unsigned long long
     unsigned long long tp = wall_clock64();
     if (acc != nullptr && threadIdx.x == 0) acc[PA_ROUNDS] += 1;
     for (int x = threadIdx.x; x < n; x += NTHREADS) {
-      uf_store<GL>(E.par0, x, x);
-      uf_store<GL>(E.par1, x, x);
+      uf_store(E.par0, x, x);
+      uf_store(E.par1, x, x);
     }
     __syncthreads();
+    // variants 1 / 2 are alternative union orders kept for measurement (both slower on gfx950:
+    // 82 / 28 us against 22 us per step on the GMM N=1000 rollout)
     if (E.variant & 1) {
-      unite_lockstep<GL>(E);  // experimental (measured slower on gfx950 so far)
+      unite_lockstep<GL>(E);
+    } else if (E.variant & 2) {
+      unite_all<GL>(E);
     } else {
       for_each_edge<GL>(E, [&](int e, int u, int v, int s) {
-        if (s == E_ALIVE) uf_unite<GL>(e < E.e0 ? E.par0 : E.par1, u, v);
+        if (s == E_ALIVE) uf_unite(e < E.e0 ? E.par0 : E.par1, u, v);
       });
     }
     __syncthreads();
@@ -344,9 +414,9 @@ __device__ int mcc_fixed_point(const EnvView<GL>& E, int* pr, unsigned long long
     tp = wall_clock64();
     int diff = 0;
     for (int x = threadIdx.x; x < n; x += NTHREADS) {
-      const int r0 = uf_find<GL>(E.par0, x), r1 = uf_find<GL>(E.par1, x);
-      uf_store<GL>(E.deg0, x, r0);
-      uf_store<GL>(E.deg1, x, r1);
+      const int r0 = uf_find(E.par0, x), r1 = uf_find(E.par1, x);
+      uf_store(E.deg0, x, r0);
+      uf_store(E.deg1, x, r1);
       diff |= (r0 != r1);
     }
     diff = __syncthreads_or(diff);
@@ -356,8 +426,8 @@ __device__ int mcc_fixed_point(const EnvView<GL>& E, int* pr, unsigned long long
     int c0 = 0, c1 = 0;
     for_each_edge<GL>(E, [&](int e, int u, int v, int s) {
       if (s != E_ALIVE) return;
-      int* other = e < E.e0 ? E.deg1 : E.deg0;  // layer-0 edges are pruned by layer-1 components
-      if (uf_load<GL>(other, u) != uf_load<GL>(other, v)) {
+      auto other = e < E.e0 ? E.deg1 : E.deg0;  // layer-0 edges are pruned by layer-1 components
+      if (uf_load(other, u) != uf_load(other, v)) {
         E.kill(e, E_PRUNED);
         if (e < E.e0) c0++; else c1++;
       }
@@ -370,13 +440,13 @@ __device__ int mcc_fixed_point(const EnvView<GL>& E, int* pr, unsigned long long
   const unsigned long long tc = wall_clock64();
   pr[0] = pruned0;
   pr[1] = pruned1;
-  for (int x = threadIdx.x; x < n; x += NTHREADS) uf_store<GL>(E.par1, x, 0);
+  for (int x = threadIdx.x; x < n; x += NTHREADS) uf_store(E.par1, x, 0);
   __syncthreads();
   for (int x = threadIdx.x; x < n; x += NTHREADS)
-    if (!E.covered(x)) uf_add<GL>(E.par1, uf_load<GL>(E.deg0, x), 1);
+    if (!E.covered(x)) uf_add(E.par1, uf_load(E.deg0, x), 1);
   __syncthreads();
   int best = 0;
-  for (int x = threadIdx.x; x < n; x += NTHREADS) best = max(best, uf_load<GL>(E.par1, x));
+  for (int x = threadIdx.x; x < n; x += NTHREADS) best = max(best, uf_load(E.par1, x));
   best = block_max_int(best, E.tmp);
   PACC(acc, PA_COUNT, tc);
   return best;
@@ -414,10 +484,11 @@ __device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, floa
     E.tmp = ia;
   } else {
     const EnvLayout L = env_layout(n, et);
-    E.par0 = ia + L.par0;
-    E.par1 = ia + L.par1;
-    E.deg0 = ia + L.deg0;
-    E.deg1 = ia + L.deg1;
+    lds_i32* la = (lds_i32*)ia;
+    E.par0 = la + L.par0;
+    E.par1 = la + L.par1;
+    E.deg0 = la + L.deg0;
+    E.deg1 = la + L.deg1;
     E.tmp = ia + L.tmp;
     lds_u8* base8 = (lds_u8*)(uint8_t*)ia;
     E.u16 = (lds_u16*)base8;
@@ -463,7 +534,9 @@ __device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, floa
   int err = 0;
   for (int k = 0; k < pend_n; ++k) {
     if (gv.alive[0] == 0 || gv.alive[1] == 0) break;  // terminal between queued actions
-    const int a = k == 0 && pend_first >= 0 ? pend_first : p.pend[gi.node_off + k];
+    const int a = k == 0 && pend_first >= 0
+                      ? pend_first
+                      : __hip_atomic_load(p.pend + gi.node_off + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (a < 0 || a >= n) { err = ERR_BADNODE; break; }
     if (E.covered(a)) { err = ERR_COVERED; break; }
     // cover a in both layers (U/mvc_env.py:74-85): its alive edges become "covered"
@@ -513,15 +586,15 @@ __device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, floa
   MD_PROF_A(2);
   // residual degrees by edge-parallel atomics
   for (int x = threadIdx.x; x < n; x += NTHREADS) {
-    uf_store<GL>(E.deg0, x, 0);
-    uf_store<GL>(E.deg1, x, 0);
+    uf_store(E.deg0, x, 0);
+    uf_store(E.deg1, x, 0);
   }
   __syncthreads();
   for_each_edge<GL>(E, [&](int e, int u, int v, int s) {
     if (s != E_ALIVE) return;
-    int* d = e < e0 ? E.deg0 : E.deg1;
-    uf_add<GL>(d, u, 1);
-    uf_add<GL>(d, v, 1);
+    auto d = e < e0 ? E.deg0 : E.deg1;
+    uf_add(d, u, 1);
+    uf_add(d, v, 1);
   });
   __syncthreads();
   // live list (ascending ids), per-layer aggregates (U/PrepareBatchGraph.py:35-74): one
@@ -534,7 +607,7 @@ __device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, floa
   int* gdeg0 = p.deg[0] + gi.node_off;
   int* gdeg1 = p.deg[1] + gi.node_off;
   for (int x = x0; x < x1; ++x) {
-    const int d0 = uf_load<GL>(E.deg0, x), d1 = uf_load<GL>(E.deg1, x);
+    const int d0 = uf_load(E.deg0, x), d1 = uf_load(E.deg1, x);
     gdeg0[x] = d0;
     gdeg1[x] = d1;
     q[x] = NEG_INF;
@@ -608,7 +681,7 @@ __device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, floa
     int k = base;
     int* lv = p.live + gi.node_off;
     for (int x = x0; x < x1; ++x)
-      if (uf_load<GL>(E.deg0, x) > 0) lv[k++] = x;
+      if (uf_load(E.deg0, x) > 0) lv[k++] = x;
   }
   if (bad && !err) err = ERR_LIVE_MISMATCH;
   const int hd0 = gv.hdmax[0], hd1 = gv.hdmax[1];

@@ -79,7 +79,8 @@ static_assert(S_END >= 64 * 128 + 128 + 4 + 256, "scratch must hold w_layer1 for
 
 constexpr float NEG_INF = -__builtin_huge_valf();
 constexpr unsigned long long BARRIER_TIMEOUT_TICKS = 400000000ull;  // 4 s at 100 MHz
-enum : int { ERR_TIMEOUT = 1, ERR_COVERED = 2, ERR_LIVE_MISMATCH = 3, ERR_BADNODE = 4 };
+enum : int { ERR_TIMEOUT = 1, ERR_COVERED = 2, ERR_LIVE_MISMATCH = 3, ERR_BADNODE = 4, ERR_HOST = 5 };
+constexpr unsigned long long HOST_TIMEOUT_TICKS = 6000000000ull;  // 60 s at 100 MHz
 
 // ------------------------------------------------------------------ small helpers
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
@@ -138,7 +139,7 @@ __device__ __forceinline__ void grid_sync(const Params& p, unsigned& target) {
     while (__hip_atomic_load(p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       if (__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
       __builtin_amdgcn_s_sleep(1);
-      if (wall_clock64() - t0 > BARRIER_TIMEOUT_TICKS) {
+      if (wall_clock64() - t0 > (p.h_req != nullptr ? HOST_TIMEOUT_TICKS : BARRIER_TIMEOUT_TICKS)) {
         __hip_atomic_store(p.err, ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -216,6 +217,44 @@ __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* tot) {
 
 #include "md_env.h"
 
+// Host selection hand-shake for graph g (ties at the max Q, or a multi-node step): publish
+// the graph's Q row to mapped host memory, raise the request tag, wait for the host's answer
+// (its selection callback = the reference's np.argsort pick), copy the actions to p.pend.
+// Returns the number of actions (0 on error; the error word is set).
+__device__ __noinline__ int host_handshake(const Params& p, const GraphInfo& gi, int g, int npred, int* misc) {
+  const unsigned tag = (p.launch_seq << 16) ^ (unsigned)(npred + 1);
+  for (int x = threadIdx.x; x < gi.n; x += NTHREADS) p.h_q[gi.node_off + x] = p.q[gi.node_off + x];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(p.h_req + g, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned long long t0 = wall_clock64();
+    int k = 0;
+    while (__hip_atomic_load(p.h_ans + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != tag) {
+      __builtin_amdgcn_s_sleep(2);
+      if (wall_clock64() - t0 > HOST_TIMEOUT_TICKS) {
+        k = -1;
+        break;
+      }
+    }
+    if (k == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      k = __hip_atomic_load(p.h_nact + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (k < 0 || k > gi.n) k = -1;
+      for (int i = 0; i < k; ++i)
+        __hip_atomic_store(p.pend + gi.node_off + i,
+                           __hip_atomic_load(p.h_act + gi.node_off + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (k < 0) set_err(p, ERR_HOST);
+    misc[3] = k;
+  }
+  __syncthreads();
+  return max(misc[3], 0);
+}
+
 // Merge arg-max partial (m2, s2, i2, c2) into (bm, bs, bi, bc); c = 0 marks an empty partial.
 __device__ __forceinline__ void argmax_combine(float& bm, float& bs, int& bi, int& bc, float m2, float s2,
                                                int i2, int c2) {
@@ -291,8 +330,18 @@ __device__ __noinline__ bool phase_a(const Params& p, int g, bool have_q, float*
       if (threadIdx.x == 0) gv.status = ST_PAUSED;
       stop = true;
     } else if (p.host_select || misc[2] != 1) {
-      if (threadIdx.x == 0) gv.status = ST_NEED_HOST;
-      stop = true;
+#ifndef MD_NO_HS
+      if (p.h_req != nullptr) {
+#else
+      if (false) {
+#endif
+        // ask the host without ending the launch; the actions land in p.pend
+        pend_n = host_handshake(p, gi, g, gv.npred, misc);
+        stop = pend_n <= 0;
+      } else {
+        if (threadIdx.x == 0) gv.status = ST_NEED_HOST;
+        stop = true;
+      }
     } else {
       pend_n = 1;
       pend_first = misc[1];
@@ -786,6 +835,19 @@ __device__ __noinline__ void attention_q_tile(const Params& p, float* lds, float
       p.prof[(size_t)pstep * PROF_SLOTS + (slot)] = wall_clock64();                                      \
   } while (0)
 
+// Tile-side timestamps of the first tile workgroup (slots 23-31: per iteration after the
+// gather, after update / normalize / stores, at the tile's end).
+#ifdef MD_NO_PROFT
+#define MD_PROF_T(slot) do {} while (0)
+#else
+#define MD_PROF_T(slot)                                                                          \
+  do {                                                                                           \
+    if (p.prof != nullptr && (int)blockIdx.x == twg0 && t == t0 && threadIdx.x == 0 &&            \
+        pstep < p.prof_cap)                                                                      \
+      p.prof[(size_t)pstep * PROF_SLOTS + (slot)] = wall_clock64();                              \
+  } while (0)
+#endif
+
 __device__ __forceinline__ void load_weights(float* dst, const float* src) {
   constexpr int N4 = W_IEND / 4, K = (N4 + NTHREADS - 1) / NTHREADS;
   const float4* s4 = (const float4*)src;
@@ -926,6 +988,7 @@ __global__ void __launch_bounds__(NTHREADS, 1) md_rollout_kernel(Params p, const
         __syncthreads();
         gather_tile(p, gi, it, rows, scr);
         __syncthreads();
+        MD_PROF_T(23 + 3 * (it - 1));
         update_tile(lds + L_W, scr);
         __syncthreads();
         normalize_tile(scr + S_E, scr);
@@ -958,7 +1021,9 @@ __global__ void __launch_bounds__(NTHREADS, 1) md_rollout_kernel(Params p, const
           }
         }
         __syncthreads();
+        MD_PROF_T(24 + 3 * (it - 1));
         if (it == 3) attention_q_tile(p, lds, scr, gi, g, rows, p.apart + (size_t)(gi.tile_off + j) * 4, htag);
+        MD_PROF_T(25 + 3 * (it - 1));
       }
       MD_PROF(3 + 2 * it);
       grid_sync(p, target);

@@ -30,6 +30,9 @@ def prof(name, team):
     print(f"{name} team={team} variant={os.environ.get('MD_VARIANT', '0')} env_mode={os.environ.get('MD_ENV_MODE', '1')}: removals {len(out[0][0])} wall {dt*1e3:.2f} ms kernel {ms:.2f} ms launches {nl}; "
           f"steps profiled {len(full)} median step {tot:.1f} us", flush=True)
     print("   " + "  ".join(f"{s}={d(a,b):.1f}" for s, a, b in seg), flush=True)
+    tt = lambda a, b: np.median((full[:, b].astype(np.int64) - full[:, a].astype(np.int64))) / 100.0
+    print("   tile wg: p1 gather %.1f upd %.1f end %.1f | p2 gather %.1f upd %.1f end %.1f | p3 gather %.1f upd %.1f attn %.1f us" % (
+        tt(11, 23), tt(23, 24), tt(24, 25), tt(12, 26), tt(26, 27), tt(27, 28), tt(13, 29), tt(29, 30), tt(30, 31)), flush=True)
     acc = full[:, 16:23].astype(np.float64)
     calls = np.maximum(acc[:, 5], 1)
     print("   env per step: rounds/call %.2f  cover %.1f  unite %.1f  label %.1f  prune %.1f  count %.1f us" % (
