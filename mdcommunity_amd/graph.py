@@ -109,6 +109,31 @@ class GSet:
         self.graph_pool.clear()
 
 
+def ensure_degree_weights(g):
+    """Graph_test.weights of the degree-cost variant (D/graph.py:80-115): filled when the
+    initial LMCC is not 1, as w_l[v] = deg_l(v) / maxdeg_l on the original layers (Python
+    int / int division, node order 0..N-1)."""
+    if g.weights[0] or g.max_rank == 1:
+        return g.weights
+    for l in range(2):
+        d = np.bincount(g.edges[l].reshape(-1), minlength=g.num_nodes)
+        mx = int(d.max())
+        g.weights[l] = {v: int(d[v]) / mx for v in range(g.num_nodes)}
+    return g.weights
+
+
+def node_weight_array(graphs):
+    """Device layout of the degree-cost node inputs: float32 [2][sum N] (layer-major)."""
+    out = []
+    for l in range(2):
+        parts = []
+        for g in graphs:
+            w = ensure_degree_weights(g)[l]
+            parts.append(np.asarray([w.get(v, 0.0) for v in range(g.num_nodes)], dtype=np.float64))
+        out.append(np.concatenate(parts) if parts else np.zeros(0))
+    return np.concatenate(out).astype(np.float32)
+
+
 def degree_weights(g):
     """Degree-cost node weights w_l(v) = deg_l(v) / maxdeg_l on the original layers
     (D/graph.py:91-115); returns float64 arrays [2][N] and the python-sum totals W_l."""

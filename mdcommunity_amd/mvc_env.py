@@ -39,7 +39,8 @@ class MvcEnv:
     def _load(self, g):
         nw = None
         if self.cost_mode == _lib.MD_COST_DEGREE:
-            nw = np.concatenate([np.asarray(g.node_weight[0], np.float32), np.asarray(g.node_weight[1], np.float32)])
+            from .graph import node_weight_array
+            nw = node_weight_array([g])
         self.engine.load_graphs([(g.num_nodes, g.edges[0], g.edges[1])], node_w=nw)
 
     # -- reference API

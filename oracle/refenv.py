@@ -25,7 +25,8 @@ MASK = -(2147483647 / 2)
 
 
 class RefGraph:
-    """Graph_test (U/graph.py:69-84) from two ordered edge lists on nodes 0..n-1."""
+    """Graph_test (U/graph.py:69-84; D/graph.py:72-115 adds the degree weights) from two
+    ordered edge lists on nodes 0..n-1."""
 
     def __init__(self, n, edges0, edges1):
         self.num_nodes = int(n)
@@ -38,6 +39,14 @@ class RefGraph:
                 self.adj[l][v].append(u)
         g1, g2 = self.nx_layers()
         self.max_rank = lmcc_size(mutual_components(g1, g2, [set(), set()]))
+        # D/graph.py:91-115 cal_degree: original degree / max degree, per layer (only when
+        # max_rank != 1 there; the weights are unused otherwise)
+        self.weights = [[], []]
+        if self.max_rank != 1:
+            for l in range(2):
+                d = [len(self.adj[l][v]) for v in range(self.num_nodes)]
+                m = max(d)
+                self.weights[l] = [x / m for x in d]
 
     def nx_layers(self, covered=(), removed=(set(), set())):
         out = []
@@ -86,10 +95,11 @@ def lmcc_size(comps):
 
 
 class RefEnv:
-    """MvcEnv, unit cost (U/mvc_env.py)."""
+    """MvcEnv: unit cost (U/mvc_env.py) or degree cost (D/mvc_env.py:75-134)."""
 
-    def __init__(self, graph):
+    def __init__(self, graph, cost="unit"):
         self.graph = graph
+        self.cost = cost
         self.covered = set()
         self.action_list = []
         self.removed = [set(), set()]
@@ -114,10 +124,19 @@ class RefEnv:
                     self.num_covered[l] += 1
         self.g1.remove_node(a)
         self.g2.remove_node(a)
-        rank = float(lmcc_size(mutual_components(self.g1, self.g2, self.removed)))
-        r_t = -rank / (self.graph.max_rank * float(self.graph.num_nodes))
-        self.score += -1 * r_t
-        self.maxcc.append(-1 * r_t * self.graph.num_nodes)
+        g = self.graph
+        if self.cost == "degree":
+            rank = lmcc_size(mutual_components(self.g1, self.g2, self.removed))
+            tw0 = sum(g.weights[0])
+            tw1 = sum(g.weights[1])
+            r_t = -rank / (g.max_rank) * (g.weights[0][a] / tw0 + g.weights[1][a] / tw1) / 2.0
+            self.score += -1 * r_t
+            self.maxcc.append(rank / (g.max_rank))
+        else:
+            rank = float(lmcc_size(mutual_components(self.g1, self.g2, self.removed)))
+            r_t = -rank / (g.max_rank * float(g.num_nodes))
+            self.score += -1 * r_t
+            self.maxcc.append(-1 * r_t * g.num_nodes)
         self.ranks.append(int(rank))
         return int(rank)
 
@@ -163,25 +182,30 @@ def featurize(graph, covered, removed):
     return ids, deg, coo, aux, counter
 
 
-def predict(weights, graph, covered, removed):
-    """Masked float64 Q row over all node ids (Predict, U/MultiDismantler_torch.py:263-302)."""
+def predict(weights, graph, covered, removed, cost="unit"):
+    """Masked float64 Q row over all node ids (Predict, U/MultiDismantler_torch.py:263-302).
+    Degree cost: node inputs [weight, 1.0] of the live nodes (D/PrepareBatchGraph.py:133-136)."""
     ids, deg, coo, aux, _ = featurize(graph, covered, removed)
     row = np.full(graph.num_nodes, MASK, dtype=np.float64)
     if ids:
-        q = refmodel.forward(weights, deg, coo, aux)
+        feat = None
+        if cost == "degree":
+            feat = [[[graph.weights[l][v], 1.0] for v in ids] for l in range(2)]
+        q = refmodel.forward(weights, deg, coo, aux, node_feat=feat)
         row[np.asarray(ids)] = q.astype(np.float64)
     for k in covered:
         row[k] = MASK
     return row
 
 
-def rollout(weights, graph, step=1, on_predict=None):
-    """GetSol (U/MultiDismantler_torch.py:759-784): returns (score, sequence, ranks, maxcc)."""
-    env = RefEnv(graph)
+def rollout(weights, graph, step=1, on_predict=None, cost="unit"):
+    """GetSol (U/MultiDismantler_torch.py:759-784; D :734-768): returns (score, sequence,
+    ranks, maxcc)."""
+    env = RefEnv(graph, cost)
     sol = []
     t = 0
     while not env.terminal():
-        q = predict(weights, graph, env.covered, env.removed)
+        q = predict(weights, graph, env.covered, env.removed, cost)
         if on_predict is not None:
             on_predict(t, q, env)
         t += 1

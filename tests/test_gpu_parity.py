@@ -155,3 +155,23 @@ def test_errors_are_reported(eng):
         eng.step(np.array([a], np.int32))  # covering a covered node (U/mvc_env.py:77 assert)
     with pytest.raises(_lib.MDError):
         eng.load_graphs([(3, np.array([[0, 0]]), np.array([[0, 1]]))])  # self-loop
+
+
+def test_shared_mode_batch_matches_dedicated(eng):
+    """A launch of more than 16 graphs takes the shared phase-A path (every workgroup steps
+    graphs, then tiles); its rollouts equal the dedicated-workgroup path of single graphs."""
+    names = ["gmm200_s7", "er100", "er300_dense"]
+    zs = [load_golden(nm) for nm in names]
+    graphs = [(int(z["n_nodes"]), z["edges0"], z["edges1"]) for z in zs]
+    single = []
+    for g in graphs:
+        eng.load_graphs([g])
+        eng.reset()
+        s, r = eng.rollout()[0]
+        single.append((s.tolist(), r.tolist()))
+    batch = [graphs[i % 3] for i in range(18)]
+    eng.load_graphs(batch)
+    eng.reset()
+    out = eng.rollout()
+    for i, (s, r) in enumerate(out):
+        assert (s.tolist(), r.tolist()) == single[i % 3], i

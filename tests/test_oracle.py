@@ -17,13 +17,22 @@ def weights():
     return refmodel.RefWeights.load(engine.DEFAULT_UNIT)
 
 
-@pytest.mark.parametrize("name", ["er100", "gmm200_s7", "er300_dense"])
-def test_rollout_matches_reference(weights, name):
+@pytest.fixture(scope="module")
+def weights_degree():
+    torch.set_num_threads(16)
+    return refmodel.RefWeights.load(engine.DEFAULT_DEGREE)
+
+
+@pytest.mark.parametrize("name", ["er100", "gmm200_s7", "er300_dense", "deg_er100", "deg_gmm200_s7"])
+def test_rollout_matches_reference(weights, weights_degree, name):
+    """Unit cost (U/) and degree cost (D/, fixtures of make_golden_degree.py)."""
     z = load_golden(name)
+    cost = "degree" if name.startswith("deg_") else "unit"
+    w = weights_degree if cost == "degree" else weights
     g = refenv.RefGraph(int(z["n_nodes"]), z["edges0"], z["edges1"])
     assert g.max_rank == int(z["max_rank"])
     rows = {}
-    score, seq, ranks, maxcc = refenv.rollout(weights, g, on_predict=lambda t, q, env: rows.__setitem__(t, q))
+    score, seq, ranks, maxcc = refenv.rollout(w, g, on_predict=lambda t, q, env: rows.__setitem__(t, q), cost=cost)
     assert seq == z["seq"].tolist()
     assert ranks == z["ranks"].tolist()
     assert score == float(z["score"])  # AUDC, bit-exact float64
