@@ -2,15 +2,19 @@
 """Benchmark of the MultiDismantler inference rollout on MI355X (BASELINE.json metric:
 node-removals/sec (whole node) + AUDC match, 2-layer synthetic N=1000).
 
-A "step" is one complete rollout (MvcEnv.s0 + GetSol loop until terminal) of the workload's
-graphs, inputs already resident in HBM.  Default workload (BASELINE configs[1]): one
-2-layer GMM graph, N=1000, generator seed 0 (mdcommunity_amd.gmm reproduces the reference's
-U/GMM.py graph for that seed), unit-cost checkpoint g0.5 iter 100000.  With --gpus N each
-rank (one process per GPU) runs its own replica (weak scaling); ``--workload batch``
-shards independent graphs over ranks and gathers their AUDC to rank 0 over RCCL.
+A "step" is one complete rollout (MvcEnv.s0 + the GetSol loop until terminal) of the
+workload's graphs, inputs already resident in HBM.  The headline workload (BASELINE configs[1])
+is one 2-layer GMM graph, N=1000, generator seed 0 (mdcommunity_amd.gmm reproduces the
+reference's U/GMM.py graph for that seed), unit-cost checkpoint g0.5 iter 100000; with
+--gpus N every rank (one process per GPU) runs its own replica (weak scaling).
 
-Prints one JSON line (rank 0) with the roofline of the rollout kernel and the CPU baseline
-(the oracle, a reference-shaped restatement, timed on this host's cores).
+The same run also measures the batched path (configs[2]: 256 graphs N=1000 per GPU, seeds
+sharded contiguously over ranks, per-graph AUDC gathered over RCCL) as the "batch" object.
+
+Prints one JSON line (rank 0) with the roofline of the rollout kernel (HIP-event device time
+of every launch in the timed region, algorithmic flops / bytes from the device's own
+per-prediction trace) and the CPU baseline (the oracle, a reference-shaped
+restatement, timed on this host's cores on a bounded sample).
 """
 import argparse
 import json
@@ -24,8 +28,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "node-removals/sec (whole node) + AUDC match, 2-layer synthetic N=1000"
-PEAK_FP32_TFLOPS = 157.3   # MI355X FP32 matrix (= vector) peak, MI355X_MICROARCH.md
+PEAK_FP32_TFLOPS = 157.3   # MI355X dense FP32 matrix peak (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E peak
+CKPT = "U/models/g0.5_TORCH-Model_GMM_30_50/nrange_30_50_iter_100000.ckpt"
 
 
 def step_flops(n, m0, m1, g=1):
@@ -44,10 +49,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["single", "batch"], default="single")
     ap.add_argument("--n", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--graphs-per-rank", type=int, default=256)
+    ap.add_argument("--batch-graphs", type=int, default=256, help="graphs per GPU of the batch object (0: skip)")
+    ap.add_argument("--batch-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-seconds", type=float, default=12.0)
     return ap.parse_args()
@@ -55,7 +60,8 @@ def parse():
 
 def cpu_baseline(edges, n, seconds):
     """The oracle (reference-shaped CPU restatement: Python featurisation + torch-CPU
-    forward + networkx MCC each step) timed on this host, whole rollouts until ~seconds."""
+    forward + networkx MCC each step) timed on this host: whole rollouts of the bench graph
+    until `seconds` have passed."""
     import torch
     from oracle import refenv, refmodel
     from mdcommunity_amd import engine
@@ -77,38 +83,82 @@ def cpu_baseline(edges, n, seconds):
                 audc=score)
 
 
+def audc_of(ranks, max_rank, n):
+    s = 0.0
+    for r in ranks:
+        s += -1 * (-float(r) / (int(max_rank) * float(n)))  # U/mvc_env.py:86,133-137
+    return s
+
+
+def run_steps(eng, steps):
+    """`steps` timed rollouts (reset = MvcEnv.s0 in md_env_kernel, then the device rollout
+    loop in md_rollout_kernel).  Returns the HIP-event device time and launch count of the
+    rollout kernel, the same for the s0 launches, removals and the last outputs."""
+    kernel_ms, launches, removals, s0_ms = 0.0, 0, 0, 0.0
+    last = None
+    for _ in range(steps):
+        mr = eng.reset()
+        ms, _ = eng.last_timing()
+        s0_ms += ms
+        outs = eng.rollout()
+        ms, nl = eng.last_timing()
+        kernel_ms += ms
+        launches += nl
+        removals += sum(len(o[0]) for o in outs)
+        last = (mr, outs)
+    return kernel_ms, launches, removals, last, s0_ms
+
+
+def trace_work(eng, n_graphs):
+    flops, nbytes, preds = 0.0, 0.0, 0
+    for gidx in range(n_graphs):
+        tr = eng.trace(gidx)
+        for n_t, a0, a1 in zip(tr["n_live"], tr["m0"], tr["m1"]):
+            flops += step_flops(float(n_t), float(a0), float(a1))
+            nbytes += step_bytes(float(n_t), float(a0), float(a1))
+            preds += 1
+    return flops, nbytes, preds
+
+
+def roofline(flops_per_step, bytes_per_step, kernel_ms_per_step, launches_per_step, traffic):
+    t = kernel_ms_per_step * 1e-3
+    achieved = flops_per_step / t / 1e12 if t > 0 else 0.0
+    return {
+        "bound": "mfma",
+        "achieved": achieved,
+        "peak": PEAK_FP32_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": achieved / PEAK_FP32_TFLOPS,
+        "traffic": traffic,
+        "algorithmic_flops_per_launch": flops_per_step / max(1e-9, launches_per_step),
+        "algorithmic_bytes_per_launch": bytes_per_step / max(1e-9, launches_per_step),
+        "kernel_ms_per_launch": kernel_ms_per_step / max(1e-9, launches_per_step),
+        "hbm_achieved_GBs": bytes_per_step / t / 1e9 if t > 0 else 0.0,
+        "hbm_frac": (bytes_per_step / t / 1e9) / PEAK_HBM_GBS if t > 0 else 0.0,
+    }
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    dev = None
     if world > 1:
         import torch
         import torch.distributed as tdist
         torch.cuda.set_device(local)
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
         dist = tdist
+        dev = "cuda"
 
-    from mdcommunity_amd import _lib, engine, gmm
+    from mdcommunity_amd import _lib, engine, gmm, parallel
 
     weights = engine.load_weights(engine.DEFAULT_UNIT)
     eng = _lib.Engine(weights, device=local if world > 1 else 0)
-    if args.workload == "single":
-        seeds = [args.seed]
-    else:
-        seeds = [rank * args.graphs_per_rank + i for i in range(args.graphs_per_rank)]
-    graphs = [(args.n,) + gmm.gmm_pair(args.n, seed=s) for s in seeds]
-    eng.load_graphs(graphs)
-
-    def one_step():
-        mr = eng.reset()
-        outs = eng.rollout()
-        ms, launches = eng.last_timing()
-        return mr, outs, ms, launches
-
-    for _ in range(max(0, args.warmup)):
-        one_step()
+    edges = gmm.gmm_pair(args.n, seed=args.seed)
+    eng.load_graphs([(args.n,) + edges])
 
     def sync():
         if dist is not None:
@@ -116,59 +166,69 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    sync()
-    t0 = time.perf_counter()
-    kernel_ms, launches, removals = 0.0, 0, 0
-    last = None
-    for _ in range(args.steps):
-        mr, outs, ms, nl = one_step()
-        kernel_ms += ms
-        launches += nl
-        removals += sum(len(o[0]) for o in outs)
-        last = (mr, outs)
-    sync()
-    elapsed = time.perf_counter() - t0
-
-    # roofline accounting from the device's own per-prediction trace
-    flops = 0.0
-    nbytes = 0.0
-    for gidx in range(len(graphs)):
-        tr = eng.trace(gidx)
-        for n_t, a0, a1 in zip(tr["n_live"], tr["m0"], tr["m1"]):
-            flops += step_flops(float(n_t), float(a0), float(a1))
-            nbytes += step_bytes(float(n_t), float(a0), float(a1))
-    mr, outs = last
-    audc = []
-    for (n, _, _), m, (seq, ranks) in zip(graphs, mr, outs):
-        s = 0.0
-        for r in ranks:
-            s += -1 * (-float(r) / (int(m) * float(n)))
-        audc.append(s)
-
-    tot_removals = removals
-    max_elapsed = elapsed
-    all_audc = audc
+    # ---------------- headline: single graph rollouts (configs[1]); --steps 0 skips it (profiling
+    # the batch object alone)
+    kernel_ms, launches, removals, elapsed, s0_ms = 0.0, 0, 0, 1e-9, 0.0
+    flops = nbytes = 0.0
+    preds, audc, seq = 0, None, np.zeros(0, np.int32)
+    if args.steps > 0:
+        run_steps(eng, max(0, args.warmup))
+        sync()
+        t0 = time.perf_counter()
+        kernel_ms, launches, removals, last, s0_ms = run_steps(eng, args.steps)
+        sync()
+        elapsed = time.perf_counter() - t0
+        flops, nbytes, preds = trace_work(eng, 1)
+        mr, outs = last
+        seq, ranks = outs[0]
+        audc = audc_of(ranks, mr[0], args.n)
+    tot_removals, max_elapsed = removals, elapsed
     if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        max_elapsed = float(t.item())
-        r = torch.tensor([removals], dtype=torch.int64, device="cuda")
-        dist.all_reduce(r, op=dist.ReduceOp.SUM)
-        tot_removals = int(r.item())
-        a = torch.tensor(audc, dtype=torch.float64, device="cuda")
-        gathered = [torch.zeros_like(a) for _ in range(world)]
-        dist.all_gather(gathered, a)  # per-graph AUDC scalars to every rank (RCCL over xGMI)
-        all_audc = [float(x) for g in gathered for x in g.tolist()]
+        max_elapsed = parallel.max_over_ranks(dist, elapsed, dev)
+        tot_removals = parallel.sum_over_ranks(dist, removals, dev)
+
+    # ---------------- batch object (configs[2] per GPU; configs[4] shape across ranks)
+    batch = None
+    if args.batch_graphs > 0:
+        total = args.batch_graphs * world
+        lo, hi = parallel.shard(total, rank, world)
+        bgraphs = [(args.n,) + gmm.gmm_pair(args.n, seed=s) for s in range(lo, hi)]
+        beng = _lib.Engine(weights, device=local if world > 1 else 0)
+        beng.load_graphs(bgraphs)
+        run_steps(beng, 1)
+        sync()
+        tb = time.perf_counter()
+        bk_ms, bl, brem, blast, _ = run_steps(beng, args.batch_steps)
+        sync()
+        belapsed = time.perf_counter() - tb
+        bflops, bbytes, _ = trace_work(beng, len(bgraphs))
+        bmr, bouts = blast
+        baudc = [audc_of(r, m, n) for (n, _, _), m, (_, r) in zip(bgraphs, bmr, bouts)]
+        brem_per_graph = [len(s) for s, _ in bouts]
+        if dist is not None:
+            baudc, brem_per_graph = parallel.gather_results(dist, baudc, brem_per_graph, dev)  # RCCL over xGMI
+            belapsed = parallel.max_over_ranks(dist, belapsed, dev)
+            brem = parallel.sum_over_ranks(dist, brem, dev)
+        beng.close()
+        batch = {
+            "workload": "%d 2-layer GMM graphs N=%d (seeds 0..%d, %d per GPU), full rollouts per step"
+                        % (total, args.n, total - 1, args.batch_graphs),
+            "value": brem / belapsed,
+            "unit": "removals/s",
+            "steps": args.batch_steps,
+            "ms_per_step": belapsed / args.batch_steps * 1e3,
+            "removals_per_step": brem / args.batch_steps,
+            "audc_mean": float(np.mean(baudc)),
+            "graphs": len(baudc),
+            "roofline": roofline(bflops, bbytes, bk_ms / args.batch_steps, bl / args.batch_steps, None),
+        }
 
     if rank == 0:
         golden = None
         gpath = os.path.join(ROOT, "tests", "golden", f"rollout_gmm1000_s{args.seed}.npz")
-        if args.workload == "single" and args.n == 1000 and os.path.exists(gpath):
+        if args.n == 1000 and os.path.exists(gpath):
             z = np.load(gpath)
             golden = dict(audc=float(z["score"]), seq=z["seq"].tolist())
-        per_launch_ms = kernel_ms / max(1, launches)
-        achieved_tflops = flops / args.steps / (kernel_ms / args.steps * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
         traffic = None
         tfile = os.path.join(ROOT, "profiles", "traffic_r01.json")
         if os.path.exists(tfile):
@@ -181,44 +241,34 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": max_elapsed / args.steps * 1e3,
+            "ms_per_step": max_elapsed / max(1, args.steps) * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic (GMM generator = reference U/GMM.py streams)",
+            "data": "synthetic (GMM generator = reference U/GMM.py streams; random seed graphs)",
             "config": {
-                "workload": ("single 2-layer GMM graph N=%d seed %d, full rollout per step" % (args.n, args.seed))
-                if args.workload == "single" else
-                ("%d 2-layer GMM graphs N=%d per GPU, sharded by seed, full rollouts per step"
-                 % (args.graphs_per_rank, args.n)),
-                "graphs_per_gpu": len(graphs),
+                "workload": "single 2-layer GMM graph N=%d seed %d, unit cost, full rollout per step "
+                            "(one replica per GPU)" % (args.n, args.seed),
                 "n_nodes": args.n,
-                "removals_per_step": tot_removals / args.steps,
-                "parallelism": "replicas" if args.workload == "single" else "graph-sharded dp%d" % world,
-                "checkpoint": "U/models/g0.5_TORCH-Model_GMM_30_50/nrange_30_50_iter_100000.ckpt",
+                "removals_per_step": tot_removals / max(1, args.steps),
+                "parallelism": "replicas x%d" % world,
+                "checkpoint": CKPT,
             },
-            "audc": all_audc[0] if len(all_audc) == 1 else float(np.mean(all_audc)),
-            "audc_match": (abs(all_audc[0] - golden["audc"]) == 0.0) if golden else None,
-            "seq_match": (outs[0][0].tolist() == golden["seq"]) if golden else None,
-            "kernel_ms_per_step": kernel_ms / args.steps,
-            "launches_per_step": launches / args.steps,
-            "roofline": {
-                "bound": "mfma",
-                "achieved": achieved_tflops,
-                "peak": PEAK_FP32_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": achieved_tflops / PEAK_FP32_TFLOPS,
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": nbytes / args.steps / max(1e-9, launches / args.steps),
-                "algorithmic_flops_per_launch": flops / args.steps / max(1e-9, launches / args.steps),
-                "kernel_ms_per_launch": per_launch_ms,
-                "hbm_frac": (nbytes / args.steps / (kernel_ms / args.steps * 1e-3) / 1e9) / PEAK_HBM_GBS
-                if kernel_ms > 0 else 0.0,
-            },
+            "audc": audc,
+            "audc_match": (audc == golden["audc"]) if golden and audc is not None else None,
+            "seq_match": (seq.tolist() == golden["seq"]) if golden and audc is not None else None,
+            "kernel_ms_per_step": kernel_ms / max(1, args.steps),
+            "s0_kernel_ms_per_step": s0_ms / max(1, args.steps),
+            "launches_per_step": launches / max(1, args.steps),
+            "predictions_per_step": preds,
+            "roofline": roofline(flops, nbytes, kernel_ms / max(1, args.steps), launches / max(1, args.steps), traffic),
+            "batch": batch,
         }
-        if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(graphs[0][1:], args.n, args.cpu_sample_seconds)
+        if world == 1 and not args.no_cpu_baseline and args.steps > 0:
+            cb = cpu_baseline(edges, args.n, args.cpu_sample_seconds)
+            line["cpu_baseline"] = cb
+            line["vs_cpu_baseline"] = line["value"] / cb["value"]
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

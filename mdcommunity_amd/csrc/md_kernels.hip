@@ -877,7 +877,10 @@ __device__ __forceinline__ int tile_graph(const int* pref, int ng, int t) {
 }
 
 // ------------------------------------------------------------------ the kernel
-__global__ void __launch_bounds__(NTHREADS, 1) md_rollout_kernel(Params p, const float* __restrict__ wimg) {
+// One body, two entry points so profiles separate the work: md_rollout_kernel runs whole
+// rollouts (RUN_ROLLOUT); md_env_kernel runs single environment steps and predictions
+// (RUN_STEP: MvcEnv.s0 / queued actions, RUN_PREDICT).
+__device__ __forceinline__ void engine_body(const Params& p, const float* __restrict__ wimg) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* scr = lds + L_SCR;
   int* pref = (int*)(lds + L_PREF);
@@ -1036,6 +1039,14 @@ __global__ void __launch_bounds__(NTHREADS, 1) md_rollout_kernel(Params p, const
   }
 }
 
+__global__ void __launch_bounds__(NTHREADS, 1) md_rollout_kernel(Params p, const float* __restrict__ wimg) {
+  engine_body(p, wimg);
+}
+
+__global__ void __launch_bounds__(NTHREADS, 1) md_env_kernel(Params p, const float* __restrict__ wimg) {
+  engine_body(p, wimg);
+}
+
 // Reset every graph in glist to the initial (pre-s0) state.
 __global__ void md_reset_kernel(Params p) {
   const int gidx = blockIdx.x;
@@ -1101,7 +1112,10 @@ void build_weight_image(const float* w, float* img) {
 }
 
 hipError_t launch_rollout(const Params& p, const float* wimg, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(md_rollout_kernel, dim3(grid), dim3(NTHREADS), lds_bytes(), s, p, wimg);
+  if (p.run_mode == RUN_ROLLOUT)
+    hipLaunchKernelGGL(md_rollout_kernel, dim3(grid), dim3(NTHREADS), lds_bytes(), s, p, wimg);
+  else
+    hipLaunchKernelGGL(md_env_kernel, dim3(grid), dim3(NTHREADS), lds_bytes(), s, p, wimg);
   return hipGetLastError();
 }
 
@@ -1111,7 +1125,9 @@ hipError_t launch_reset(const Params& p, hipStream_t s) {
 }
 
 hipError_t set_kernel_attrs() {
-  return hipFuncSetAttribute((const void*)md_rollout_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             lds_bytes());
+  hipError_t e = hipFuncSetAttribute((const void*)md_rollout_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     lds_bytes());
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)md_env_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes());
 }
 }  // namespace md
