@@ -182,6 +182,17 @@ def main():
         mr, outs = last
         seq, ranks = outs[0]
         audc = audc_of(ranks, mr[0], args.n)
+    # host-buffer-inclusive rate (edge lists uploaded over PCIe by md_load_graphs, sequences
+    # read back): reported beside `value`, never as it (Measurement)
+    pcie_rate = None
+    if args.steps > 0:
+        tp = time.perf_counter()
+        prem = 0
+        for _ in range(3):
+            eng.load_graphs([(args.n,) + edges])
+            eng.reset()
+            prem += sum(len(o[0]) for o in eng.rollout())
+        pcie_rate = prem / (time.perf_counter() - tp)
     tot_removals, max_elapsed = removals, elapsed
     if dist is not None:
         max_elapsed = parallel.max_over_ranks(dist, elapsed, dev)
@@ -262,6 +273,7 @@ def main():
             "s0_kernel_ms_per_step": s0_ms / max(1, args.steps),
             "launches_per_step": launches / max(1, args.steps),
             "predictions_per_step": preds,
+            "pcie_inclusive_value": pcie_rate,
             "roofline": roofline(flops, nbytes, kernel_ms / max(1, args.steps), launches / max(1, args.steps), traffic),
             "batch": batch,
         }

@@ -56,7 +56,11 @@ typedef struct md_ctx md_ctx;
  * choice is `np.argsort(-q)[:step]` (U/MultiDismantler_torch.py:769), i.e. numpy's
  * unstable sort order, so the library hands the masked Q row (float64, masked entries =
  * -1073741823.5 as U/MultiDismantler_torch.py:60,291-299) to the host, which writes
- * `n_out` node ids, best first, into `actions`.  Return 0 on success. */
+ * `n_out` node ids, best first, into `actions`.  Return 0 on success.
+ * The callback runs on the calling thread while the rollout kernel waits for its answer
+ * (the Q row and the answer travel through mapped pinned memory; no relaunch), so it must
+ * return within 60 s (else MD_ETIMEOUT); MD_HOST_HANDSHAKE=0 in the environment falls back
+ * to ending the launch and relaunching after the callback. */
 typedef int (*md_select_cb)(void* user, int graph, const double* q, int n_nodes, int n_out,
                             int32_t* actions);
 
@@ -125,12 +129,12 @@ md_status md_get_state(md_ctx* ctx, int graph, uint8_t* covered, uint8_t* remove
 md_status md_set_state(md_ctx* ctx, int graph, const uint8_t* covered, const uint8_t* removed0,
                        const uint8_t* removed1);
 
-/* Execution geometry: workgroups cooperating on one graph ("team"), 0 = automatic
- * (whole GPU for one graph, one workgroup per graph for large batches). */
+/* Execution geometry override: number of tile workgroups of a launch, 0 = automatic
+ * (one per 16-node tile, at most one workgroup per CU).  Results do not depend on it. */
 md_status md_set_team_size(md_ctx* ctx, int team_size);
 
-/* Device time (ms) of the last md_rollout / md_predict kernel launches, measured with HIP
- * events on the context's stream, and the number of launches they took. */
+/* Device time (ms) of the kernel launches of the last md_reset / md_predict / md_step /
+ * md_rollout call, measured with HIP events on the context's stream, and their count. */
 md_status md_last_timing(md_ctx* ctx, double* kernel_ms, int32_t* launches);
 
 /* Diagnostics: record device wall-clock (100 MHz) phase timestamps of workgroup 0,
