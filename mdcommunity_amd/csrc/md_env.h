@@ -28,7 +28,8 @@ typedef __attribute__((address_space(3))) v4u lds_u4;
   } while (0)
 
 // Profile accumulators (slots 16.. of a profiled step; workgroup 0, thread 0 writes).
-enum { PA_ROUNDS = 0, PA_UNITE = 1, PA_LABEL = 2, PA_PRUNE = 3, PA_COUNT = 4, PA_CALLS = 5, PA_COVER = 6 };
+enum { PA_ROUNDS = 0, PA_UNITE = 1, PA_LABEL = 2, PA_PRUNE = 3, PA_COUNT = 4, PA_CALLS = 5, PA_COVER = 6,
+       PA_INIT = 16, PA_FINDONLY = 17, PA_EDGES = 18, PA_UNIONS = 19 };  // 16+: slots 32.. of the step
 #define PACC(acc, slot, t0)                                                          \
   do {                                                                               \
     if ((acc) != nullptr && threadIdx.x == 0) (acc)[slot] += wall_clock64() - (t0);  \
@@ -122,15 +123,21 @@ __device__ __forceinline__ void uf_unite2(P par, int a, int b) {
 struct EnvLayout {
   int ew;                        // words of the edge region
   int cov;                       // byte offset of the covered flags
+  int al0, al1, dl;              // byte offsets of the alive-edge lists (ping-pong) and the dead list
+  int hdr;                       // word offset of {alive count, dead count, current list}
   int par0, par1, deg0, deg1, tmp, total;
 };
 __host__ __device__ inline EnvLayout env_layout(int n, int et) {
   EnvLayout L;
   const int e8 = (et + 7) & ~7, e16 = (et + 15) & ~15;
-  L.cov = 4 * e8 + 2 * e16;
-  const int eb = L.cov + ((n + 15) & ~15);
+  L.cov = 4 * e8 + e16;                       // u16 u, u16 v, u8 state
+  L.al0 = L.cov + ((n + 15) & ~15);           // u16 edge ids
+  L.al1 = L.al0 + 2 * e8;
+  L.dl = L.al1 + 2 * e8;
+  const int eb = L.dl + 2 * e8;
   L.ew = ((eb + 15) / 16) * 4;
-  L.par0 = L.ew;
+  L.hdr = L.ew;
+  L.par0 = L.hdr + 4;
   L.par1 = L.par0 + n;
   L.deg0 = L.par1 + n;
   L.deg1 = L.deg0 + n;
@@ -152,8 +159,11 @@ struct EnvView {
   lds_u16* u16;                 // LDS mode: endpoints [et]
   lds_u16* v16;
   lds_u8* st;                   // LDS mode: edge states [et]
-  lds_u8* st_old;               // LDS mode: edge states at the last write-back
   lds_u8* cov8;                 // LDS mode: covered flags [n]
+  lds_u16* al;                  // LDS mode: alive edge ids (current list, al_n() entries)
+  lds_u16* al_other;            //           the other half of the ping-pong pair
+  lds_u16* dl;                  //           edges killed since the last write-back
+  lds_i32* hdr;                 //           {alive count, dead count, current list 0/1}
   const int* gu[2];             // global mode
   const int* gv[2];
   uint8_t* gst[2];
@@ -243,135 +253,75 @@ __device__ __forceinline__ int2 block_sum2(int a, int b, int* tmp) {
   return r;
 }
 
-// ------------------------------------------------------------------ unions
-// Union of every alive edge (both layers) into par0 / par1, four unions in flight per thread:
-// each iteration loads the parents of all current endpoints (eight independent LDS loads),
-// then every union advances one hop with path splitting, stops when both ends meet, or hooks
-// root hi -> lo with compare-and-swap (a failed CAS re-reads next iteration).
-template <bool GL>
-__device__ void unite_lockstep(const EnvView<GL>& E) {
-  constexpr int K = 4;
-  int gcur = (int)threadIdx.x - NTHREADS, kk = 8, ge = threadIdx.x;
-  v4u U = (v4u)(0u), V = U;
-  v2u S = (v2u)(0u);
-  const int ngr = (E.et + 7) >> 3;
-  auto feed = [&](int& a, int& b, int& l) -> bool {
-    if constexpr (GL) {
-      while (ge < E.et) {
-        const int e = ge;
-        ge += NTHREADS;
-        if (E.state(e) == E_ALIVE) {
-          a = E.u(e);
-          b = E.v(e);
-          l = e < E.e0 ? 0 : 1;
-          return true;
-        }
-      }
-      return false;
-    } else {
-      while (true) {
-        if (kk == 8) {
-          gcur += NTHREADS;
-          if (gcur >= ngr) return false;
-          U = ((const lds_u4*)E.u16)[gcur];
-          V = ((const lds_u4*)E.v16)[gcur];
-          S = ((const lds_u2*)E.st)[gcur];
-          kk = 0;
-        }
-        const int k = kk++;
-        const int e = 8 * gcur + k;
-        if (e >= E.et) {
-          kk = 8;
-          continue;
-        }
-        const unsigned sw = k < 4 ? S.x : S.y;
-        if (((sw >> (8 * (k & 3))) & 0xffu) != E_ALIVE) continue;
-        const unsigned uw = sel4(U, k >> 1), vw = sel4(V, k >> 1);
-        a = (int)((uw >> (16 * (k & 1))) & 0xffffu);
-        b = (int)((vw >> (16 * (k & 1))) & 0xffffu);
-        l = e < E.e0 ? 0 : 1;
-        return true;
-      }
-    }
-  };
-  int x[K], y[K], xp[K], yp[K], lay[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    int l = -1;
-    lay[k] = feed(x[k], y[k], l) ? l : -1;
-    xp[k] = yp[k] = -1;
-  }
-  while (lay[0] >= 0 || lay[1] >= 0 || lay[2] >= 0 || lay[3] >= 0) {
-    int fx[K], fy[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      if (lay[k] >= 0) {
-        auto par = lay[k] ? E.par1 : E.par0;
-        fx[k] = uf_load(par, x[k]);
-        fy[k] = uf_load(par, y[k]);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      if (lay[k] < 0) continue;
-      auto par = lay[k] ? E.par1 : E.par0;
-      const bool rx = fx[k] == x[k], ry = fy[k] == y[k];
-      if (!rx) {
-        if (xp[k] >= 0) uf_store(par, xp[k], fx[k]);  // path splitting
-        xp[k] = x[k];
-        x[k] = fx[k];
-      }
-      if (!ry) {
-        if (yp[k] >= 0) uf_store(par, yp[k], fy[k]);
-        yp[k] = y[k];
-        y[k] = fy[k];
-      }
-      bool done = x[k] == y[k];
-      if (!done && rx && ry) {
-        const int hi = max(x[k], y[k]), lo = min(x[k], y[k]);
-        done = uf_cas(par, hi, hi, lo) == hi;
-      }
-      if (done) {
-        int l = -1;
-        lay[k] = feed(x[k], y[k], l) ? l : -1;
-        xp[k] = yp[k] = -1;
-      }
+// ------------------------------------------------------------------ alive-edge list
+// LDS mode keeps the ids of the alive edges in a compact list (edges only die during a
+// rollout), so the per-step passes -- cover, unions, prune, degrees -- touch the alive edges
+// only and every lane of a wave has work; the edges killed since the last write-back are kept
+// in the dead list.  Global mode scans all edges.
+template <bool GL, class F>
+__device__ __forceinline__ void for_each_alive(const EnvView<GL>& E, F&& f) {
+  if constexpr (GL) {
+    for (int e = threadIdx.x; e < E.et; e += NTHREADS)
+      if (E.state(e) == E_ALIVE) f(e, E.u(e), E.v(e));
+  } else {
+    const int na = E.hdr[0];
+    const lds_u16* al = E.hdr[2] ? E.al_other : E.al;
+    for (int i = threadIdx.x; i < na; i += NTHREADS) {
+      const int e = al[i];
+      if (E.st[e] == E_ALIVE) f(e, (int)E.u16[e], (int)E.v16[e]);
     }
   }
 }
 
-// Union of every alive edge (both layers): per group of eight edges the parents of all
-// sixteen endpoints are loaded at once, edges whose endpoints already share a parent are
-// skipped, the rest start their lockstep climb one hop up.
+// Builds the alive list from the staged edge states (ascending edge ids).
 template <bool GL>
-__device__ void unite_all(const EnvView<GL>& E) {
-  if constexpr (GL) {
-    for (int e = threadIdx.x; e < E.et; e += NTHREADS)
-      if (E.state(e) == E_ALIVE) uf_unite(e < E.e0 ? E.par0 : E.par1, E.u(e), E.v(e));
-  } else {
-    const int ng = (E.et + 7) >> 3;
-    for (int g = threadIdx.x; g < ng; g += NTHREADS) {
-      const v4u U = ((const lds_u4*)E.u16)[g];
-      const v4u V = ((const lds_u4*)E.v16)[g];
-      const v2u S = ((const lds_u2*)E.st)[g];
-      int pu[8], pv[8];
-      bool al[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int e = 8 * g + k;
-        const unsigned sw = k < 4 ? S.x : S.y;
-        al[k] = e < E.et && ((sw >> (8 * (k & 3))) & 0xffu) == E_ALIVE;
-        if (al[k]) {
-          auto par = e < E.e0 ? E.par0 : E.par1;
-          const unsigned uw = sel4(U, k >> 1), vw = sel4(V, k >> 1);
-          pu[k] = uf_load(par, (int)((uw >> (16 * (k & 1))) & 0xffffu));
-          pv[k] = uf_load(par, (int)((vw >> (16 * (k & 1))) & 0xffffu));
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (al[k] && pu[k] != pv[k]) uf_unite2(8 * g + k < E.e0 ? E.par0 : E.par1, pu[k], pv[k]);
+__device__ void build_alive(const EnvView<GL>& E) {
+  if constexpr (!GL) {
+    const int chunk = (E.et + NTHREADS - 1) / NTHREADS;
+    const int e0 = min(E.et, (int)threadIdx.x * chunk), e1 = min(E.et, e0 + chunk);
+    int keep = 0;
+    for (int e = e0; e < e1; ++e) keep += E.st[e] == E_ALIVE;
+    int tot = 0;
+    int k = block_excl_scan(keep, E.tmp, &tot);
+    for (int e = e0; e < e1; ++e)
+      if (E.st[e] == E_ALIVE) E.al[k++] = (uint16_t)e;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      E.hdr[0] = tot;
+      E.hdr[1] = 0;
+      E.hdr[2] = 0;
     }
+    __syncthreads();
+  }
+}
+
+// Drops the entries whose edge died from the alive list (kept entries stay in order) and
+// appends them to the dead list.
+template <bool GL>
+__device__ void compact_alive(const EnvView<GL>& E) {
+  if constexpr (!GL) {
+    const int na = E.hdr[0], nd0 = E.hdr[1], cur = E.hdr[2];
+    const lds_u16* src = cur ? E.al_other : E.al;
+    lds_u16* dst = cur ? E.al : E.al_other;
+    const int chunk = (na + NTHREADS - 1) / NTHREADS;
+    const int i0 = min(na, (int)threadIdx.x * chunk), i1 = min(na, i0 + chunk);
+    int keep = 0;
+    for (int i = i0; i < i1; ++i) keep += E.st[src[i]] == E_ALIVE;
+    int totk = 0, totd = 0;
+    int k = block_excl_scan(keep, E.tmp, &totk);
+    int d = nd0 + block_excl_scan(i1 - i0 - keep, E.tmp, &totd);
+    for (int i = i0; i < i1; ++i) {
+      const int e = src[i];
+      if (E.st[e] == E_ALIVE) dst[k++] = (uint16_t)e;
+      else E.dl[d++] = (uint16_t)e;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      E.hdr[0] = totk;
+      E.hdr[1] = nd0 + totd;
+      E.hdr[2] = 1 - cur;
+    }
+    __syncthreads();
   }
 }
 
@@ -398,19 +348,17 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
       uf_store(E.par1, x, x);
     }
     __syncthreads();
-    // variants 1 / 2 are alternative union orders kept for measurement (both slower on gfx950:
-    // 82 / 28 us against 22 us per step on the GMM N=1000 rollout)
-    if (E.variant & 1) {
-      unite_lockstep<GL>(E);
-    } else if (E.variant & 2) {
-      unite_all<GL>(E);
-    } else {
-      for_each_edge<GL>(E, [&](int e, int u, int v, int s) {
-        if (s == E_ALIVE) uf_unite(e < E.e0 ? E.par0 : E.par1, u, v);
-      });
-    }
+    PACC(acc, PA_INIT, tp);
+    for_each_alive<GL>(E, [&](int e, int u, int v) { uf_unite(e < E.e0 ? E.par0 : E.par1, u, v); });
     __syncthreads();
     PACC(acc, PA_UNITE, tp);
+    if (acc != nullptr && (E.variant & 8)) {
+      // diagnostics: alive edges per round
+      int ne = 0;
+      for_each_alive<GL>(E, [&](int, int, int) { ne++; });
+      const int2 c = block_sum2(ne, 0, E.tmp);
+      if (threadIdx.x == 0) acc[PA_EDGES] += c.x;
+    }
     tp = wall_clock64();
     int diff = 0;
     for (int x = threadIdx.x; x < n; x += NTHREADS) {
@@ -424,8 +372,7 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
     tp = wall_clock64();
     if (!diff) break;
     int c0 = 0, c1 = 0;
-    for_each_edge<GL>(E, [&](int e, int u, int v, int s) {
-      if (s != E_ALIVE) return;
+    for_each_alive<GL>(E, [&](int e, int u, int v) {
       auto other = e < E.e0 ? E.deg1 : E.deg0;  // layer-0 edges are pruned by layer-1 components
       if (uf_load(other, u) != uf_load(other, v)) {
         E.kill(e, E_PRUNED);
@@ -435,6 +382,7 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
     const int2 c = block_sum2(c0, c1, E.tmp);
     pruned0 += c.x;
     pruned1 += c.y;
+    compact_alive<GL>(E);
     PACC(acc, PA_PRUNE, tp);
   }
   const unsigned long long tc = wall_clock64();
@@ -494,8 +442,11 @@ __device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, floa
     E.u16 = (lds_u16*)base8;
     E.v16 = E.u16 + ((et + 7) & ~7);
     E.st = base8 + 4 * ((et + 7) & ~7);
-    E.st_old = E.st + ((et + 15) & ~15);
     E.cov8 = base8 + L.cov;
+    E.al = (lds_u16*)(base8 + L.al0);
+    E.al_other = (lds_u16*)(base8 + L.al1);
+    E.dl = (lds_u16*)(base8 + L.dl);
+    E.hdr = la + L.hdr;
     if (!staged) {
       // batched so every thread keeps 8 independent global loads in flight
       for (int e0b = 0; e0b < et; e0b += 8 * NTHREADS) {
@@ -517,11 +468,12 @@ __device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, floa
             E.u16[e] = (uint16_t)uu[k];
             E.v16[e] = (uint16_t)vv[k];
             E.st[e] = (uint8_t)ss[k];
-            E.st_old[e] = (uint8_t)ss[k];
           }
         }
       }
       for (int x = threadIdx.x; x < n; x += NTHREADS) E.cov8[x] = E.gcov[x];
+      __syncthreads();
+      build_alive<GL>(E);
     }
     __syncthreads();
   }
@@ -542,13 +494,14 @@ __device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, floa
     // cover a in both layers (U/mvc_env.py:74-85): its alive edges become "covered"
     const unsigned long long tcv = wall_clock64();
     int c0 = 0, c1 = 0;
-    for_each_edge<GL>(E, [&](int e, int u, int v, int s) {
-      if (s == E_ALIVE && (u == a || v == a)) {
+    for_each_alive<GL>(E, [&](int e, int u, int v) {
+      if (u == a || v == a) {
         E.kill(e, E_COVERED);
         if (e < e0) c0++; else c1++;
       }
     });
     const int2 c = block_sum2(c0, c1, E.tmp);
+    compact_alive<GL>(E);
     if (threadIdx.x == 0) {
       E.gcov[a] = 1;
       if constexpr (!GL) E.cov8[a] = 1;
@@ -590,8 +543,7 @@ __device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, floa
     uf_store(E.deg1, x, 0);
   }
   __syncthreads();
-  for_each_edge<GL>(E, [&](int e, int u, int v, int s) {
-    if (s != E_ALIVE) return;
+  for_each_alive<GL>(E, [&](int e, int u, int v) {
     auto d = e < e0 ? E.deg0 : E.deg1;
     uf_add(d, u, 1);
     uf_add(d, v, 1);
@@ -696,25 +648,18 @@ __device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, floa
     gv.twohop[1] = th1;
   }
   if constexpr (!GL) {
-    // write back changed edge states; dead edges drop out of the gather's CSR view
-    const int ng8 = (et + 7) >> 3;
-    for (int g = threadIdx.x; g < ng8; g += NTHREADS) {
-      const v2u S = ((const lds_u2*)E.st)[g], O = ((const lds_u2*)E.st_old)[g];
-      if (S.x == O.x && S.y == O.y) continue;
-      ((lds_u2*)E.st_old)[g] = S;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int e = 8 * g + k;
-        const unsigned s = ((k < 4 ? S.x : S.y) >> (8 * (k & 3))) & 0xffu;
-        const unsigned o = ((k < 4 ? O.x : O.y) >> (8 * (k & 3))) & 0xffu;
-        if (e < et && s != o) {
-          const int l = e < e0 ? 0 : 1, kk = e < e0 ? e : e - e0;
-          E.gst[l][kk] = (uint8_t)s;
-          E.calive[l][E.epos[l][2 * kk]] = 0;
-          E.calive[l][E.epos[l][2 * kk + 1]] = 0;
-        }
-      }
+    // write back the edges killed since the last write-back; dead edges drop out of the
+    // gather's CSR view
+    const int nd = E.hdr[1];
+    for (int i = threadIdx.x; i < nd; i += NTHREADS) {
+      const int e = E.dl[i];
+      const int l = e < e0 ? 0 : 1, kk = e < e0 ? e : e - e0;
+      E.gst[l][kk] = E.st[e];
+      E.calive[l][E.epos[l][2 * kk]] = 0;
+      E.calive[l][E.epos[l][2 * kk + 1]] = 0;
     }
+    __syncthreads();
+    if (threadIdx.x == 0) E.hdr[1] = 0;
   }
   MD_PROF_A(14);
   // First-layer embedding by degree (unit cost): X = [d/dmax, d/dmax] (net :252-261),

@@ -61,8 +61,8 @@ constexpr int S_E = S_M + 2 * 128 * LDT;// [2][64][17] new embedding / attention
 constexpr int S_F = S_E + 2 * 64 * LDT; // [2][64][17] tanh features / Q-head input
 constexpr int S_HID = S_F + 2 * 64 * LDT;   // [2][16][33]
 constexpr int S_RED = S_HID + 2 * 16 * 33;  // [2][16][8] sum-of-squares partials
-constexpr int S_DOT = S_RED + 256;          // [16][4] attention gate dot products
-constexpr int S_Q = S_DOT + 64;             // [2][16]
+constexpr int S_DOT = S_RED + 256;          // [16][3] attention gate dot products, [2][16] gates
+constexpr int S_Q = S_DOT + 96;             // [2][16]
 constexpr int S_ROW = S_Q + 32;             // [16] node id per tile row (int)
 constexpr int S_YP = S_ROW + 16;            // [2][4][128] virtual-node GEMV partials
 constexpr int S_YM = S_YP + 1024;           // [2][128]
@@ -217,6 +217,23 @@ __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* tot) {
 
 #include "md_env.h"
 
+// Merge arg-max partial (m2, s2, i2, c2) into (bm, bs, bi, bc); c = 0 marks an empty partial.
+__device__ __forceinline__ void argmax_combine(float& bm, float& bs, int& bi, int& bc, float m2, float s2,
+                                               int i2, int c2) {
+  if (bc == 0) {
+    bm = m2; bs = s2; bi = i2; bc = c2;
+  } else if (m2 > bm) {
+    bs = fmaxf(bm, s2);
+    bm = m2; bi = i2; bc = c2;
+  } else if (m2 == bm) {
+    bc += c2;
+    bi = min(bi, i2);
+    bs = fmaxf(bs, s2);
+  } else {
+    bs = fmaxf(bs, m2);
+  }
+}
+
 // Host selection hand-shake for graph g (ties at the max Q, or a multi-node step): publish
 // the graph's Q row to mapped host memory, raise the request tag, wait for the host's answer
 // (its selection callback = the reference's np.argsort pick), copy the actions to p.pend.
@@ -253,23 +270,6 @@ __device__ __noinline__ int host_handshake(const Params& p, const GraphInfo& gi,
   }
   __syncthreads();
   return max(misc[3], 0);
-}
-
-// Merge arg-max partial (m2, s2, i2, c2) into (bm, bs, bi, bc); c = 0 marks an empty partial.
-__device__ __forceinline__ void argmax_combine(float& bm, float& bs, int& bi, int& bc, float m2, float s2,
-                                               int i2, int c2) {
-  if (bc == 0) {
-    bm = m2; bs = s2; bi = i2; bc = c2;
-  } else if (m2 > bm) {
-    bs = fmaxf(bm, s2);
-    bm = m2; bi = i2; bc = c2;
-  } else if (m2 == bm) {
-    bc += c2;
-    bi = min(bi, i2);
-    bs = fmaxf(bs, s2);
-  } else {
-    bs = fmaxf(bs, m2);
-  }
 }
 
 // Phase A of one graph: reduce the previous prediction, then apply / MCC / features.
@@ -721,8 +721,13 @@ __device__ __noinline__ void head_iteration(const Params& p, float* lds, float* 
 
 // Attention + Q head for one tile whose final embeddings are in S_E (both layers).
 // Writes q for valid rows and this tile's arg-max partial.
+#define TSTAMP(k)                                        \
+  do {                                                   \
+    if (ts != nullptr && threadIdx.x == 0) ts[k] = wall_clock64(); \
+  } while (0)
 __device__ __noinline__ void attention_q_tile(const Params& p, float* lds, float* scr, const GraphInfo& gi, int g,
-                                              const int* rows, float* apart_out, unsigned long long htag) {
+                                              const int* rows, float* apart_out, unsigned long long htag,
+                                              unsigned long long* ts) {
   const float* wi = lds + L_W;
   const int w = wave_id(), l = w >> 2, cb = w & 3, lane = lane_id();
   const int ar = lane & 15, ak = lane >> 4;
@@ -740,14 +745,25 @@ __device__ __noinline__ void attention_q_tile(const Params& p, float* lds, float
     for (int r = 0; r < 4; ++r) atf[col * LDT + 4 * ak + r] = tanhf(a[r] + b);
   }
   __syncthreads();
+  TSTAMP(38);
   float* dot = scr + S_DOT;
-  if (w == 0 && lane < 48) {
-    const int row = lane & 15, kind = lane >> 4;  // 0: F0F0, 1: F1F1, 2: F0F1
-    const float* fa = scr + S_F + (kind == 1 ? 64 * LDT : 0);
-    const float* fb = scr + S_F + (kind == 0 ? 0 : 64 * LDT);
-    float a = 0.f;
-    for (int c = 0; c < 64; ++c) a = fmaf(fa[c * LDT + row] * fb[c * LDT + row], wi[W_ILW + c], a);
-    dot[row * 4 + kind] = a;
+  float* gate = dot + 48;  // [2][16] weight of the other layer per (layer, row)
+  if (w == 0) {
+    if (lane < 48) {
+      const int row = lane & 15, kind = lane >> 4;  // 0: F0F0, 1: F1F1, 2: F0F1
+      const float* fa = scr + S_F + (kind == 1 ? 64 * LDT : 0);
+      const float* fb = scr + S_F + (kind == 0 ? 0 : 64 * LDT);
+      float a = 0.f;
+#pragma unroll 16
+      for (int c = 0; c < 64; ++c) a = fmaf(fa[c * LDT + row] * fb[c * LDT + row], wi[W_ILW + c], a);
+      dot[row * 3 + kind] = a;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are done
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 32) {
+      const int ll = lane >> 4, row = lane & 15;
+      gate[ll * 16 + row] = other_gate(ll, dot[row * 3 + 0], dot[row * 3 + 1], dot[row * 3 + 2], wi[W_ILB]);
+    }
   }
   __syncthreads();
   {
@@ -755,29 +771,50 @@ __device__ __noinline__ void attention_q_tile(const Params& p, float* lds, float
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 4 * ak + r;
-      const float g = other_gate(l, dot[row * 4 + 0], dot[row * 4 + 1], dot[row * 4 + 2], wi[W_ILB]);
-      ate[col * LDT + row] = atf[col * LDT + row] + g * oth[col * LDT + row];
+      ate[col * LDT + row] = atf[col * LDT + row] + gate[l * 16 + row] * oth[col * LDT + row];
     }
   }
   __syncthreads();
   normalize_tile(scr + S_E, scr);
   __syncthreads();
+  TSTAMP(39);
   if (htag != 0ull) head_receive(p, lds, g, htag);
+  TSTAMP(40);
   {
     // e[a] = sum_b (h[a] * y[b]) * cp[b]: the reference's outer product then x cross_product
-    // (net :356-363), a batched [64,64]x[64,1] matmul = an FMA chain over b.
-    const float* ys = lds + L_YS;
-    for (int idx = threadIdx.x; idx < 2 * 16 * 64; idx += NTHREADS) {
-      const int ll = idx >> 10, row = (idx >> 6) & 15, a = idx & 63;
-      const float h = scr[S_E + ll * 64 * LDT + a * LDT + row];
-      const float* yy = ys + ll * 64;
-      float acc = 0.f;
-#pragma unroll 8
-      for (int b = 0; b < 64; ++b) acc = fmaf(h * yy[b], wi[W_ICP + b], acc);
-      scr[S_F + ll * 64 * LDT + a * LDT + row] = acc;
+    // (net :356-363), a batched [64,64]x[64,1] matmul = an FMA chain over b.  Each thread
+    // runs four independent chains of one layer (256 threads per layer).
+    const int ll = threadIdx.x >> 8, t = threadIdx.x & 255;
+    const float* at = scr + S_E + ll * 64 * LDT;
+    float h[4], acc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int idx = t + 256 * k, row = idx >> 6, a = idx & 63;
+      h[k] = at[a * LDT + row];
+      acc[k] = 0.f;
+    }
+    const float4* y4 = (const float4*)(lds + L_YS + ll * 64);
+    const float4* c4 = (const float4*)(wi + W_ICP);
+#pragma unroll 4
+    for (int b4 = 0; b4 < 16; ++b4) {
+      const float4 yv = y4[b4], cv = c4[b4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc[k] = fmaf(h[k] * yv.x, cv.x, acc[k]);
+        acc[k] = fmaf(h[k] * yv.y, cv.y, acc[k]);
+        acc[k] = fmaf(h[k] * yv.z, cv.z, acc[k]);
+        acc[k] = fmaf(h[k] * yv.w, cv.w, acc[k]);
+      }
+    }
+    float* af = scr + S_F + ll * 64 * LDT;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int idx = t + 256 * k, row = idx >> 6, a = idx & 63;
+      af[a * LDT + row] = acc[k];
     }
   }
   __syncthreads();
+  TSTAMP(41);
   float* hid = scr + S_HID;
   if (cb < 2) {
     const float* hf = wi + W_IH1 + cb * 16 * 64;
@@ -798,32 +835,36 @@ __device__ __noinline__ void attention_q_tile(const Params& p, float* lds, float
     ql[ll * 16 + row] = a;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  TSTAMP(42);
+  if (threadIdx.x < 64) {
+    // q = w0 * Q0 + w1 * Q1 per row, and the tile's arg-max partial by a 16-lane butterfly
+    // (max / min index / count / second: order-free, as the sequential scan)
     const float* gs = lds + L_GS;
+    const int lane = threadIdx.x;
     float bm = NEG_INF, bs = NEG_INF;
     int bi = 0x7fffffff, bc = 0;
-    float* qg = p.q + gi.node_off;
-    for (int row = 0; row < 16; ++row) {
-      const int v = rows[row];
-      if (v < 0) continue;
-      const float qq = gs[0] * ql[row] + gs[1] * ql[16 + row];
-      qg[v] = qq;
-      if (qq > bm) {
-        bs = bm;
+    if (lane < 16) {
+      const int v = rows[lane];
+      if (v >= 0) {
+        const float qq = gs[0] * ql[lane] + gs[1] * ql[16 + lane];
+        p.q[gi.node_off + v] = qq;
         bm = qq;
         bi = v;
         bc = 1;
-      } else if (qq == bm) {
-        bc++;
-        bi = min(bi, v);
-      } else if (qq > bs) {
-        bs = qq;
       }
     }
-    apart_out[0] = bm;
-    apart_out[1] = bs;
-    apart_out[2] = __int_as_float(bi);
-    apart_out[3] = __int_as_float(bc);
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      const float m2 = __shfl_xor(bm, o, 64), s2 = __shfl_xor(bs, o, 64);
+      const int i2 = __shfl_xor(bi, o, 64), c2 = __shfl_xor(bc, o, 64);
+      if (c2 != 0) argmax_combine(bm, bs, bi, bc, m2, s2, i2, c2);
+    }
+    if (lane == 0) {
+      apart_out[0] = bm;
+      apart_out[1] = bs;
+      apart_out[2] = __int_as_float(bi);
+      apart_out[3] = __int_as_float(bc);
+    }
   }
   __syncthreads();
 }
@@ -994,8 +1035,10 @@ __device__ __forceinline__ void engine_body(const Params& p, const float* __rest
         MD_PROF_T(23 + 3 * (it - 1));
         update_tile(lds + L_W, scr);
         __syncthreads();
+        if (it == 1) MD_PROF_T(36);
         normalize_tile(scr + S_E, scr);
         __syncthreads();
+        if (it == 1) MD_PROF_T(37);
         if (threadIdx.x < 128) {
           // tile partial sums of the virtual node (rows in ascending compact order from 0)
           const int l = threadIdx.x >> 6, c = threadIdx.x & 63;
@@ -1025,7 +1068,12 @@ __device__ __forceinline__ void engine_body(const Params& p, const float* __rest
         }
         __syncthreads();
         MD_PROF_T(24 + 3 * (it - 1));
-        if (it == 3) attention_q_tile(p, lds, scr, gi, g, rows, p.apart + (size_t)(gi.tile_off + j) * 4, htag);
+        if (it == 3) {
+          unsigned long long* ts = nullptr;
+          if (p.prof != nullptr && (int)blockIdx.x == twg0 && t == t0 && pstep < p.prof_cap)
+            ts = p.prof + (size_t)pstep * PROF_SLOTS;
+          attention_q_tile(p, lds, scr, gi, g, rows, p.apart + (size_t)(gi.tile_off + j) * 4, htag, ts);
+        }
         MD_PROF_T(25 + 3 * (it - 1));
       }
       MD_PROF(3 + 2 * it);
