@@ -565,7 +565,7 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   }
   HIPCHK(c, c->covered.alloc(tn));
   HIPCHK(c, c->live.alloc(tn));
-  if (c->need_gscr) HIPCHK(c, c->gscr.alloc(4 * tn));
+  HIPCHK(c, c->gscr.alloc(4 * tn));  // global-mode environment scratch (16 B per node; always, so MD_VARIANT=64 can force that mode)
   HIPCHK(c, c->pend.alloc(tn));
   HIPCHK(c, c->tr_action.alloc(tn));
   HIPCHK(c, c->tr_rank.alloc(tn));

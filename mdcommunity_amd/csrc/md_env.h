@@ -182,18 +182,18 @@ struct EnvView {
     if constexpr (GL) return gv[layer_of(e)][local(e)]; else return v16[e];
   }
   __device__ __forceinline__ int state(int e) const {
-    if constexpr (GL) return gst[layer_of(e)][local(e)]; else return st[e];
+    if constexpr (GL) return ldc(gst[layer_of(e)] + local(e)); else return st[e];
   }
   __device__ __forceinline__ int covered(int x) const {
-    if constexpr (GL) return gcov[x]; else return cov8[x];
+    if constexpr (GL) return ldc(gcov + x); else return cov8[x];
   }
   // alive -> dead transition (the LDS mode writes back at the end of phase A)
   __device__ __forceinline__ void kill(int e, uint8_t s) const {
     if constexpr (GL) {
       const int l = layer_of(e), k = local(e);
-      gst[l][k] = s;
-      calive[l][epos[l][2 * k]] = 0;
-      calive[l][epos[l][2 * k + 1]] = 0;
+      stc(gst[l] + k, s);
+      stc(calive[l] + epos[l][2 * k], (uint8_t)0);
+      stc(calive[l] + epos[l][2 * k + 1], (uint8_t)0);
     } else {
       st[e] = s;
     }
@@ -458,7 +458,7 @@ __device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, floa
             const int l = e < e0 ? 0 : 1, kk = e < e0 ? e : e - e0;
             uu[k] = E.gu[l][kk];
             vv[k] = E.gv[l][kk];
-            ss[k] = E.gst[l][kk];
+            ss[k] = ldc(E.gst[l] + kk);
           }
         }
 #pragma unroll
@@ -503,7 +503,7 @@ __device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, floa
     const int2 c = block_sum2(c0, c1, E.tmp);
     compact_alive<GL>(E);
     if (threadIdx.x == 0) {
-      E.gcov[a] = 1;
+      stc(E.gcov + a, (uint8_t)1);
       if constexpr (!GL) E.cov8[a] = 1;
     }
     __syncthreads();
@@ -560,9 +560,9 @@ __device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, floa
   int* gdeg1 = p.deg[1] + gi.node_off;
   for (int x = x0; x < x1; ++x) {
     const int d0 = uf_load(E.deg0, x), d1 = uf_load(E.deg1, x);
-    gdeg0[x] = d0;
-    gdeg1[x] = d1;
-    q[x] = NEG_INF;
+    stc(gdeg0 + x, d0);
+    stc(gdeg1 + x, d1);
+    stc(q + x, NEG_INF);
     bad |= ((d0 > 0) != (d1 > 0));
     if (d0 > 0) {
       nlive++;
@@ -633,7 +633,7 @@ __device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, floa
     int k = base;
     int* lv = p.live + gi.node_off;
     for (int x = x0; x < x1; ++x)
-      if (uf_load(E.deg0, x) > 0) lv[k++] = x;
+      if (uf_load(E.deg0, x) > 0) stc(lv + k++, x);
   }
   if (bad && !err) err = ERR_LIVE_MISMATCH;
   const int hd0 = gv.hdmax[0], hd1 = gv.hdmax[1];
@@ -654,9 +654,9 @@ __device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, floa
     for (int i = threadIdx.x; i < nd; i += NTHREADS) {
       const int e = E.dl[i];
       const int l = e < e0 ? 0 : 1, kk = e < e0 ? e : e - e0;
-      E.gst[l][kk] = E.st[e];
-      E.calive[l][E.epos[l][2 * kk]] = 0;
-      E.calive[l][E.epos[l][2 * kk + 1]] = 0;
+      stc(E.gst[l] + kk, (uint8_t)E.st[e]);
+      stc(E.calive[l] + E.epos[l][2 * kk], (uint8_t)0);
+      stc(E.calive[l] + E.epos[l][2 * kk + 1], (uint8_t)0);
     }
     __syncthreads();
     if (threadIdx.x == 0) E.hdr[1] = 0;
@@ -677,7 +677,7 @@ __device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, floa
         const float f = (float)d / (float)dm;
         const float x = fmaxf(fmaf(f, w1, fmaf(f, w0, 0.f)), 0.f);
         const float nr = wave_norm64(x);
-        tab[(size_t)d * EMB + lane] = x / fmaxf(nr, 1e-12f);
+        stc(tab + (size_t)d * EMB + lane, x / fmaxf(nr, 1e-12f));
       }
     }
     if (threadIdx.x == 0) {

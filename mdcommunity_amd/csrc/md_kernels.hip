@@ -66,7 +66,13 @@ constexpr int S_Q = S_DOT + 96;             // [2][16]
 constexpr int S_ROW = S_Q + 32;             // [16] node id per tile row (int)
 constexpr int S_YP = S_ROW + 16;            // [2][4][128] virtual-node GEMV partials
 constexpr int S_YM = S_YP + 1024;           // [2][128]
-constexpr int S_END = S_YM + 256;
+// The neighbour lists alias the virtual-node scratch S_YP/S_YM: the graph-head workgroup
+// never gathers, and shared-mode tile workgroups rebuild the lists after each chain.
+constexpr int S_NBH = S_YP;                 // neighbour-list header (ints, see build_nb_lists)
+constexpr int S_NBL = S_NBH + 136;          // [2][NB_CAP] u16 alive neighbour ids, CSR order
+constexpr int NB_CAP = 2088;                // alive neighbour entries per layer kept for a tile
+constexpr int S_END = S_NBL + NB_CAP;
+constexpr int STG_ROWS = 68;                // neighbour rows per layer staged per batch ([S_M, S_HID))
 constexpr int L_TOTAL = L_SCR + S_END;      // floats of dynamic LDS per workgroup
 // phase A uses [L_W, L_TOTAL) (weights are reloaded afterwards)
 constexpr int A_WORDS = L_TOTAL - L_W;
@@ -76,6 +82,7 @@ static_assert(L_W % 4 == 0 && L_SCR % 4 == 0, "16-byte aligned regions");
 static_assert(sizeof(GraphVar) <= 32 * 4, "GraphVar must fit its LDS slot");
 static_assert(L_TOTAL * 4 + 1024 <= 163840, "LDS budget");
 static_assert(S_END >= 64 * 128 + 128 + 4 + 256, "scratch must hold w_layer1 for the graph head");
+static_assert(2 * STG_ROWS * 64 <= S_HID - S_M, "neighbour staging fits [S_M, S_HID)");
 
 constexpr float NEG_INF = -__builtin_huge_valf();
 constexpr unsigned long long BARRIER_TIMEOUT_TICKS = 400000000ull;  // 4 s at 100 MHz
@@ -123,29 +130,78 @@ __device__ __forceinline__ float wave_norm64(float x) {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
 
+// ------------------------------------------------------------------ inter-workgroup data
+// Every array one workgroup writes and another reads inside a launch moves with agent-scope
+// (sc1) global stores and loads: the hand-off protocol of MI355X_MICROARCH.md
+// (inter-workgroup visibility, first table row: every storing wave drains vmcnt before the
+// barrier arrival, one lane signals with an agent-scope atomic, the consumer polls with an
+// sc1 load and reads after a workgroup barrier), so the grid barrier needs neither an L2
+// write-back nor an L1 invalidate.  Static data (CSR, weights, graph info) use plain loads.
+typedef __attribute__((address_space(1))) int g_i32;
+typedef __attribute__((address_space(1))) unsigned g_u32;
+typedef __attribute__((address_space(1))) float g_f32;
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+typedef float v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ int ldc(const int* a) {
+  return __hip_atomic_load((g_i32*)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ldc(const float* a) {
+  return __hip_atomic_load((g_f32*)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint8_t ldc(const uint8_t* a) {
+  return __hip_atomic_load((g_u8*)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stc(int* a, int v) {
+  __hip_atomic_store((g_i32*)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stc(float* a, float v) {
+  __hip_atomic_store((g_f32*)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stc(uint8_t* a, uint8_t v) {
+  __hip_atomic_store((g_u8*)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 16-byte sc1 accesses through a buffer resource on a wave-uniform base.
+__device__ __forceinline__ float4 ldc4(const float* base, int byte_off) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+  const v4f v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16 /* sc1 */);
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void stc4(float* base, int byte_off, float4 x) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+  const v4f v = {x.x, x.y, x.z, x.w};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, 16 /* sc1 */);
+}
+constexpr int GV_WORDS = (int)(sizeof(GraphVar) / 4);
+// GraphVar of graph g into `dst` (LDS), GV_WORDS threads in parallel; the caller syncs.
+__device__ __forceinline__ void gv_load(const Params& p, int g, GraphVar* dst) {
+  if (threadIdx.x < GV_WORDS) ((int*)dst)[threadIdx.x] = ldc((const int*)(p.gvar + g) + threadIdx.x);
+}
+__device__ __forceinline__ void gv_store(const Params& p, int g, const GraphVar* src) {
+  if (threadIdx.x < GV_WORDS) stc((int*)(p.gvar + g) + threadIdx.x, ((const int*)src)[threadIdx.x]);
+}
+
 // ------------------------------------------------------------------ grid barrier
-// Monotonic counter; agent-scope release before the arrival and acquire after the wait
-// (cdna_hip_programming.md §6 Guideline 16).  Bounded spin: on timeout the error word is set
-// and every later barrier falls through, so the grid drains.
+// Monotonic counter: every wave drains its stores (vmcnt), the workgroup syncs, one lane adds
+// to the counter (agent-scope atomic) and polls it with sc1 loads; all data crossing the
+// barrier is sc1 on both sides.  Bounded spin: on timeout the error word is set and every
+// later barrier falls through, so the grid drains.
 __device__ __forceinline__ void grid_sync(const Params& p, unsigned& target) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   target += gridDim.x;
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(p.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // every inter-workgroup datum is sc1 (see ldc / stc): no release / acquire fences
+    __hip_atomic_fetch_add((g_u32*)p.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load(p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+    while (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (__hip_atomic_load((g_i32*)p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
       __builtin_amdgcn_s_sleep(1);
       if (wall_clock64() - t0 > (p.h_req != nullptr ? HOST_TIMEOUT_TICKS : BARRIER_TIMEOUT_TICKS)) {
         __hip_atomic_store(p.err, ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
 }
@@ -240,7 +296,7 @@ __device__ __forceinline__ void argmax_combine(float& bm, float& bs, int& bi, in
 // Returns the number of actions (0 on error; the error word is set).
 __device__ __noinline__ int host_handshake(const Params& p, const GraphInfo& gi, int g, int npred, int* misc) {
   const unsigned tag = (p.launch_seq << 16) ^ (unsigned)(npred + 1);
-  for (int x = threadIdx.x; x < gi.n; x += NTHREADS) p.h_q[gi.node_off + x] = p.q[gi.node_off + x];
+  for (int x = threadIdx.x; x < gi.n; x += NTHREADS) p.h_q[gi.node_off + x] = ldc(p.q + gi.node_off + x);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -279,7 +335,7 @@ __device__ __noinline__ bool phase_a(const Params& p, int g, bool have_q, float*
   const GraphInfo gi = p.ginfo[g];
   // a dedicated environment workgroup that already stepped this graph in this launch holds
   // its current GraphVar in LDS (nobody else writes it during a launch)
-  if (threadIdx.x == 0 && !(staged && p.n_env > 0)) gv = p.gvar[g];
+  if (!(staged && p.n_env > 0)) gv_load(p, g, &gv);
   __syncthreads();
   if (gv.status != ST_RUN) return staged;
   int pend_n = 0, pend_first = -1;
@@ -294,7 +350,7 @@ __device__ __noinline__ bool phase_a(const Params& p, int g, bool have_q, float*
       const int lane = threadIdx.x;
       const int nt = (gv.n_live + TILE - 1) / TILE;
       for (int j = lane; j < nt; j += 64) {
-        const float4 ap = *(const float4*)(p.apart + (size_t)(gi.tile_off + j) * 4);
+        const float4 ap = ldc4(p.apart, (gi.tile_off + j) * 16);
         const int c = __float_as_int(ap.w);
         if (c == 0) continue;
         argmax_combine(bm, bs, bi, bc, ap.x, ap.y, __float_as_int(ap.z), c);
@@ -352,7 +408,7 @@ __device__ __noinline__ bool phase_a(const Params& p, int g, bool have_q, float*
   __syncthreads();
   if (!stop) {
     const int et = gi.e[0] + gi.e[1];
-    const bool fits = phase_a_fits_lds(gi.n, et);
+    const bool fits = phase_a_fits_lds(gi.n, et) && !(p.variant & 64);  // 64: force global mode (tests)
     float* area = lds + L_W;
     const bool was_staged = staged && fits;
     staged = fits;
@@ -368,7 +424,7 @@ __device__ __noinline__ bool phase_a(const Params& p, int g, bool have_q, float*
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) p.gvar[g] = gv;
+  gv_store(p, g, &gv);
   __syncthreads();
   return staged;
 }
@@ -392,7 +448,6 @@ __device__ __noinline__ void gather_tile(const Params& p, const GraphInfo& gi, i
   } else {
     hp = p.H[l][(it - 2) & 1] + (size_t)gi.node_off * EMB;
   }
-  const float4* hp4 = (const float4*)hp;
   const int r = 4 * (w & 3) + grp;
   const int v = rows[r];
   int rb = 0, re = 0;
@@ -400,8 +455,8 @@ __device__ __noinline__ void gather_tile(const Params& p, const GraphInfo& gi, i
   if (v >= 0) {
     rb = rp[v];
     re = rp[v + 1];
-    const int ov = table ? deg[v] : v;
-    own = hp4[(size_t)ov * 16 + qd];
+    const int ov = table ? ldc(deg + v) : v;
+    own = ldc4(hp, ov * 256 + qd * 16);
   }
   int nch = (re - rb + 15) >> 4;
   nch = max(nch, __shfl_xor(nch, 16, 64));
@@ -409,8 +464,8 @@ __device__ __noinline__ void gather_tile(const Params& p, const GraphInfo& gi, i
   for (int ch = 0; ch < nch; ++ch) {
     const int e = rb + 16 * ch + qd;
     int nb = -1;
-    if (e < re && ca[e]) nb = adj[e];
-    if (table && nb >= 0) nb = deg[nb];
+    if (e < re && ldc(ca + e)) nb = adj[e];
+    if (table && nb >= 0) nb = ldc(deg + nb);
     const unsigned long long m = __ballot(nb >= 0);
     unsigned gm = (unsigned)(m >> (16 * grp)) & 0xFFFFu;
     // the alive neighbours in CSR order (== reference in_edges order), 4 rows x 4 loads in flight
@@ -429,7 +484,7 @@ __device__ __noinline__ void gather_tile(const Params& p, const GraphInfo& gi, i
       for (int k = 0; k < 4; ++k) src[k] = __shfl(nb, 16 * grp + (j[k] < 0 ? 0 : j[k]), 64);
       float4 x[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) x[k] = j[k] >= 0 ? hp4[(size_t)src[k] * 16 + qd] : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int k = 0; k < 4; ++k) x[k] = j[k] >= 0 ? ldc4(hp, src[k] * 256 + qd * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         if (j[k] >= 0) {
@@ -440,6 +495,159 @@ __device__ __noinline__ void gather_tile(const Params& p, const GraphInfo& gi, i
         }
       }
     }
+  }
+  float* atp = scr + S_P + l * 64 * LDT;
+  float* atx = scr + S_X + l * 64 * LDT;
+  const int c = 4 * qd;
+  atp[(c + 0) * LDT + r] = acc.x;
+  atp[(c + 1) * LDT + r] = acc.y;
+  atp[(c + 2) * LDT + r] = acc.z;
+  atp[(c + 3) * LDT + r] = acc.w;
+  atx[(c + 0) * LDT + r] = own.x;
+  atx[(c + 1) * LDT + r] = own.y;
+  atx[(c + 2) * LDT + r] = own.z;
+  atx[(c + 3) * LDT + r] = own.w;
+}
+
+// Alive neighbour lists of the tile's rows for both layers (waves 0-3: layer 0, 4-7: layer
+// 1), in CSR order (= reference in_edges order), kept in LDS for the three iterations of a
+// step.  Header (ints at S_NBH): off[2][16], cnt[2][16] (alive, per row), rawb[2][16],
+// rawc[2][16] (CSR extent), tot[2].  Returns false when a layer has more than NB_CAP alive
+// entries (the tile then uses gather_tile).
+__device__ __noinline__ bool build_nb_lists(const Params& p, const GraphInfo& gi, const int* rows, float* scr) {
+  const int w = wave_id(), l = w >> 2, lane = lane_id(), t = threadIdx.x & 255;
+  lds_i32* hdr = (lds_i32*)(int*)(scr + S_NBH);
+  lds_i32* tmp = (lds_i32*)(int*)(scr + S_RED);  // [2][4] wave totals
+  lds_u16* nbl = (lds_u16*)(uint16_t*)(scr + S_NBL) + l * NB_CAP;
+  const int* rp = p.rowptr[l] + gi.roff[l];
+  const int* adj = p.adj[l] + gi.coff[l];
+  const uint8_t* ca = p.calive[l] + gi.coff[l];
+  if (t < 16) {
+    const int v = rows[t];
+    int b = 0, c = 0;
+    if (v >= 0) {
+      b = rp[v];
+      c = rp[v + 1] - b;
+    }
+    hdr[64 + l * 16 + t] = b;
+    hdr[96 + l * 16 + t] = c;
+    hdr[32 + l * 16 + t] = 0;
+  }
+  __syncthreads();
+  int pre[17];
+  pre[0] = 0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) pre[r + 1] = pre[r] + hdr[96 + l * 16 + r];
+  const int T = pre[16];
+  const int chunk = (T + 255) >> 8;
+  const int i0 = min(T, t * chunk), i1 = min(T, i0 + chunk);
+  // my entries: alive flags and neighbour ids, 8 loads in flight at a time
+  int keep = 0;
+  int r = 0;
+  while (r < 15 && pre[r + 1] <= i0) ++r;
+  for (int i = i0; i < i1; ++i) {
+    while (pre[r + 1] <= i) ++r;
+    const int pos = hdr[64 + l * 16 + r] + (i - pre[r]);
+    keep += ldc(ca + pos) != 0;
+  }
+  // exclusive scan of keep over the layer's 256 threads
+  int incl = keep;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) tmp[w] = incl;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int x = tmp[l * 4 + k];
+    if (k < (w & 3)) base += x;
+    tot += x;
+  }
+  int o = base + incl - keep;
+  r = 0;
+  while (r < 15 && pre[r + 1] <= i0) ++r;
+  for (int i = i0; i < i1; ++i) {
+    while (pre[r + 1] <= i) ++r;
+    const int pos = hdr[64 + l * 16 + r] + (i - pre[r]);
+    if (ldc(ca + pos)) {
+      if (o < NB_CAP) nbl[o] = (uint16_t)adj[pos];
+      ++o;
+      __hip_atomic_fetch_add(hdr + 32 + l * 16 + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  __syncthreads();
+  if (t < 16) {
+    int off = 0;
+    for (int k = 0; k < t; ++k) off += hdr[32 + l * 16 + k];
+    hdr[l * 16 + t] = off;
+    if (t == 0) hdr[128 + l] = tot;
+  }
+  const int over = __syncthreads_or(tot > NB_CAP);
+  return !over;
+}
+
+// Gather for one tile from the alive neighbour lists: per batch the layer's 256 threads stage
+// up to STG_ROWS neighbour rows (five 16-byte loads in flight per thread) into [S_M, S_HID),
+// then each 16-lane group adds its row's neighbours in CSR order (the reference's sequential
+// scatter-add order).  Same results as gather_tile; high-degree rows no longer serialise
+// their loads.
+__device__ __noinline__ void gather_tile2(const Params& p, const GraphInfo& gi, int it, const int* rows, float* scr) {
+  const int w = wave_id(), l = w >> 2, lane = lane_id(), t = threadIdx.x & 255;
+  const int grp = lane >> 4, qd = lane & 15;
+  const int* deg = p.deg[l] + gi.node_off;
+  const float* hp;
+  bool table = false;
+  if (it == 1) {
+    hp = p.h0tab[l] + (size_t)gi.node_off * EMB;
+    table = p.node_w == nullptr;
+  } else {
+    hp = p.H[l][(it - 2) & 1] + (size_t)gi.node_off * EMB;
+  }
+  const lds_i32* hdr = (const lds_i32*)(const int*)(scr + S_NBH);
+  const lds_u16* nbl = (const lds_u16*)(const uint16_t*)(scr + S_NBL) + l * NB_CAP;
+  const int r = 4 * (w & 3) + grp;
+  const int v = rows[r];
+  float4 own = {0.f, 0.f, 0.f, 0.f}, acc = {0.f, 0.f, 0.f, 0.f};
+  if (v >= 0) {
+    const int ov = table ? ldc(deg + v) : v;
+    own = ldc4(hp, ov * 256 + qd * 16);
+  }
+  const int myoff = hdr[l * 16 + r], mycnt = hdr[32 + l * 16 + r];
+  const int totl = hdr[128 + l];
+  const int nbat = (max(hdr[128], hdr[129]) + STG_ROWS - 1) / STG_ROWS;
+  float4* stg = (float4*)(scr + S_M) + l * STG_ROWS * 16;
+  for (int b = 0; b < nbat; ++b) {
+    const int base = b * STG_ROWS;
+    int src[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int k = t + 256 * i, row = base + (k >> 4);
+      src[i] = -1;
+      if (k < STG_ROWS * 16 && row < totl) {
+        const int id = nbl[row];
+        src[i] = table ? ldc(deg + id) : id;
+      }
+    }
+    float4 x[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+      if (src[i] >= 0) x[i] = ldc4(hp, src[i] * 256 + ((t + 256 * i) & 15) * 16);
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+      if (src[i] >= 0) stg[t + 256 * i] = x[i];
+    __syncthreads();
+    const int lo = max(myoff, base), hi = min(myoff + mycnt, base + STG_ROWS);
+    for (int k = lo; k < hi; ++k) {
+      const float4 y = stg[(k - base) * 16 + qd];
+      acc.x = acc.x + y.x;
+      acc.y = acc.y + y.y;
+      acc.z = acc.z + y.z;
+      acc.w = acc.w + y.w;
+    }
+    __syncthreads();
   }
   float* atp = scr + S_P + l * 64 * LDT;
   float* atx = scr + S_X + l * 64 * LDT;
@@ -525,7 +733,7 @@ __device__ void graph_sum(const Params& p, const GraphInfo& gi, int nt, int slot
   for (int jb = j0; jb < j1; jb += 16) {
     float x[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) x[k] = jb + k < j1 ? sp[(size_t)(jb + k) * 384] : 0.f;
+    for (int k = 0; k < 16; ++k) x[k] = jb + k < j1 ? ldc(sp + (size_t)(jb + k) * 384) : 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k)
       if (jb + k < j1) a = a + x[k];
@@ -669,16 +877,15 @@ __device__ __noinline__ void graph_head(const Params& p, float* lds, float* scr,
 constexpr int HB_FLOATS = 144;
 __device__ __forceinline__ void head_publish(const Params& p, const float* lds, int g, unsigned long long htag) {
   if (threadIdx.x < HB_FLOATS)
-    __hip_atomic_store(p.hbuf + (size_t)g * HB_FLOATS + threadIdx.x, lds[L_YS + threadIdx.x], __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    stc(p.hbuf + (size_t)g * HB_FLOATS + threadIdx.x, lds[L_YS + threadIdx.x]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(p.hflag + g, htag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_store((g_u64*)(p.hflag + g), htag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void head_receive(const Params& p, float* lds, int g, unsigned long long htag) {
   if (threadIdx.x == 0) {
     const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load(p.hflag + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != htag) {
+    while (__hip_atomic_load((g_u64*)(p.hflag + g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != htag) {
       if (__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
       __builtin_amdgcn_s_sleep(1);
       if (wall_clock64() - t0 > BARRIER_TIMEOUT_TICKS) {
@@ -690,7 +897,7 @@ __device__ __forceinline__ void head_receive(const Params& p, float* lds, int g,
   __syncthreads();
   if (threadIdx.x < HB_FLOATS)
     lds[L_YS + threadIdx.x] =
-        __hip_atomic_load(p.hbuf + (size_t)g * HB_FLOATS + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ldc(p.hbuf + (size_t)g * HB_FLOATS + threadIdx.x);
   __syncthreads();
 }
 
@@ -700,7 +907,9 @@ __device__ __forceinline__ void head_receive(const Params& p, float* lds, int g,
 __device__ __noinline__ void head_iteration(const Params& p, float* lds, float* scr, int g, int it,
                                             unsigned long long htag) {
   const GraphInfo gi = p.ginfo[g];
-  const GraphVar gv = p.gvar[g];
+  gv_load(p, g, (GraphVar*)(lds + L_GV));
+  __syncthreads();
+  const GraphVar gv = *(const GraphVar*)(lds + L_GV);
   if (gv.status != ST_RUN) return;
   const int nt = (gv.n_live + TILE - 1) / TILE;
   float* sbuf = scr + S_HID;  // [2][64]
@@ -847,7 +1056,7 @@ __device__ __noinline__ void attention_q_tile(const Params& p, float* lds, float
       const int v = rows[lane];
       if (v >= 0) {
         const float qq = gs[0] * ql[lane] + gs[1] * ql[16 + lane];
-        p.q[gi.node_off + v] = qq;
+        stc(p.q + gi.node_off + v, qq);
         bm = qq;
         bi = v;
         bc = 1;
@@ -859,12 +1068,7 @@ __device__ __noinline__ void attention_q_tile(const Params& p, float* lds, float
       const int i2 = __shfl_xor(bi, o, 64), c2 = __shfl_xor(bc, o, 64);
       if (c2 != 0) argmax_combine(bm, bs, bi, bc, m2, s2, i2, c2);
     }
-    if (lane == 0) {
-      apart_out[0] = bm;
-      apart_out[1] = bs;
-      apart_out[2] = __int_as_float(bi);
-      apart_out[3] = __int_as_float(bc);
-    }
+    if (lane == 0) stc4(apart_out, 0, make_float4(bm, bs, __int_as_float(bi), __int_as_float(bc)));
   }
   __syncthreads();
 }
@@ -977,7 +1181,7 @@ __device__ __forceinline__ void engine_body(const Params& p, const float* __rest
     // ---------------- tile prefix over the launch's graphs
     for (int i = threadIdx.x; i < ng; i += NTHREADS) {
       const GraphVar* gv = p.gvar + p.glist[i];
-      pref[i + 1] = gv->status == ST_RUN ? (gv->n_live + TILE - 1) / TILE : 0;
+      pref[i + 1] = ldc(&gv->status) == ST_RUN ? (ldc(&gv->n_live) + TILE - 1) / TILE : 0;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -991,6 +1195,7 @@ __device__ __forceinline__ void engine_body(const Params& p, const float* __rest
     const int tb = (int)blockIdx.x - twg0;
     const bool tiles = !is_env && !is_head;
     const int t0 = tiles ? min(ttot, tb * per) : 0, t1 = tiles ? min(ttot, t0 + per) : 0;
+    bool nb_ok = false;
     // hand-off tag of this step's graph head (unique per launch and step)
     const unsigned long long htag = ded ? ((unsigned long long)p.launch_seq << 24) | (unsigned)(pstep + 1) : 0ull;
 
@@ -1005,7 +1210,9 @@ __device__ __forceinline__ void engine_body(const Params& p, const float* __rest
         const int j = t - pref[gl];  // tile within the graph
         if (it >= 2 && gl != cur && cur != 0x7fffffff) {
           // virtual-node chain of this graph (identical in every workgroup that needs it)
-          const GraphVar gv = p.gvar[g];
+          gv_load(p, g, (GraphVar*)(lds + L_GV));
+          __syncthreads();
+          const GraphVar gv = *(const GraphVar*)(lds + L_GV);
           const int nt = (gv.n_live + TILE - 1) / TILE;
           float* sbuf = scr + S_HID;  // [2][64]
           float* yw = lds + L_YW;
@@ -1015,9 +1222,9 @@ __device__ __forceinline__ void engine_body(const Params& p, const float* __rest
             vrow_update(lds + L_W, scr, sbuf, yw);  // Y1 from S0
             graph_sum(p, gi, nt, 1, sbuf, scr + S_YP);
             vrow_update(lds + L_W, scr, sbuf, yw);  // Y2 from S1
-            if (threadIdx.x < 128) p.ybuf[(size_t)g * 128 + threadIdx.x] = yw[threadIdx.x];
+            if (threadIdx.x < 128) stc(p.ybuf + (size_t)g * 128 + threadIdx.x, yw[threadIdx.x]);
           } else {
-            if (threadIdx.x < 128) yw[threadIdx.x] = p.ybuf[(size_t)g * 128 + threadIdx.x];
+            if (threadIdx.x < 128) yw[threadIdx.x] = ldc(p.ybuf + (size_t)g * 128 + threadIdx.x);
             graph_sum(p, gi, nt, 2, sbuf, scr + S_YP);
             vrow_update(lds + L_W, scr, sbuf, yw);  // Y3 from S2
             graph_head(p, lds, scr, gi, gv);
@@ -1026,12 +1233,23 @@ __device__ __forceinline__ void engine_body(const Params& p, const float* __rest
         }
         if (threadIdx.x < TILE) {
           const int r = j * TILE + threadIdx.x;
-          const GraphVar* gvp = p.gvar + g;
-          rows[threadIdx.x] = r < gvp->n_live ? p.live[gi.node_off + r] : -1;
+          const int nl = ldc(&p.gvar[g].n_live);
+          const int lv = ldc(p.live + gi.node_off + min(r, gi.n - 1));
+          rows[threadIdx.x] = r < nl ? lv : -1;
         }
         __syncthreads();
-        gather_tile(p, gi, it, rows, scr);
+        // alive neighbour lists: built at iteration 1, kept for 2 and 3 when this workgroup
+        // has a single tile (its LDS copy is intact)
+        unsigned long long tg0 = 0;
+        if (p.prof != nullptr && it == 2 && threadIdx.x == 0 && pstep < p.prof_cap) {
+          tg0 = wall_clock64();
+          atomicMax(p.prof + (size_t)pstep * PROF_SLOTS + 47, tg0);  // latest tile start (it 2)
+        }
+        if (it == 1 || t1 - t0 > 1 || !ded) nb_ok = (p.variant & 16) ? false : build_nb_lists(p, gi, rows, scr);
+        if (nb_ok) gather_tile2(p, gi, it, rows, scr);
+        else gather_tile(p, gi, it, rows, scr);
         __syncthreads();
+        if (tg0 != 0) atomicMax(p.prof + (size_t)pstep * PROF_SLOTS + 46, wall_clock64() - tg0);  // longest gather (it 2)
         MD_PROF_T(23 + 3 * (it - 1));
         update_tile(lds + L_W, scr);
         __syncthreads();
@@ -1052,19 +1270,20 @@ __device__ __forceinline__ void engine_body(const Params& p, const float* __rest
           }
           float* sp = p.spart + (size_t)(gi.tile_off + j) * 384;
           if (it == 1) {
-            sp[l * 64 + c] = s_old;        // S0 (first-layer input)
-            sp[128 + l * 64 + c] = s_new;  // S1
+            stc(sp + l * 64 + c, s_old);        // S0 (first-layer input)
+            stc(sp + 128 + l * 64 + c, s_new);  // S1
           } else if (it == 2) {
-            sp[256 + l * 64 + c] = s_new;  // S2
+            stc(sp + 256 + l * 64 + c, s_new);  // S2
           }
         }
         if (it < 3) {
+          // new embeddings to HBM as 16-byte sc1 stores: 16 lanes per row, 4 rows per wave
           const int w = wave_id(), l = w >> 2, lane = lane_id();
           float* hb = p.H[l][(it - 1) & 1] + (size_t)gi.node_off * EMB;
-          for (int r = 4 * (w & 3); r < 4 * (w & 3) + 4; ++r) {
-            const int v = rows[r];
-            if (v >= 0) hb[(size_t)v * EMB + lane] = scr[S_E + l * 64 * LDT + lane * LDT + r];
-          }
+          const int r = 4 * (w & 3) + (lane >> 4), q4 = lane & 15;
+          const int v = rows[r];
+          const float* e = scr + S_E + l * 64 * LDT + 4 * q4 * LDT + r;
+          if (v >= 0) stc4(hb, v * 256 + q4 * 16, make_float4(e[0], e[LDT], e[2 * LDT], e[3 * LDT]));
         }
         __syncthreads();
         MD_PROF_T(24 + 3 * (it - 1));
@@ -1075,6 +1294,8 @@ __device__ __forceinline__ void engine_body(const Params& p, const float* __rest
           attention_q_tile(p, lds, scr, gi, g, rows, p.apart + (size_t)(gi.tile_off + j) * 4, htag, ts);
         }
         MD_PROF_T(25 + 3 * (it - 1));
+        if (p.prof != nullptr && threadIdx.x == 0 && pstep < p.prof_cap)
+          atomicMax(p.prof + (size_t)pstep * PROF_SLOTS + 42 + it, wall_clock64());  // slowest tile's end
       }
       MD_PROF(3 + 2 * it);
       grid_sync(p, target);

@@ -175,3 +175,22 @@ def test_shared_mode_batch_matches_dedicated(eng):
     out = eng.rollout()
     for i, (s, r) in enumerate(out):
         assert (s.tolist(), r.tolist()) == single[i % 3], i
+
+
+def test_global_memory_environment_mode(monkeypatch):
+    """Graphs too large for one workgroup's LDS run the environment step on HBM scratch
+    (EnvView<true>); MD_VARIANT=64 forces that mode for small graphs: same results."""
+    monkeypatch.setenv("MD_VARIANT", "64")
+    e = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
+    try:
+        for name in ("er100", "gmm200_s7", "er300_dense"):
+            z = load_golden(name)
+            n = int(z["n_nodes"])
+            e.load_graphs([(n, z["edges0"], z["edges1"])])
+            assert int(e.reset()[0]) == int(z["max_rank"])
+            seq, ranks = e.rollout()[0]
+            k = first_ambiguous(z)
+            assert seq[:k].tolist() == z["seq"][:k].tolist()
+            assert audc(ranks, int(z["max_rank"]), n) == float(z["score"])
+    finally:
+        e.close()
