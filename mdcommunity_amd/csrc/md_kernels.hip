@@ -184,33 +184,36 @@ __device__ __forceinline__ void gv_store(const Params& p, int g, const GraphVar*
 // ------------------------------------------------------------------ grid barrier
 // Monotonic counter: every wave drains its stores (vmcnt), the workgroup syncs, one lane adds
 // to the counter (agent-scope atomic) and polls it with sc1 loads; all data crossing the
-// barrier is sc1 on both sides.  Bounded spin: on timeout the error word is set and every
-// later barrier falls through, so the grid drains.
-__device__ __forceinline__ void grid_sync(const Params& p, unsigned& target) {
+// barrier is sc1 on both sides.  An error sets bit 31 of the counter (BAR_ERR) besides the
+// error word: every barrier then falls through and reports it, so no workgroup needs a
+// separate load of the error word on the critical path.  Bounded spin: a timeout raises
+// ERR_TIMEOUT the same way, so the grid drains.
+constexpr unsigned BAR_ERR = 0x80000000u;
+__device__ __forceinline__ void raise_err(const Params& p, int code) {
+  __hip_atomic_store(p.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_or((g_u32*)p.bar, BAR_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// returns true (uniformly) when an error was raised anywhere in the grid
+__device__ __forceinline__ bool grid_sync(const Params& p, unsigned& target, int* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   target += gridDim.x;
   if (threadIdx.x == 0) {
-    // every inter-workgroup datum is sc1 (see ldc / stc): no release / acquire fences
     __hip_atomic_fetch_add((g_u32*)p.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (__hip_atomic_load((g_i32*)p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+    unsigned v;
+    while ((v = __hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < target) {
       __builtin_amdgcn_s_sleep(1);
       if (wall_clock64() - t0 > (p.h_req != nullptr ? HOST_TIMEOUT_TICKS : BARRIER_TIMEOUT_TICKS)) {
-        __hip_atomic_store(p.err, ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        raise_err(p, ERR_TIMEOUT);
+        v = BAR_ERR;
         break;
       }
     }
+    *flag = (v & BAR_ERR) != 0;
   }
   __syncthreads();
-}
-
-__device__ __forceinline__ int load_err(const Params& p) {
-  return __hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void set_err(const Params& p, int code) {
-  __hip_atomic_store(p.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *flag != 0;
 }
 
 // ------------------------------------------------------------------ block reductions
@@ -321,7 +324,7 @@ __device__ __noinline__ int host_handshake(const Params& p, const GraphInfo& gi,
                            __hip_atomic_load(p.h_act + gi.node_off + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (k < 0) set_err(p, ERR_HOST);
+    if (k < 0) raise_err(p, ERR_HOST);
     misc[3] = k;
   }
   __syncthreads();
@@ -416,7 +419,7 @@ __device__ __noinline__ bool phase_a(const Params& p, int g, bool have_q, float*
                          : env_step<true>(p, gi, gv, area, pend_n, pend_first, lds, false);
     if (threadIdx.x == 0) {
       gv.npend = 0;
-      if (err) set_err(p, err);
+      if (err) raise_err(p, err);
       const bool term = gv.alive[0] == 0 || gv.alive[1] == 0;
       if (term) gv.status = ST_TERMINAL;
       else if (p.run_mode == RUN_STEP) gv.status = ST_PAUSED;
@@ -886,10 +889,10 @@ __device__ __forceinline__ void head_receive(const Params& p, float* lds, int g,
   if (threadIdx.x == 0) {
     const unsigned long long t0 = wall_clock64();
     while (__hip_atomic_load((g_u64*)(p.hflag + g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != htag) {
-      if (__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+      if (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR) break;
       __builtin_amdgcn_s_sleep(1);
       if (wall_clock64() - t0 > BARRIER_TIMEOUT_TICKS) {
-        __hip_atomic_store(p.err, ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        raise_err(p, ERR_TIMEOUT);
         break;
       }
     }
@@ -1156,6 +1159,7 @@ __device__ __forceinline__ void engine_body(const Params& p, const float* __rest
   }
 
   unsigned target = 0;
+  int* bflag = (int*)(lds + L_MISC) + 61;  // barrier error broadcast
   int pstep = 0;
   bool have_q = false, staged = false;
   const int ng = p.nglist;
@@ -1175,9 +1179,9 @@ __device__ __forceinline__ void engine_body(const Params& p, const float* __rest
       if (wdirty) load_weights(lds + L_W, wimg);
     }
     MD_PROF(3);
-    grid_sync(p, target);
+    const bool errA = grid_sync(p, target, bflag);
     MD_PROF(4);
-    if (load_err(p)) break;
+    if (errA) break;
     // ---------------- tile prefix over the launch's graphs
     for (int i = threadIdx.x; i < ng; i += NTHREADS) {
       const GraphVar* gv = p.gvar + p.glist[i];
@@ -1195,7 +1199,7 @@ __device__ __forceinline__ void engine_body(const Params& p, const float* __rest
     const int tb = (int)blockIdx.x - twg0;
     const bool tiles = !is_env && !is_head;
     const int t0 = tiles ? min(ttot, tb * per) : 0, t1 = tiles ? min(ttot, t0 + per) : 0;
-    bool nb_ok = false;
+    bool nb_ok = false, failed = false;
     // hand-off tag of this step's graph head (unique per launch and step)
     const unsigned long long htag = ded ? ((unsigned long long)p.launch_seq << 24) | (unsigned)(pstep + 1) : 0ull;
 
@@ -1299,11 +1303,11 @@ __device__ __forceinline__ void engine_body(const Params& p, const float* __rest
           atomicMax(p.prof + (size_t)pstep * PROF_SLOTS + 42 + it, wall_clock64());  // slowest tile's end
       }
       MD_PROF(3 + 2 * it);
-      grid_sync(p, target);
+      failed = grid_sync(p, target, bflag);
       MD_PROF(4 + 2 * it);
-      if (load_err(p)) break;
+      if (failed) break;
     }
-    if (load_err(p)) break;
+    if (failed) break;
     have_q = true;
     pstep++;
   }
