@@ -239,7 +239,10 @@ def main():
         gpath = os.path.join(ROOT, "tests", "golden", f"rollout_gmm1000_s{args.seed}.npz")
         if args.n == 1000 and os.path.exists(gpath):
             z = np.load(gpath)
-            golden = dict(audc=float(z["score"]), seq=z["seq"].tolist())
+            amb = np.flatnonzero((z["step_stats"][:, 3] > 1) | (z["step_gap"] < 1e-6))
+            # the reference's own pick is a tie / near-tie from step k on (tests/test_gpu_parity.py)
+            k = int(amb[0]) if amb.size else len(z["seq"])
+            golden = dict(audc=float(z["score"]), seq=z["seq"].tolist(), k=k)
         traffic = None
         tfile = os.path.join(ROOT, "profiles", "traffic_r01.json")
         if os.path.exists(tfile):
@@ -268,7 +271,9 @@ def main():
             },
             "audc": audc,
             "audc_match": (audc == golden["audc"]) if golden and audc is not None else None,
-            "seq_match": (seq.tolist() == golden["seq"]) if golden and audc is not None else None,
+            "seq_match": (seq.tolist()[:golden["k"]] == golden["seq"][:golden["k"]]) if golden and audc is not None else None,
+            "seq_checked_steps": golden["k"] if golden else None,
+            "seq_full_match": (seq.tolist() == golden["seq"]) if golden and audc is not None else None,
             "kernel_ms_per_step": kernel_ms / max(1, args.steps),
             "s0_kernel_ms_per_step": s0_ms / max(1, args.steps),
             "launches_per_step": launches / max(1, args.steps),

@@ -1249,8 +1249,7 @@ __device__ __forceinline__ void engine_body(const Params& p, const float* __rest
           tg0 = wall_clock64();
           atomicMax(p.prof + (size_t)pstep * PROF_SLOTS + 47, tg0);  // latest tile start (it 2)
         }
-        // (dedicated mode only: with many tiles per workgroup the list build does not pay)
-        if (it == 1 || t1 - t0 > 1 || !ded) nb_ok = ded && !(p.variant & 16) && build_nb_lists(p, gi, rows, scr);
+        if (it == 1 || t1 - t0 > 1 || !ded) nb_ok = !(p.variant & 16) && build_nb_lists(p, gi, rows, scr);
         if (nb_ok) gather_tile2(p, gi, it, rows, scr);
         else gather_tile(p, gi, it, rows, scr);
         __syncthreads();
