@@ -213,6 +213,7 @@ const char* err_name(int e) {
     case 3: return "live node sets differ between layers (U/PrepareBatchGraph.py:73)";
     case 4: return "action out of range";
     case 5: return "host selection failed";
+    case 6: return "kernel argument layout differs from the compiled assumption";
     default: return "unknown device error";
   }
 }

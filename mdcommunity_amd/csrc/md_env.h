@@ -406,7 +406,7 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
 // ascending live-node list and the per-layer aggregates, the write-back of edge states and
 // the unit-cost first-layer table.  Returns 0 or an ERR_* code.
 template <bool GL>
-__device__ int env_step(const Params& p, const GraphInfo& gi, GraphVar& gv, float* area, int pend_n,
+__device__ int env_step(KParams& p, const GraphInfo& gi, GraphVar& gv, float* area, int pend_n,
                         int pend_first, const float* lds_base, bool staged) {
   const int n = gi.n, e0 = gi.e[0], e1 = gi.e[1], et = e0 + e1;
   EnvView<GL> E;

@@ -86,7 +86,22 @@ static_assert(2 * STG_ROWS * 64 <= S_HID - S_M, "neighbour staging fits [S_M, S_
 
 constexpr float NEG_INF = -__builtin_huge_valf();
 constexpr unsigned long long BARRIER_TIMEOUT_TICKS = 400000000ull;  // 4 s at 100 MHz
-enum : int { ERR_TIMEOUT = 1, ERR_COVERED = 2, ERR_LIVE_MISMATCH = 3, ERR_BADNODE = 4, ERR_HOST = 5 };
+enum : int { ERR_TIMEOUT = 1, ERR_COVERED = 2, ERR_LIVE_MISMATCH = 3, ERR_BADNODE = 4, ERR_HOST = 5, ERR_ABI = 6 };
+
+// Kernel arguments of md_rollout_kernel / md_env_kernel, (Params, const float*), read in every
+// device function through the implicit-argument pointer (SGPRs s[8:9] in callees) at a fixed
+// offset below it: s_load of uniform fields straight from the kernarg segment.  A Params
+// reference passed to a non-inlined function would travel as a per-lane (VGPR) pointer to a
+// private copy: flat loads from scratch and waterfall loops around every buffer resource.
+typedef const __attribute__((address_space(4))) Params KParams;
+constexpr int KARG_BYTES = (int)((sizeof(Params) + 7) & ~(size_t)7) + 8;  // Params, wimg
+__device__ __forceinline__ KParams& kp() {
+  return *(KParams*)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_implicitarg_ptr() - KARG_BYTES);
+}
+__device__ __forceinline__ bool kargs_layout_ok() {
+  return (const __attribute__((address_space(4))) char*)__builtin_amdgcn_implicitarg_ptr() -
+             (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() == KARG_BYTES;
+}
 constexpr unsigned long long HOST_TIMEOUT_TICKS = 6000000000ull;  // 60 s at 100 MHz
 
 // ------------------------------------------------------------------ small helpers
@@ -162,22 +177,29 @@ __device__ __forceinline__ void stc(uint8_t* a, uint8_t v) {
   __hip_atomic_store((g_u8*)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // 16-byte sc1 accesses through a buffer resource on a wave-uniform base.
+// The base must be wave-uniform (every caller passes an array base): it is moved to SGPRs so
+// the buffer resource is scalar (no waterfall loop when the base arrived in VGPRs).
+__device__ __forceinline__ void* uniform_ptr(const void* q) {
+  const unsigned long long a = (unsigned long long)q;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return (void*)(((unsigned long long)hi << 32) | lo);
+}
 __device__ __forceinline__ float4 ldc4(const float* base, int byte_off) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(base), 0, 0x7fffffff, 0x00020000);
   const v4f v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16 /* sc1 */);
   return make_float4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void stc4(float* base, int byte_off, float4 x) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(base), 0, 0x7fffffff, 0x00020000);
   const v4f v = {x.x, x.y, x.z, x.w};
   __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, 16 /* sc1 */);
 }
 constexpr int GV_WORDS = (int)(sizeof(GraphVar) / 4);
 // GraphVar of graph g into `dst` (LDS), GV_WORDS threads in parallel; the caller syncs.
-__device__ __forceinline__ void gv_load(const Params& p, int g, GraphVar* dst) {
+__device__ __forceinline__ void gv_load(KParams& p, int g, GraphVar* dst) {
   if (threadIdx.x < GV_WORDS) ((int*)dst)[threadIdx.x] = ldc((const int*)(p.gvar + g) + threadIdx.x);
 }
-__device__ __forceinline__ void gv_store(const Params& p, int g, const GraphVar* src) {
+__device__ __forceinline__ void gv_store(KParams& p, int g, const GraphVar* src) {
   if (threadIdx.x < GV_WORDS) stc((int*)(p.gvar + g) + threadIdx.x, ((const int*)src)[threadIdx.x]);
 }
 
@@ -189,12 +211,12 @@ __device__ __forceinline__ void gv_store(const Params& p, int g, const GraphVar*
 // separate load of the error word on the critical path.  Bounded spin: a timeout raises
 // ERR_TIMEOUT the same way, so the grid drains.
 constexpr unsigned BAR_ERR = 0x80000000u;
-__device__ __forceinline__ void raise_err(const Params& p, int code) {
+__device__ __forceinline__ void raise_err(KParams& p, int code) {
   __hip_atomic_store(p.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_fetch_or((g_u32*)p.bar, BAR_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // returns true (uniformly) when an error was raised anywhere in the grid
-__device__ __forceinline__ bool grid_sync(const Params& p, unsigned& target, int* flag) {
+__device__ __forceinline__ bool grid_sync(KParams& p, unsigned& target, int* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   target += gridDim.x;
@@ -297,7 +319,8 @@ __device__ __forceinline__ void argmax_combine(float& bm, float& bs, int& bi, in
 // the graph's Q row to mapped host memory, raise the request tag, wait for the host's answer
 // (its selection callback = the reference's np.argsort pick), copy the actions to p.pend.
 // Returns the number of actions (0 on error; the error word is set).
-__device__ __noinline__ int host_handshake(const Params& p, const GraphInfo& gi, int g, int npred, int* misc) {
+__device__ __noinline__ int host_handshake(KParams&, const GraphInfo gi, int g, int npred, int* misc) {
+  KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   const unsigned tag = (p.launch_seq << 16) ^ (unsigned)(npred + 1);
   for (int x = threadIdx.x; x < gi.n; x += NTHREADS) p.h_q[gi.node_off + x] = ldc(p.q + gi.node_off + x);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -332,7 +355,8 @@ __device__ __noinline__ int host_handshake(const Params& p, const GraphInfo& gi,
 }
 
 // Phase A of one graph: reduce the previous prediction, then apply / MCC / features.
-__device__ __noinline__ bool phase_a(const Params& p, int g, bool have_q, float* lds, bool staged) {
+__device__ __noinline__ bool phase_a(KParams&, int g, bool have_q, float* lds, bool staged) {
+  KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   GraphVar& gv = *(GraphVar*)(lds + L_GV);
   int* misc = (int*)(lds + L_MISC);
   const GraphInfo gi = p.ginfo[g];
@@ -436,7 +460,8 @@ __device__ __noinline__ bool phase_a(const Params& p, int g, bool have_q, float*
 // Gather for one tile: waves 0-3 layer 0, 4-7 layer 1; each wave handles rows 4*(w&3)..+3
 // concurrently, one 16-lane group per row, every lane owning 4 features (float4 loads).
 // it == 1: previous embedding = first-layer table (by degree, unit cost) or static input.
-__device__ __noinline__ void gather_tile(const Params& p, const GraphInfo& gi, int it, const int* rows, float* scr) {
+__device__ __noinline__ void gather_tile(KParams&, const GraphInfo gi, int it, const int* rows, float* scr) {
+  KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   const int w = wave_id(), l = w >> 2, lane = lane_id();
   const int grp = lane >> 4, qd = lane & 15;
   const int* rp = p.rowptr[l] + gi.roff[l];
@@ -517,7 +542,8 @@ __device__ __noinline__ void gather_tile(const Params& p, const GraphInfo& gi, i
 // step.  Header (ints at S_NBH): off[2][16], cnt[2][16] (alive, per row), rawb[2][16],
 // rawc[2][16] (CSR extent), tot[2].  Returns false when a layer has more than NB_CAP alive
 // entries (the tile then uses gather_tile).
-__device__ __noinline__ bool build_nb_lists(const Params& p, const GraphInfo& gi, const int* rows, float* scr) {
+__device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const int* rows, float* scr) {
+  KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   const int w = wave_id(), l = w >> 2, lane = lane_id(), t = threadIdx.x & 255;
   lds_i32* hdr = (lds_i32*)(int*)(scr + S_NBH);
   lds_i32* tmp = (lds_i32*)(int*)(scr + S_RED);  // [2][4] wave totals
@@ -597,7 +623,8 @@ __device__ __noinline__ bool build_nb_lists(const Params& p, const GraphInfo& gi
 // then each 16-lane group adds its row's neighbours in CSR order (the reference's sequential
 // scatter-add order).  Same results as gather_tile; high-degree rows no longer serialise
 // their loads.
-__device__ __noinline__ void gather_tile2(const Params& p, const GraphInfo& gi, int it, const int* rows, float* scr) {
+__device__ __noinline__ void gather_tile2(KParams&, const GraphInfo gi, int it, const int* rows, float* scr) {
+  KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   const int w = wave_id(), l = w >> 2, lane = lane_id(), t = threadIdx.x & 255;
   const int grp = lane >> 4, qd = lane & 15;
   const int* deg = p.deg[l] + gi.node_off;
@@ -727,7 +754,7 @@ __device__ __noinline__ void normalize_tile(float* at, float* scr) {
 // Sum of one graph's per-tile partial sums (slot) -> out[2][64]: four threads per output each
 // add a contiguous quarter of the tiles in order, then the quarters are added in order
 // (a fixed order, identical in every workgroup).
-__device__ void graph_sum(const Params& p, const GraphInfo& gi, int nt, int slot, float* out, float* tmp4) {
+__device__ void graph_sum(KParams& p, const GraphInfo& gi, int nt, int slot, float* out, float* tmp4) {
   const int o = threadIdx.x & 127, qt = threadIdx.x >> 7;
   const int per = (nt + 3) >> 2;
   const int j0 = min(nt, qt * per), j1 = min(nt, j0 + per);
@@ -804,8 +831,9 @@ __device__ __forceinline__ float other_gate(int l, float d00, float d11, float d
 
 // Graph rows: y_l from the final virtual-node embeddings E_l = Y3_l (in L_YW), the layer-mix
 // weights softmax(relu(y_l.WL1).WL2) and the aux features (U/PrepareBatchGraph.py:92-101).
-__device__ __noinline__ void graph_head(const Params& p, float* lds, float* scr, const GraphInfo& gi,
+__device__ __noinline__ void graph_head(KParams&, float* lds, float* scr, const GraphInfo gi,
                                         const GraphVar& gv) {
+  KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   const int w = wave_id(), l = w >> 2, q = w & 3, lane = lane_id();
   const float* wi = lds + L_W;
   float* gs = lds + L_GS;
@@ -878,14 +906,14 @@ __device__ __noinline__ void graph_head(const Params& p, float* lds, float* scr,
 // (MI355X_MICROARCH.md, inter-workgroup visibility, first table row), so no L2 write-back or
 // L1 invalidate is needed.
 constexpr int HB_FLOATS = 144;
-__device__ __forceinline__ void head_publish(const Params& p, const float* lds, int g, unsigned long long htag) {
+__device__ __forceinline__ void head_publish(KParams& p, const float* lds, int g, unsigned long long htag) {
   if (threadIdx.x < HB_FLOATS)
     stc(p.hbuf + (size_t)g * HB_FLOATS + threadIdx.x, lds[L_YS + threadIdx.x]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store((g_u64*)(p.hflag + g), htag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void head_receive(const Params& p, float* lds, int g, unsigned long long htag) {
+__device__ __forceinline__ void head_receive(KParams& p, float* lds, int g, unsigned long long htag) {
   if (threadIdx.x == 0) {
     const unsigned long long t0 = wall_clock64();
     while (__hip_atomic_load((g_u64*)(p.hflag + g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != htag) {
@@ -907,8 +935,9 @@ __device__ __forceinline__ void head_receive(const Params& p, float* lds, int g,
 // One iteration of the graph-head workgroup (dedicated mode) for graph g: it == 2 builds
 // Y1, Y2 from the S0 / S1 tile partials of iteration 1; it == 3 builds Y3 from S2, runs the
 // graph head and publishes it.  Same arithmetic as the shared-mode path in the tile loop.
-__device__ __noinline__ void head_iteration(const Params& p, float* lds, float* scr, int g, int it,
+__device__ __noinline__ void head_iteration(KParams&, float* lds, float* scr, int g, int it,
                                             unsigned long long htag) {
+  KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   const GraphInfo gi = p.ginfo[g];
   gv_load(p, g, (GraphVar*)(lds + L_GV));
   __syncthreads();
@@ -937,9 +966,10 @@ __device__ __noinline__ void head_iteration(const Params& p, float* lds, float* 
   do {                                                   \
     if (ts != nullptr && threadIdx.x == 0) ts[k] = wall_clock64(); \
   } while (0)
-__device__ __noinline__ void attention_q_tile(const Params& p, float* lds, float* scr, const GraphInfo& gi, int g,
+__device__ __noinline__ void attention_q_tile(KParams&, float* lds, float* scr, const GraphInfo gi, int g,
                                               const int* rows, float* apart_out, unsigned long long htag,
                                               unsigned long long* ts) {
+  KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   const float* wi = lds + L_W;
   const int w = wave_id(), l = w >> 2, cb = w & 3, lane = lane_id();
   const int ar = lane & 15, ak = lane >> 4;
@@ -1128,7 +1158,7 @@ __device__ __forceinline__ int tile_graph(const int* pref, int ng, int t) {
 // One body, two entry points so profiles separate the work: md_rollout_kernel runs whole
 // rollouts (RUN_ROLLOUT); md_env_kernel runs single environment steps and predictions
 // (RUN_STEP: MvcEnv.s0 / queued actions, RUN_PREDICT).
-__device__ __forceinline__ void engine_body(const Params& p, const float* __restrict__ wimg) {
+__device__ __forceinline__ void engine_body(KParams& p, const float* __restrict__ wimg) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* scr = lds + L_SCR;
   int* pref = (int*)(lds + L_PREF);
@@ -1313,11 +1343,19 @@ __device__ __forceinline__ void engine_body(const Params& p, const float* __rest
 }
 
 __global__ void __launch_bounds__(NTHREADS, 1) md_rollout_kernel(Params p, const float* __restrict__ wimg) {
-  engine_body(p, wimg);
+  if (!kargs_layout_ok()) {
+    if (threadIdx.x == 0) __hip_atomic_store(p.err, ERR_ABI, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  engine_body(kp(), wimg);
 }
 
 __global__ void __launch_bounds__(NTHREADS, 1) md_env_kernel(Params p, const float* __restrict__ wimg) {
-  engine_body(p, wimg);
+  if (!kargs_layout_ok()) {
+    if (threadIdx.x == 0) __hip_atomic_store(p.err, ERR_ABI, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  engine_body(kp(), wimg);
 }
 
 // Reset every graph in glist to the initial (pre-s0) state.
