@@ -112,6 +112,29 @@ __device__ __forceinline__ f4 mfma16(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Sequential chain acc = fmaf(a(k), b(k), acc), k = k0 .. k0 + K - 1 in order (the reference's
+// MKL k-ascending chain), the operands of each block of B terms loaded together ahead of its
+// arithmetic: LDS latency is paid once per block, not once per term.  Small register
+// footprint on purpose: a callee's VGPR count is what its callers must keep clear.
+template <int K, int B = 16, class FA, class FB>
+__device__ __forceinline__ float fma_chain(float acc, int k0, FA&& fa, FB&& fb) {
+  static_assert(K % B == 0, "block size");
+#pragma unroll
+  for (int blk = 0; blk < K / B; ++blk) {
+    float x[B], y[B];
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      x[i] = fa(k0 + blk * B + i);
+      y[i] = fb(k0 + blk * B + i);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < B; ++i) acc = fmaf(x[i], y[i], acc);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return acc;
+}
+
 // Weight element W[k][c] of a [K][64] matrix stored in B-fragment order at `base`.
 __device__ __forceinline__ float wget(const float* base, int ksteps, int k, int c) {
   return base[((c >> 4) * ksteps + (k >> 2)) * 64 + ((k & 3) << 4) + (c & 15)];
@@ -702,11 +725,24 @@ __device__ __noinline__ void update_tile(const float* wi, float* scr) {
   const float* p1 = wi + W_IP1 + cb * 16 * 64;
   const float* p2 = wi + W_IP2 + cb * 16 * 64;
   const float* p3 = wi + W_IP3 + cb * 32 * 64;
-  f4 a1 = {0.f, 0.f, 0.f, 0.f}, a2 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
+  // operands of both chains loaded up front (every LDS read in flight before the first
+  // MFMA), the P3 fragments before the workgroup barrier
+  float xa[16], xb[16], wa[16], wb[16], wc[32];
+#pragma unroll
   for (int s = 0; s < 16; ++s) {
-    a1 = mfma16(atp[(4 * s + ak) * LDT + ar], p1[s * 64 + lane], a1);
-    a2 = mfma16(atx[(4 * s + ak) * LDT + ar], p2[s * 64 + lane], a2);
+    xa[s] = atp[(4 * s + ak) * LDT + ar];
+    wa[s] = p1[s * 64 + lane];
+    xb[s] = atx[(4 * s + ak) * LDT + ar];
+    wb[s] = p2[s * 64 + lane];
+  }
+#pragma unroll
+  for (int s = 0; s < 32; ++s) wc[s] = p3[s * 64 + lane];
+  __builtin_amdgcn_sched_barrier(0);  // keep every read ahead of the MFMA chains
+  f4 a1 = {0.f, 0.f, 0.f, 0.f}, a2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    a1 = mfma16(xa[s], wa[s], a1);
+    a2 = mfma16(xb[s], wb[s], a2);
   }
   const int col = 16 * cb + ar;
 #pragma unroll
@@ -715,9 +751,13 @@ __device__ __noinline__ void update_tile(const float* wi, float* scr) {
     atm[(64 + col) * LDT + 4 * ak + r] = a2[r];
   }
   __syncthreads();
+  float xm[32];
+#pragma unroll
+  for (int s = 0; s < 32; ++s) xm[s] = atm[(4 * s + ak) * LDT + ar];
+  __builtin_amdgcn_sched_barrier(0);
   f4 a3 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-  for (int s = 0; s < 32; ++s) a3 = mfma16(atm[(4 * s + ak) * LDT + ar], p3[s * 64 + lane], a3);
+#pragma unroll
+  for (int s = 0; s < 32; ++s) a3 = mfma16(xm[s], wc[s], a3);
   float* ate = scr + S_E + l * 64 * LDT;
 #pragma unroll
   for (int r = 0; r < 4; ++r) ate[col * LDT + 4 * ak + r] = fmaxf(a3[r], 0.f);
@@ -782,11 +822,10 @@ __device__ __noinline__ void vrow_update(const float* wi, float* scr, const floa
   float* ym = scr + S_YM + l * 128;
   {
     const int k0 = q * 16;
-    float a1 = 0.f, a2 = 0.f;
-    for (int k = k0; k < k0 + 16; ++k) {
-      a1 = fmaf(s[l * 64 + k], wget(wi + W_IP1, 16, k, lane), a1);
-      a2 = fmaf(y[l * 64 + k], wget(wi + W_IP2, 16, k, lane), a2);
-    }
+    const float a1 = fma_chain<16>(0.f, k0, [&](int k) { return s[l * 64 + k]; },
+                                   [&](int k) { return wget(wi + W_IP1, 16, k, lane); });
+    const float a2 = fma_chain<16>(0.f, k0, [&](int k) { return y[l * 64 + k]; },
+                                   [&](int k) { return wget(wi + W_IP2, 16, k, lane); });
     yp[q * 128 + lane] = a1;
     yp[q * 128 + 64 + lane] = a2;
   }
@@ -798,8 +837,8 @@ __device__ __noinline__ void vrow_update(const float* wi, float* scr, const floa
   __syncthreads();
   {
     const int k0 = q * 32;
-    float a = 0.f;
-    for (int k = k0; k < k0 + 32; ++k) a = fmaf(ym[k], wget(wi + W_IP3, 32, k, lane), a);
+    const float a = fma_chain<32>(0.f, k0, [&](int k) { return ym[k]; },
+                                  [&](int k) { return wget(wi + W_IP3, 32, k, lane); });
     yp[q * 128 + lane] = a;
   }
   __syncthreads();
@@ -829,10 +868,21 @@ __device__ __forceinline__ float other_gate(int l, float d00, float d11, float d
   return l == 0 ? e1 * inv : e0 * inv;
 }
 
+// w_layer1 [64][128] into LDS (the graph-head workgroup keeps it for the whole launch).
+__device__ __forceinline__ void stage_wl1(KParams& p, float* wl1) {
+  constexpr int N4 = 64 * 128 / 4, K = N4 / NTHREADS;
+  const float4* src = (const float4*)(p.w + W_WL1);
+  float4 t[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) t[k] = src[k * NTHREADS + threadIdx.x];
+#pragma unroll
+  for (int k = 0; k < K; ++k) ((float4*)wl1)[k * NTHREADS + threadIdx.x] = t[k];
+}
+
 // Graph rows: y_l from the final virtual-node embeddings E_l = Y3_l (in L_YW), the layer-mix
 // weights softmax(relu(y_l.WL1).WL2) and the aux features (U/PrepareBatchGraph.py:92-101).
 __device__ __noinline__ void graph_head(KParams&, float* lds, float* scr, const GraphInfo gi,
-                                        const GraphVar& gv) {
+                                        const GraphVar& gv, bool wl1_resident) {
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   const int w = wave_id(), l = w >> 2, q = w & 3, lane = lane_id();
   const float* wi = lds + L_W;
@@ -842,22 +892,20 @@ __device__ __noinline__ void graph_head(KParams&, float* lds, float* scr, const 
   float* wl1 = scr;                 // [64][128] staged w_layer1
   float* f = scr + 64 * 128;        // [2][64] tanh features
   float* dots = f + 128;            // [4]
-  float* zh = dots + 4;             // [2][128]
-  for (int i = threadIdx.x; i < 64 * 128 / 4; i += NTHREADS)
-    ((float4*)wl1)[i] = ((const float4*)(p.w + W_WL1))[i];
+  float* zh = dots + 4;             // [2][128] hidden, then the 2 layer logits
+  if (!wl1_resident) stage_wl1(p, wl1);
   if (q == 0) {
     // F = tanh(E.T + b): the graph row is part of the reference's [n+1, 64] sgemm -> FMA chain
-    float a = 0.f;
-    for (int k = 0; k < 64; ++k) a = fmaf(y[l * 64 + k], wget(wi + W_IT, 16, k, lane), a);
+    const float a = fma_chain<64>(0.f, 0, [&](int k) { return y[l * 64 + k]; },
+                                  [&](int k) { return wget(wi + W_IT, 16, k, lane); });
     f[l * 64 + lane] = tanhf(a + wi[W_ITB + lane]);
   }
   __syncthreads();
   if (w == 0 && lane < 3) {
     const float* fa = f + (lane == 1 ? 64 : 0);
     const float* fb = f + (lane == 0 ? 0 : 64);
-    float a = 0.f;
-    for (int c = 0; c < 64; ++c) a = fmaf(fa[c] * fb[c], wi[W_ILW + c], a);
-    dots[lane] = a;  // 0: F0F0, 1: F1F1, 2: F0F1
+    dots[lane] = fma_chain<64>(0.f, 0, [&](int c) { return fa[c] * fb[c]; },
+                               [&](int c) { return wi[W_ILW + c]; });  // 0: F0F0, 1: F1F1, 2: F0F1
   }
   __syncthreads();
   if (q == 0) {
@@ -869,18 +917,20 @@ __device__ __noinline__ void graph_head(KParams&, float* lds, float* scr, const 
   __syncthreads();
   if (threadIdx.x < 256) {
     const int ll = threadIdx.x >> 7, j = threadIdx.x & 127;
-    float a = 0.f;
-    for (int k = 0; k < 64; ++k) a = fmaf(ys[ll * 64 + k], wl1[k * 128 + j], a);
+    const float a = fma_chain<64>(0.f, 0, [&](int k) { return ys[ll * 64 + k]; },
+                                  [&](int k) { return wl1[k * 128 + j]; });
     zh[ll * 128 + j] = fmaxf(a, 0.f);
   }
   __syncthreads();
+  if (threadIdx.x < 2) {
+    // the two layer logits, one lane each
+    const int ll = threadIdx.x;
+    zh[256 + ll] = fma_chain<128>(0.f, 0, [&](int j) { return zh[ll * 128 + j]; },
+                                  [&](int j) { return wi[W_IWL2 + j]; });
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    float z[2];
-    for (int ll = 0; ll < 2; ++ll) {
-      float a = 0.f;
-      for (int j = 0; j < 128; ++j) a = fmaf(zh[ll * 128 + j], wi[W_IWL2 + j], a);
-      z[ll] = a;
-    }
+    const float z[2] = {zh[256], zh[257]};
     const float m = fmaxf(z[0], z[1]);
     const float e0 = expf(z[0] - m), e1 = expf(z[1] - m);
     const float inv = 1.f / (e0 + e1);
@@ -955,7 +1005,7 @@ __device__ __noinline__ void head_iteration(KParams&, float* lds, float* scr, in
   } else {
     graph_sum(p, gi, nt, 2, sbuf, scr + S_YP);
     vrow_update(lds + L_W, scr, sbuf, yw);  // Y3 from S2
-    graph_head(p, lds, scr, gi, gv);
+    graph_head(p, lds, scr, gi, gv, true);
     head_publish(p, lds, g, htag);
   }
 }
@@ -979,9 +1029,16 @@ __device__ __noinline__ void attention_q_tile(KParams&, float* lds, float* scr, 
   {
     // F_l = tanh(E_l . T + b)
     const float* tf = wi + W_IT + cb * 16 * 64;
+    float xa[16], wa[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      xa[s] = ate[(4 * s + ak) * LDT + ar];
+      wa[s] = tf[s * 64 + lane];
+    }
+    __builtin_amdgcn_sched_barrier(0);
     f4 a = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int s = 0; s < 16; ++s) a = mfma16(ate[(4 * s + ak) * LDT + ar], tf[s * 64 + lane], a);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) a = mfma16(xa[s], wa[s], a);
     const float b = wi[W_ITB + col];
 #pragma unroll
     for (int r = 0; r < 4; ++r) atf[col * LDT + 4 * ak + r] = tanhf(a[r] + b);
@@ -996,8 +1053,19 @@ __device__ __noinline__ void attention_q_tile(KParams&, float* lds, float* scr, 
       const float* fa = scr + S_F + (kind == 1 ? 64 * LDT : 0);
       const float* fb = scr + S_F + (kind == 0 ? 0 : 64 * LDT);
       float a = 0.f;
-#pragma unroll 16
-      for (int c = 0; c < 64; ++c) a = fmaf(fa[c * LDT + row] * fb[c * LDT + row], wi[W_ILW + c], a);
+#pragma unroll
+      for (int h = 0; h < 64; h += 32) {
+        float xa[32], xb[32], ww[32];
+#pragma unroll
+        for (int c = 0; c < 32; ++c) {
+          xa[c] = fa[(h + c) * LDT + row];
+          xb[c] = fb[(h + c) * LDT + row];
+          ww[c] = wi[W_ILW + h + c];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = 0; c < 32; ++c) a = fmaf(xa[c] * xb[c], ww[c], a);
+      }
       dot[row * 3 + kind] = a;
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are done
@@ -1008,6 +1076,7 @@ __device__ __noinline__ void attention_q_tile(KParams&, float* lds, float* scr, 
     }
   }
   __syncthreads();
+  TSTAMP(33);
   {
     const float* oth = scr + S_F + (1 - l) * 64 * LDT;
 #pragma unroll
@@ -1017,6 +1086,7 @@ __device__ __noinline__ void attention_q_tile(KParams&, float* lds, float* scr, 
     }
   }
   __syncthreads();
+  TSTAMP(35);
   normalize_tile(scr + S_E, scr);
   __syncthreads();
   TSTAMP(39);
@@ -1060,9 +1130,16 @@ __device__ __noinline__ void attention_q_tile(KParams&, float* lds, float* scr, 
   float* hid = scr + S_HID;
   if (cb < 2) {
     const float* hf = wi + W_IH1 + cb * 16 * 64;
+    float xa[16], wa[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      xa[s] = atf[(4 * s + ak) * LDT + ar];
+      wa[s] = hf[s * 64 + lane];
+    }
+    __builtin_amdgcn_sched_barrier(0);
     f4 a = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int s = 0; s < 16; ++s) a = mfma16(atf[(4 * s + ak) * LDT + ar], hf[s * 64 + lane], a);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) a = mfma16(xa[s], wa[s], a);
 #pragma unroll
     for (int r = 0; r < 4; ++r) hid[(l * 16 + 4 * ak + r) * 33 + col] = fmaxf(a[r], 0.f);
   }
@@ -1071,8 +1148,8 @@ __device__ __noinline__ void attention_q_tile(KParams&, float* lds, float* scr, 
   if (threadIdx.x < 32) {
     const int ll = threadIdx.x >> 4, row = threadIdx.x & 15;
     const float* gs = lds + L_GS;
-    float a = 0.f;
-    for (int k = 0; k < 32; ++k) a = fmaf(hid[(ll * 16 + row) * 33 + k], wi[W_IW2 + k], a);
+    float a = fma_chain<32>(0.f, 0, [&](int k) { return hid[(ll * 16 + row) * 33 + k]; },
+                            [&](int k) { return wi[W_IW2 + k]; });
     for (int k = 0; k < 4; ++k) a = fmaf(gs[4 + ll * 4 + k], wi[W_IW2 + 32 + k], a);
     ql[ll * 16 + row] = a;
   }
@@ -1177,6 +1254,7 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
   const int ntw = gridDim.x - twg0;
   if (!is_env) {
     load_weights(lds + L_W, wimg);
+    if (is_head) stage_wl1(p, scr);  // graph_head's w_layer1, resident for the launch
     __syncthreads();
     if (wave_id() == 0) {
       // constant virtual-node input: normalize(relu([1,1] . w_n2l))  (net :247,272-283)
@@ -1261,11 +1339,12 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
             if (threadIdx.x < 128) yw[threadIdx.x] = ldc(p.ybuf + (size_t)g * 128 + threadIdx.x);
             graph_sum(p, gi, nt, 2, sbuf, scr + S_YP);
             vrow_update(lds + L_W, scr, sbuf, yw);  // Y3 from S2
-            graph_head(p, lds, scr, gi, gv);
+            graph_head(p, lds, scr, gi, gv, false);
           }
           cur = gl;
         }
-        if (threadIdx.x < TILE) {
+        // rows of the tile (unchanged during a step: a single-tile workgroup keeps them)
+        if ((it == 1 || t1 - t0 > 1) && threadIdx.x < TILE) {
           const int r = j * TILE + threadIdx.x;
           const int nl = ldc(&p.gvar[g].n_live);
           const int lv = ldc(p.live + gi.node_off + min(r, gi.n - 1));
