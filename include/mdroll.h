@@ -143,7 +143,7 @@ md_status md_last_timing(md_ctx* ctx, double* kernel_ms, int32_t* launches);
  * following calls (0 disables).
  * md_profile_read copies the timestamps accumulated since md_profile was called and returns
  * the number of steps recorded in *n_steps. */
-#define MD_PROF_SLOTS 48
+#define MD_PROF_SLOTS 64
 md_status md_profile(md_ctx* ctx, int steps);
 md_status md_profile_read(md_ctx* ctx, uint64_t* out, int capacity_steps, int32_t* n_steps);
 

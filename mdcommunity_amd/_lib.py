@@ -19,7 +19,7 @@ MD_WEIGHT_FLOATS = 31205
 STATUS_NAMES = {1: "MD_EINVAL", 2: "MD_EHIP", 3: "MD_EOOM", 4: "MD_ESTATE", 5: "MD_ETIMEOUT", 6: "MD_ECALLBACK"}
 
 # Every symbol include/mdroll.h declares (checked by tests/test_abi.py).
-PROF_SLOTS = 48  # MD_PROF_SLOTS in include/mdroll.h
+PROF_SLOTS = 64  # MD_PROF_SLOTS in include/mdroll.h
 
 EXPORTS = ("md_create", "md_destroy", "md_last_error", "md_set_weights", "md_load_graphs", "md_reset",
            "md_predict", "md_step", "md_rollout", "md_rollout_trace", "md_get_state", "md_set_state",

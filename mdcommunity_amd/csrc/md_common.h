@@ -15,7 +15,7 @@ constexpr int BP_ITERS = 3;      // max_bp_iter, :62
 constexpr int NTHREADS = 512;    // 8 waves: waves 0-3 work on layer 0, waves 4-7 on layer 1
 constexpr int TILE = 16;         // node rows per MFMA tile (v_mfma_f32_16x16x4_f32)
 constexpr int G_CAP = 512;       // graphs per kernel launch (the host chunks larger batches)
-constexpr int PROF_SLOTS = 48;   // MD_PROF_SLOTS (include/mdroll.h)
+constexpr int PROF_SLOTS = 64;   // MD_PROF_SLOTS (include/mdroll.h)
 
 // Offsets (floats) of each tensor in the packed weight blob (see include/mdroll.h).
 enum WOff : int {

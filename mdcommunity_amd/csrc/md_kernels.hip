@@ -69,8 +69,8 @@ constexpr int S_YM = S_YP + 1024;           // [2][128]
 // The neighbour lists alias the virtual-node scratch S_YP/S_YM: the graph-head workgroup
 // never gathers, and shared-mode tile workgroups rebuild the lists after each chain.
 constexpr int S_NBH = S_YP;                 // neighbour-list header (ints, see build_nb_lists)
-constexpr int S_NBL = S_NBH + 136;          // [2][NB_CAP] u16 alive neighbour ids, CSR order
-constexpr int NB_CAP = 2088;                // alive neighbour entries per layer kept for a tile
+constexpr int S_NBL = S_NBH + 172;          // [2][NB_CAP] u16 alive neighbour ids, CSR order
+constexpr int NB_CAP = 2052;                // alive neighbour entries per layer kept for a tile
 constexpr int S_END = S_NBL + NB_CAP;
 constexpr int STG_ROWS = 68;                // neighbour rows per layer staged per batch ([S_M, S_HID))
 constexpr int L_TOTAL = L_SCR + S_END;      // floats of dynamic LDS per workgroup
@@ -378,7 +378,7 @@ __device__ __noinline__ int host_handshake(KParams&, const GraphInfo gi, int g, 
 }
 
 // Phase A of one graph: reduce the previous prediction, then apply / MCC / features.
-__device__ __noinline__ bool phase_a(KParams&, int g, bool have_q, float* lds, bool staged) {
+__device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds, bool staged) {
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   GraphVar& gv = *(GraphVar*)(lds + L_GV);
   int* misc = (int*)(lds + L_MISC);
@@ -586,18 +586,47 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
     hdr[32 + l * 16 + t] = 0;
   }
   __syncthreads();
-  int pre[17];
-  pre[0] = 0;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) pre[r + 1] = pre[r] + hdr[96 + l * 16 + r];
+  // CSR-extent prefix per row in LDS (a per-thread array indexed at run time would live in
+  // scratch memory)
+  lds_i32* pre = hdr + 136 + l * 17;
+  if (t < 17) {
+    int a = 0;
+    for (int k = 0; k < t; ++k) a += hdr[96 + l * 16 + k];
+    pre[t] = a;
+  }
+  __syncthreads();
   const int T = pre[16];
   const int chunk = (T + 255) >> 8;
   const int i0 = min(T, t * chunk), i1 = min(T, i0 + chunk);
-  // my entries: alive flags and neighbour ids, 8 loads in flight at a time
+  // my entries: alive flags and neighbour ids, the first four of them with all their loads in
+  // flight together and kept in registers for the second pass
   int keep = 0;
   int r = 0;
   while (r < 15 && pre[r + 1] <= i0) ++r;
-  for (int i = i0; i < i1; ++i) {
+  const int r0 = r;
+  int posv[4], nbv[4], fl[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int i = i0 + k;
+    posv[k] = -1;
+    if (i < i1) {
+      while (pre[r + 1] <= i) ++r;
+      posv[k] = hdr[64 + l * 16 + r] + (i - pre[r]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    fl[k] = 0;
+    nbv[k] = 0;
+    if (posv[k] >= 0) {
+      fl[k] = ldc(ca + posv[k]);
+      nbv[k] = adj[posv[k]];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) keep += fl[k] != 0;
+  const int rt = r;
+  for (int i = i0 + 4; i < i1; ++i) {
     while (pre[r + 1] <= i) ++r;
     const int pos = hdr[64 + l * 16 + r] + (i - pre[r]);
     keep += ldc(ca + pos) != 0;
@@ -619,9 +648,21 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
     tot += x;
   }
   int o = base + incl - keep;
-  r = 0;
-  while (r < 15 && pre[r + 1] <= i0) ++r;
-  for (int i = i0; i < i1; ++i) {
+  r = r0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int i = i0 + k;
+    if (i < i1) {
+      while (pre[r + 1] <= i) ++r;
+      if (fl[k]) {
+        if (o < NB_CAP) nbl[o] = (uint16_t)nbv[k];
+        ++o;
+        __hip_atomic_fetch_add(hdr + 32 + l * 16 + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+  }
+  r = rt;
+  for (int i = i0 + 4; i < i1; ++i) {
     while (pre[r + 1] <= i) ++r;
     const int pos = hdr[64 + l * 16 + r] + (i - pre[r]);
     if (ldc(ca + pos)) {
@@ -879,10 +920,20 @@ __device__ __forceinline__ void stage_wl1(KParams& p, float* wl1) {
   for (int k = 0; k < K; ++k) ((float4*)wl1)[k * NTHREADS + threadIdx.x] = t[k];
 }
 
+// Aux features of layer ll (U/PrepareBatchGraph.py:92-101): fp64 division, then fp32 as
+// torch.tensor(...).type(FloatTensor).  They depend on the environment state only.
+__device__ __forceinline__ void graph_aux(float* gs, const GraphInfo& gi, const GraphVar& gv, int ll) {
+  const double N = (double)gi.n;
+  gs[4 + ll * 4 + 0] = (float)((double)gv.n_cov / N);
+  gs[4 + ll * 4 + 1] = (float)((double)gv.counter[ll] / (double)gi.e[ll]);
+  gs[4 + ll * 4 + 2] = (float)((double)gv.twohop[ll] / (N * N));
+  gs[4 + ll * 4 + 3] = 1.0f;
+}
+
 // Graph rows: y_l from the final virtual-node embeddings E_l = Y3_l (in L_YW), the layer-mix
 // weights softmax(relu(y_l.WL1).WL2) and the aux features (U/PrepareBatchGraph.py:92-101).
 __device__ __noinline__ void graph_head(KParams&, float* lds, float* scr, const GraphInfo gi,
-                                        const GraphVar& gv, bool wl1_resident) {
+                                        const GraphVar& gv, bool wl1_resident, bool aux_ready) {
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   const int w = wave_id(), l = w >> 2, q = w & 3, lane = lane_id();
   const float* wi = lds + L_W;
@@ -936,15 +987,8 @@ __device__ __noinline__ void graph_head(KParams&, float* lds, float* scr, const 
     const float inv = 1.f / (e0 + e1);
     gs[0] = e0 * inv;
     gs[1] = e1 * inv;
-    // aux features: fp64 division, then fp32 as torch.tensor(...).type(FloatTensor)
-    const double N = (double)gi.n;
-    for (int ll = 0; ll < 2; ++ll) {
-      gs[4 + ll * 4 + 0] = (float)((double)gv.n_cov / N);
-      gs[4 + ll * 4 + 1] = (float)((double)gv.counter[ll] / (double)gi.e[ll]);
-      gs[4 + ll * 4 + 2] = (float)((double)gv.twohop[ll] / (N * N));
-      gs[4 + ll * 4 + 3] = 1.0f;
-    }
   }
+  if (!aux_ready && threadIdx.x < 2) graph_aux(gs, gi, gv, threadIdx.x);
   __syncthreads();
 }
 
@@ -988,11 +1032,30 @@ __device__ __forceinline__ void head_receive(KParams& p, float* lds, int g, unsi
 __device__ __noinline__ void head_iteration(KParams&, float* lds, float* scr, int g, int it,
                                             unsigned long long htag) {
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
-  const GraphInfo gi = p.ginfo[g];
-  gv_load(p, g, (GraphVar*)(lds + L_GV));
+  // diagnostics: iteration-3 timestamps of the first graph's head workgroup (slots 48-53)
+  unsigned long long* hts = nullptr;
+  if (p.prof != nullptr && it == 3 && (int)blockIdx.x == p.n_env && threadIdx.x == 0) {
+    const int ps = ((volatile int*)(lds + L_MISC))[60];
+    if (ps < p.prof_cap) hts = p.prof + (size_t)ps * PROF_SLOTS;
+  }
+#define HSTAMP(k)                              \
+  do {                                         \
+    if (hts != nullptr) hts[k] = wall_clock64(); \
+  } while (0)
+  HSTAMP(48);
+  // graph info and state (fixed until the next phase A) are read at iteration 2 and kept in
+  // LDS for iteration 3, whose head work is on the critical path
+  GraphInfo* gic = (GraphInfo*)((int*)(lds + L_MISC) + 16);
+  if (it == 2) {
+    if (threadIdx.x < (int)(sizeof(GraphInfo) / 4)) ((int*)gic)[threadIdx.x] = ((const int*)(p.ginfo + g))[threadIdx.x];
+    gv_load(p, g, (GraphVar*)(lds + L_GV));
+  }
   __syncthreads();
-  const GraphVar gv = *(const GraphVar*)(lds + L_GV);
+  // references into LDS (a private copy would go through scratch memory)
+  const GraphInfo& gi = *gic;
+  const GraphVar& gv = *(const GraphVar*)(lds + L_GV);
   if (gv.status != ST_RUN) return;
+  if (it == 2 && threadIdx.x < 2) graph_aux(lds + L_GS, gi, gv, threadIdx.x);
   const int nt = (gv.n_live + TILE - 1) / TILE;
   float* sbuf = scr + S_HID;  // [2][64]
   float* yw = lds + L_YW;
@@ -1003,10 +1066,15 @@ __device__ __noinline__ void head_iteration(KParams&, float* lds, float* scr, in
     graph_sum(p, gi, nt, 1, sbuf, scr + S_YP);
     vrow_update(lds + L_W, scr, sbuf, yw);  // Y2 from S1
   } else {
+    HSTAMP(49);
     graph_sum(p, gi, nt, 2, sbuf, scr + S_YP);
+    HSTAMP(50);
     vrow_update(lds + L_W, scr, sbuf, yw);  // Y3 from S2
-    graph_head(p, lds, scr, gi, gv, true);
+    HSTAMP(51);
+    graph_head(p, lds, scr, gi, gv, true, true);
+    HSTAMP(52);
     head_publish(p, lds, g, htag);
+    HSTAMP(53);
   }
 }
 
@@ -1324,7 +1392,7 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
           // virtual-node chain of this graph (identical in every workgroup that needs it)
           gv_load(p, g, (GraphVar*)(lds + L_GV));
           __syncthreads();
-          const GraphVar gv = *(const GraphVar*)(lds + L_GV);
+          const GraphVar& gv = *(const GraphVar*)(lds + L_GV);
           const int nt = (gv.n_live + TILE - 1) / TILE;
           float* sbuf = scr + S_HID;  // [2][64]
           float* yw = lds + L_YW;
@@ -1339,7 +1407,7 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
             if (threadIdx.x < 128) yw[threadIdx.x] = ldc(p.ybuf + (size_t)g * 128 + threadIdx.x);
             graph_sum(p, gi, nt, 2, sbuf, scr + S_YP);
             vrow_update(lds + L_W, scr, sbuf, yw);  // Y3 from S2
-            graph_head(p, lds, scr, gi, gv, false);
+            graph_head(p, lds, scr, gi, gv, false, false);
           }
           cur = gl;
         }
