@@ -214,7 +214,7 @@ const char* err_name(int e) {
     case 4: return "action out of range";
     case 5: return "host selection failed";
     case 6: return "kernel argument layout differs from the compiled assumption";
-    default: return "unknown device error";
+    default: return e >= 1000 ? "bounds check failed (debug build; site = code - 1000)" : "unknown device error";
   }
 }
 
@@ -343,7 +343,7 @@ md_status launch_chunk(md_ctx* c, const int* gl, int ngl, int run_mode, int host
   c->last_ms += ms;
   c->last_launches += 1;
   if (dev_err == 5 && sel != nullptr && !sel->err.empty()) return fail(c, MD_ECALLBACK, "%s", sel->err.c_str());
-  if (dev_err) return fail(c, dev_err == 1 ? MD_ETIMEOUT : MD_EINVAL, "device: %s", err_name(dev_err));
+  if (dev_err) return fail(c, dev_err == 1 ? MD_ETIMEOUT : MD_EINVAL, "device: %s (code %d)", err_name(dev_err), dev_err);
   if (c->prof_cap > 0) {
     std::vector<unsigned long long> tmp((size_t)c->prof_cap * PROF_SLOTS);
     HIPCHK(c, hipMemcpy(tmp.data(), c->prof.p, sizeof(unsigned long long) * tmp.size(), hipMemcpyDeviceToHost));

@@ -334,12 +334,16 @@ __device__ void compact_alive(const EnvView<GL>& E) {
 // Component labels (root ids) go to the degree arrays, free until after the fixed point: a
 // path-halving find may rewrite a parent slot with a non-root ancestor after its owner stored
 // the root, so the parent array itself is not a label map.
+// `cover` >= 0: first cover that node (U/mvc_env.py:74-85) inside the first union pass -- its
+// alive edges become covered instead of being united -- and return the covered edge counts
+// per layer in cc[2].
 template <bool GL>
-__device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long long* acc) {
+__device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long long* acc, int cover, int* cc) {
   const EnvView<GL> E = Ein;  // fields in registers
   const int n = E.gi->n;
   int pruned0 = 0, pruned1 = 0;
   if (acc != nullptr && threadIdx.x == 0) acc[PA_CALLS] += 1;
+  bool first = true, compacted = cover < 0;
   while (true) {
     unsigned long long tp = wall_clock64();
     if (acc != nullptr && threadIdx.x == 0) acc[PA_ROUNDS] += 1;
@@ -349,7 +353,19 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
     }
     __syncthreads();
     PACC(acc, PA_INIT, tp);
-    for_each_alive<GL>(E, [&](int e, int u, int v) { uf_unite(e < E.e0 ? E.par0 : E.par1, u, v); });
+    int k0 = 0, k1 = 0;
+    if (first && cover >= 0) {
+      for_each_alive<GL>(E, [&](int e, int u, int v) {
+        if (u == cover || v == cover) {
+          E.kill(e, E_COVERED);
+          if (e < E.e0) k0++; else k1++;
+        } else {
+          uf_unite(e < E.e0 ? E.par0 : E.par1, u, v);
+        }
+      });
+    } else {
+      for_each_alive<GL>(E, [&](int e, int u, int v) { uf_unite(e < E.e0 ? E.par0 : E.par1, u, v); });
+    }
     __syncthreads();
     PACC(acc, PA_UNITE, tp);
     if (acc != nullptr && (E.variant & 8)) {
@@ -367,10 +383,23 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
       uf_store(E.deg1, x, r1);
       diff |= (r0 != r1);
     }
-    diff = __syncthreads_or(diff);
+    if (first && cover >= 0) {
+      // covered-edge counts and the partition test in one block exchange
+      // (per layer at most n - 1 < 2^16 covered edges; at most 512 threads with diff set)
+      const int2 c = block_sum2(k0, k1 + (diff ? 1 << 16 : 0), E.tmp);
+      cc[0] = c.x;
+      cc[1] = c.y & 0xffff;
+      diff = (c.y >> 16) != 0;
+    } else {
+      diff = __syncthreads_or(diff);
+    }
+    first = false;
     PACC(acc, PA_LABEL, tp);
     tp = wall_clock64();
-    if (!diff) break;
+    if (!diff) {
+      if (!compacted) compact_alive<GL>(E);  // the covered edges move to the dead list
+      break;
+    }
     int c0 = 0, c1 = 0;
     for_each_alive<GL>(E, [&](int e, int u, int v) {
       auto other = e < E.e0 ? E.deg1 : E.deg0;  // layer-0 edges are pruned by layer-1 components
@@ -383,6 +412,7 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
     pruned0 += c.x;
     pruned1 += c.y;
     compact_alive<GL>(E);
+    compacted = true;
     PACC(acc, PA_PRUNE, tp);
   }
   const unsigned long long tc = wall_clock64();
@@ -491,43 +521,38 @@ __device__ int env_step(KParams& p, const GraphInfo& gi, GraphVar& gv, float* ar
                       : __hip_atomic_load(p.pend + gi.node_off + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (a < 0 || a >= n) { err = ERR_BADNODE; break; }
     if (E.covered(a)) { err = ERR_COVERED; break; }
-    // cover a in both layers (U/mvc_env.py:74-85): its alive edges become "covered"
+    // cover a in both layers (U/mvc_env.py:74-85) -- its alive edges become "covered", done
+    // inside the first union pass of the fixed point -- then the mutual-LMCC fixed point
     const unsigned long long tcv = wall_clock64();
-    int c0 = 0, c1 = 0;
-    for_each_alive<GL>(E, [&](int e, int u, int v) {
-      if (u == a || v == a) {
-        E.kill(e, E_COVERED);
-        if (e < e0) c0++; else c1++;
-      }
-    });
-    const int2 c = block_sum2(c0, c1, E.tmp);
-    compact_alive<GL>(E);
+    __syncthreads();  // every thread has read covered(a) before it is set
     if (threadIdx.x == 0) {
       stc(E.gcov + a, (uint8_t)1);
       if constexpr (!GL) E.cov8[a] = 1;
     }
     __syncthreads();
     PACC(acc, PA_COVER, tcv);
-    int pr[2];
-    const int lm = mcc_fixed_point<GL>(E, pr, acc);
+    int pr[2], c[2];
+    const int lm = mcc_fixed_point<GL>(E, pr, acc, a, c);
     if (threadIdx.x == 0) {
-      gv.counter[0] += c.x;
-      gv.counter[1] += c.y;
+      gv.counter[0] += c[0];
+      gv.counter[1] += c[1];
       gv.removed[0] += pr[0];
       gv.removed[1] += pr[1];
-      gv.alive[0] -= c.x + pr[0];
-      gv.alive[1] -= c.y + pr[1];
+      gv.alive[0] -= c[0] + pr[0];
+      gv.alive[1] -= c[1] + pr[1];
       gv.n_cov += 1;
       gv.lmcc = lm;
-      p.tr_action[gi.node_off + gv.steps] = a;
-      p.tr_rank[gi.node_off + gv.steps] = lm;
+      if (MD_BOK(gv.steps < gi.n, 8)) {
+        p.tr_action[gi.node_off + gv.steps] = a;
+        p.tr_rank[gi.node_off + gv.steps] = lm;
+      }
       gv.steps += 1;
     }
     __syncthreads();
   }
   if (!gv.s0_done && !err) {
     int pr[2];
-    const int lm = mcc_fixed_point<GL>(E, pr, acc);
+    const int lm = mcc_fixed_point<GL>(E, pr, acc, -1, nullptr);
     if (threadIdx.x == 0) {
       gv.removed[0] += pr[0];
       gv.removed[1] += pr[1];
@@ -633,7 +658,10 @@ __device__ int env_step(KParams& p, const GraphInfo& gi, GraphVar& gv, float* ar
     int k = base;
     int* lv = p.live + gi.node_off;
     for (int x = x0; x < x1; ++x)
-      if (uf_load(E.deg0, x) > 0) stc(lv + k++, x);
+      if (uf_load(E.deg0, x) > 0) {
+        if (MD_BOK(k < n, 9)) stc(lv + k, x);
+        ++k;
+      }
   }
   if (bad && !err) err = ERR_LIVE_MISMATCH;
   const int hd0 = gv.hdmax[0], hd1 = gv.hdmax[1];
@@ -654,6 +682,7 @@ __device__ int env_step(KParams& p, const GraphInfo& gi, GraphVar& gv, float* ar
     for (int i = threadIdx.x; i < nd; i += NTHREADS) {
       const int e = E.dl[i];
       const int l = e < e0 ? 0 : 1, kk = e < e0 ? e : e - e0;
+      if (!MD_BOK(e < et && i < et, 10)) continue;
       stc(E.gst[l] + kk, (uint8_t)E.st[e]);
       stc(E.calive[l] + E.epos[l][2 * kk], (uint8_t)0);
       stc(E.calive[l] + E.epos[l][2 * kk + 1], (uint8_t)0);

@@ -238,6 +238,17 @@ __device__ __forceinline__ void raise_err(KParams& p, int code) {
   __hip_atomic_store(p.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_fetch_or((g_u32*)p.bar, BAR_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Debug builds (-DMD_DEBUG_BOUNDS): index checks that raise error 1000 + site instead of
+// letting a bad index reach memory.
+#ifdef MD_DEBUG_BOUNDS
+__device__ __forceinline__ bool md_bok(bool ok, int site) {
+  if (!ok) raise_err(kp(), 1000 + site);
+  return ok;
+}
+#define MD_BOK(cond, site) md_bok((cond), (site))
+#else
+#define MD_BOK(cond, site) true
+#endif
 // returns true (uniformly) when an error was raised anywhere in the grid
 __device__ __forceinline__ bool grid_sync(KParams& p, unsigned& target, int* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -507,7 +518,7 @@ __device__ __noinline__ void gather_tile(KParams&, const GraphInfo gi, int it, c
     rb = rp[v];
     re = rp[v + 1];
     const int ov = table ? ldc(deg + v) : v;
-    own = ldc4(hp, ov * 256 + qd * 16);
+    if (MD_BOK(v < gi.n && ov >= 0 && ov < gi.n, 1)) own = ldc4(hp, ov * 256 + qd * 16);
   }
   int nch = (re - rb + 15) >> 4;
   nch = max(nch, __shfl_xor(nch, 16, 64));
@@ -619,8 +630,11 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
     fl[k] = 0;
     nbv[k] = 0;
     if (posv[k] >= 0) {
-      fl[k] = ldc(ca + posv[k]);
-      nbv[k] = adj[posv[k]];
+      if (MD_BOK(posv[k] < 2 * gi.e[l], 2)) {
+        fl[k] = ldc(ca + posv[k]);
+        nbv[k] = adj[posv[k]];
+      }
+      if (!MD_BOK(nbv[k] >= 0 && nbv[k] < gi.n, 3)) nbv[k] = 0;
     }
   }
 #pragma unroll
@@ -707,7 +721,7 @@ __device__ __noinline__ void gather_tile2(KParams&, const GraphInfo gi, int it, 
   float4 own = {0.f, 0.f, 0.f, 0.f}, acc = {0.f, 0.f, 0.f, 0.f};
   if (v >= 0) {
     const int ov = table ? ldc(deg + v) : v;
-    own = ldc4(hp, ov * 256 + qd * 16);
+    if (MD_BOK(v < gi.n && ov >= 0 && ov < gi.n, 1)) own = ldc4(hp, ov * 256 + qd * 16);
   }
   const int myoff = hdr[l * 16 + r], mycnt = hdr[32 + l * 16 + r];
   const int totl = hdr[128 + l];
@@ -722,7 +736,8 @@ __device__ __noinline__ void gather_tile2(KParams&, const GraphInfo gi, int it, 
       src[i] = -1;
       if (k < STG_ROWS * 16 && row < totl) {
         const int id = nbl[row];
-        src[i] = table ? ldc(deg + id) : id;
+        src[i] = MD_BOK(id < gi.n, 4) ? (table ? ldc(deg + id) : id) : -1;
+        if (!MD_BOK(src[i] < gi.n, 5)) src[i] = -1;
       }
     }
     float4 x[5];
@@ -1416,7 +1431,7 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
           const int r = j * TILE + threadIdx.x;
           const int nl = ldc(&p.gvar[g].n_live);
           const int lv = ldc(p.live + gi.node_off + min(r, gi.n - 1));
-          rows[threadIdx.x] = r < nl ? lv : -1;
+          rows[threadIdx.x] = r < nl && MD_BOK(lv >= 0 && lv < gi.n && nl <= gi.n, 6) ? lv : -1;
         }
         __syncthreads();
         // alive neighbour lists: built at iteration 1, kept for 2 and 3 when this workgroup
