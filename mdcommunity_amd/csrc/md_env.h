@@ -29,7 +29,7 @@ typedef __attribute__((address_space(3))) v4u lds_u4;
 
 // Profile accumulators (slots 16.. of a profiled step; workgroup 0, thread 0 writes).
 enum { PA_ROUNDS = 0, PA_UNITE = 1, PA_LABEL = 2, PA_PRUNE = 3, PA_COUNT = 4, PA_CALLS = 5, PA_COVER = 6,
-       PA_INIT = 16, PA_FINDONLY = 17, PA_EDGES = 18, PA_UNIONS = 19 };  // 16+: slots 32.. of the step
+       PA_INIT = 40, PA_FINDONLY = 41, PA_EDGES = 42, PA_UNIONS = 43 };  // 40+: slots 56.. of the step
 #define PACC(acc, slot, t0)                                                          \
   do {                                                                               \
     if ((acc) != nullptr && threadIdx.x == 0) (acc)[slot] += wall_clock64() - (t0);  \
@@ -372,8 +372,21 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
       // diagnostics: alive edges per round
       int ne = 0;
       for_each_alive<GL>(E, [&](int, int, int) { ne++; });
-      const int2 c = block_sum2(ne, 0, E.tmp);
-      if (threadIdx.x == 0) acc[PA_EDGES] += c.x;
+      // depth of every node in the union-find forest after the union pass
+      int dsum = 0;
+      for (int x = threadIdx.x; x < n; x += NTHREADS) {
+        for (int l = 0; l < 2; ++l) {
+          auto par = l ? E.par1 : E.par0;
+          int c = x, d = 0;
+          while (uf_load(par, c) != c) { c = uf_load(par, c); ++d; }
+          dsum += d;
+        }
+      }
+      const int2 c = block_sum2(ne, dsum, E.tmp);
+      if (threadIdx.x == 0) {
+        acc[PA_EDGES] += c.x;
+        acc[PA_FINDONLY] += c.y;
+      }
     }
     tp = wall_clock64();
     int diff = 0;

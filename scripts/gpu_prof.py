@@ -39,9 +39,15 @@ def prof(name, team):
         tt(23, 36), tt(36, 37), tt(37, 24), tt(29, 38), tt(38, 33), tt(33, 35), tt(35, 39), tt(39, 40), tt(40, 41), tt(41, 42), tt(42, 31)), flush=True)
     print("   slowest tile end (from barrier exit): it1 %.1f it2 %.1f it3 %.1f us" % (tt(11, 43), tt(12, 44), tt(13, 45)), flush=True)
     print("   it2: latest tile start %.1f us after WG0 exit, longest gather %.1f us" % (tt(12, 47), np.median(full[:, 46].astype(np.float64)) / 100), flush=True)
-    ex = full[:, 32:36].astype(np.float64)
-    print("   env extra: init %.1f us  findonly %.1f us  alive edges/step %.0f  (nonzero unions %.0f)" % (
-        np.median(ex[:, 0]) / 100, np.median(ex[:, 1]) / 100, np.median(ex[:, 2]), np.median(ex[:, 3])), flush=True)
+    ex = full[:, 56:60].astype(np.float64)
+    print("   env extra: init %.1f us  alive edges/step (MD_VARIANT=8) %.0f" % (np.median(ex[:, 0]) / 100, np.median(ex[:, 2])), flush=True)
+    if np.any(ex[:, 2] > 0):
+        acc_ = full[:, 16:23].astype(np.float64)
+        rate = acc_[:, 1] / 100 / np.maximum(ex[:, 2], 1) * 1000
+        q = np.percentile(np.arange(len(full)), [0, 25, 50, 75, 100]).astype(int)
+        print("   unite us per 1000 edge-rounds at steps %s: %s; edges/step %s; mean forest depth %s" % (
+            q.tolist(), np.round(rate[q], 2).tolist(), ex[q, 2].astype(int).tolist(),
+            np.round(ex[q, 1] / np.maximum(acc_[q, 0], 1) / 2000, 2).tolist()), flush=True)
     acc = full[:, 16:23].astype(np.float64)
     calls = np.maximum(acc[:, 5], 1)
     print("   env per step: rounds/call %.2f  cover %.1f  unite %.1f  label %.1f  prune %.1f  count %.1f us" % (
