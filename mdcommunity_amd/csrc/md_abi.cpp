@@ -100,7 +100,6 @@ struct md_ctx {
   DevBuf<uint8_t> estate[2], calive[2], covered;
   DevBuf<int> deg[2], live, gscr, pend, tr_action, tr_rank, tr_stat, glist, ctl;
   DevBuf<float> H[2][2], h0tab[2], q, spart, apart, ybuf, hbuf, tr_q, node_w;
-  DevBuf<unsigned long long> hflag;
   unsigned launch_seq = 0;
   // host selection hand-shake
   int host_mode = 1;
@@ -135,7 +134,7 @@ struct md_ctx {
     }
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
     tr_stat.release(); glist.release(); ctl.release(); q.release(); spart.release();
-    apart.release(); ybuf.release(); hbuf.release(); hflag.release(); tr_q.release(); node_w.release();
+    apart.release(); ybuf.release(); hbuf.release(); tr_q.release(); node_w.release();
     h_req.release(); h_ans.release(); h_nact.release(); h_act.release(); h_q.release();
     ng = 0;
     hinfo.clear();
@@ -191,7 +190,6 @@ Params make_params(md_ctx* c) {
   p.apart = c->apart.p;
   p.ybuf = c->ybuf.p;
   p.hbuf = c->hbuf.p;
-  p.hflag = c->hflag.p;
   p.pend = c->pend.p;
   p.tr_action = c->tr_action.p;
   p.tr_rank = c->tr_rank.p;
@@ -298,6 +296,9 @@ md_status launch_chunk(md_ctx* c, const int* gl, int ngl, int run_mode, int host
   const int grid = grid_size(c, v, n_env);
   HIPCHK(c, hipMemcpyAsync(c->glist.p, gl, sizeof(int) * ngl, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->ctl.p, 0, sizeof(int) * CTL_WORDS, c->stream));
+  // graph-head hand-off granules carry the step as their tag: stale tags from earlier launches
+  // must not match
+  if (n_env > 0) HIPCHK(c, hipMemsetAsync(c->hbuf.p, 0, sizeof(float) * c->hbuf.n, c->stream));
   Params p = make_params(c);
   p.nglist = ngl;
   p.n_env = n_env;
@@ -578,14 +579,12 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->spart.alloc(tt * 384));
   HIPCHK(c, c->apart.alloc(tt * 4));
   HIPCHK(c, c->ybuf.alloc((size_t)n_graphs * 128));
-  HIPCHK(c, c->hbuf.alloc((size_t)n_graphs * 144));
-  HIPCHK(c, c->hflag.alloc((size_t)n_graphs));
+  HIPCHK(c, c->hbuf.alloc((size_t)n_graphs * 144 * 2));
   HIPCHK(c, c->h_req.alloc((size_t)n_graphs));
   HIPCHK(c, c->h_ans.alloc((size_t)n_graphs));
   HIPCHK(c, c->h_nact.alloc((size_t)n_graphs));
   HIPCHK(c, c->h_act.alloc(c->tot_n));
   HIPCHK(c, c->h_q.alloc(c->tot_n));
-  HIPCHK(c, hipMemset(c->hflag.p, 0, sizeof(unsigned long long) * n_graphs));
   HIPCHK(c, hipMemcpyAsync(c->ginfo.p, info.data(), sizeof(GraphInfo) * n_graphs, hipMemcpyHostToDevice, c->stream));
   if (c->cost_mode == MD_COST_DEGREE) {
     HIPCHK(c, c->node_w.alloc(2 * tn));

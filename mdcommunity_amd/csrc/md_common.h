@@ -86,8 +86,7 @@ struct Params {
   float* spart;                    // per tile: [3 sums][2 layers][64] virtual-node partial sums
   float* apart;                    // per tile: arg-max partial {max, second, idx, count}
   float* ybuf;                     // per graph: [2][64] virtual-node embedding after iteration 2
-  float* hbuf;                     // per graph: [144] graph-head hand-off (y, mix, aux)
-  unsigned long long* hflag;       // per graph: step tag of the published graph head
+  float* hbuf;                     // per graph: [144][2] graph-head hand-off granules {value, step tag}
   int* pend;                       // per node slot: host-queued actions
   int* tr_action;                  // per node slot: removal order
   int* tr_rank;                    // per node slot: LMCC after each removal

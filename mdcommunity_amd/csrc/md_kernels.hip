@@ -490,6 +490,12 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
   return staged;
 }
 
+// Diagnostic timestamp into a profiled step's slots (ts == nullptr: off).
+#define TSTAMP(k)                                                  \
+  do {                                                             \
+    if (ts != nullptr && threadIdx.x == 0) ts[k] = wall_clock64(); \
+  } while (0)
+
 // ------------------------------------------------------------------ tile pieces
 // Gather for one tile: waves 0-3 layer 0, 4-7 layer 1; each wave handles rows 4*(w&3)..+3
 // concurrently, one 16-lane group per row, every lane owning 4 features (float4 loads).
@@ -576,7 +582,8 @@ __device__ __noinline__ void gather_tile(KParams&, const GraphInfo gi, int it, c
 // step.  Header (ints at S_NBH): off[2][16], cnt[2][16] (alive, per row), rawb[2][16],
 // rawc[2][16] (CSR extent), tot[2].  Returns false when a layer has more than NB_CAP alive
 // entries (the tile then uses gather_tile).
-__device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const int* rows, float* scr) {
+__device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const int* rows, float* scr,
+                                            unsigned long long* ts) {
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   const int w = wave_id(), l = w >> 2, lane = lane_id(), t = threadIdx.x & 255;
   lds_i32* hdr = (lds_i32*)(int*)(scr + S_NBH);
@@ -597,6 +604,7 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
     hdr[32 + l * 16 + t] = 0;
   }
   __syncthreads();
+  TSTAMP(60);
   // CSR-extent prefix per row in LDS (a per-thread array indexed at run time would live in
   // scratch memory)
   lds_i32* pre = hdr + 136 + l * 17;
@@ -606,6 +614,7 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
     pre[t] = a;
   }
   __syncthreads();
+  TSTAMP(61);
   const int T = pre[16];
   const int chunk = (T + 255) >> 8;
   const int i0 = min(T, t * chunk), i1 = min(T, i0 + chunk);
@@ -654,6 +663,7 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
   }
   if (lane == 63) tmp[w] = incl;
   __syncthreads();
+  TSTAMP(62);
   int base = 0, tot = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -686,6 +696,7 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
     }
   }
   __syncthreads();
+  TSTAMP(63);
   if (t < 16) {
     int off = 0;
     for (int k = 0; k < t; ++k) off += hdr[32 + l * 16 + k];
@@ -1009,35 +1020,34 @@ __device__ __noinline__ void graph_head(KParams&, float* lds, float* scr, const 
 
 // ------------------------------------------------------------------ graph-head hand-off
 // Dedicated mode: the graph-head workgroup publishes y (L_YS, 128 floats) and the graph
-// scalars (L_GS, 16) of graph g, then a 64-bit step tag; tile workgroups wait for the tag and
-// copy the 144 floats.  Payload and tag use agent-scope (sc1) stores and loads on both sides,
-// one signalling lane after every storing wave drained and a workgroup barrier
-// (MI355X_MICROARCH.md, inter-workgroup visibility, first table row), so no L2 write-back or
-// L1 invalidate is needed.
+// scalars (L_GS, 16) of graph g as 144 data-tagged 8-byte granules {value, tag} (one agent-
+// scope `sc1` store each, tag = step + 1; the host zeroes the buffer before each launch), and
+// each of 144 tile threads polls its own granule until the tag matches: one memory round trip
+// for the hand-off, no separate flag (MI355X_MICROARCH.md, handoff-1to1 row: 8-byte granules).
 constexpr int HB_FLOATS = 144;
 __device__ __forceinline__ void head_publish(KParams& p, const float* lds, int g, unsigned long long htag) {
-  if (threadIdx.x < HB_FLOATS)
-    stc(p.hbuf + (size_t)g * HB_FLOATS + threadIdx.x, lds[L_YS + threadIdx.x]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store((g_u64*)(p.hflag + g), htag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < HB_FLOATS) {
+    const unsigned long long gr = (htag << 32) | (unsigned)__float_as_uint(lds[L_YS + threadIdx.x]);
+    __hip_atomic_store((g_u64*)(p.hbuf + 2 * ((size_t)g * HB_FLOATS + threadIdx.x)), gr, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 __device__ __forceinline__ void head_receive(KParams& p, float* lds, int g, unsigned long long htag) {
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < HB_FLOATS) {
+    const g_u64* src = (const g_u64*)(p.hbuf + 2 * ((size_t)g * HB_FLOATS + threadIdx.x));
     const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load((g_u64*)(p.hflag + g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != htag) {
-      if (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR) break;
+    unsigned long long gr;
+    while (((gr = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != htag) {
       __builtin_amdgcn_s_sleep(1);
-      if (wall_clock64() - t0 > BARRIER_TIMEOUT_TICKS) {
+      if (wall_clock64() - t0 > BARRIER_TIMEOUT_TICKS ||
+          (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR)) {
         raise_err(p, ERR_TIMEOUT);
+        gr = 0;
         break;
       }
     }
+    lds[L_YS + threadIdx.x] = __uint_as_float((unsigned)gr);
   }
-  __syncthreads();
-  if (threadIdx.x < HB_FLOATS)
-    lds[L_YS + threadIdx.x] =
-        ldc(p.hbuf + (size_t)g * HB_FLOATS + threadIdx.x);
   __syncthreads();
 }
 
@@ -1095,10 +1105,6 @@ __device__ __noinline__ void head_iteration(KParams&, float* lds, float* scr, in
 
 // Attention + Q head for one tile whose final embeddings are in S_E (both layers).
 // Writes q for valid rows and this tile's arg-max partial.
-#define TSTAMP(k)                                        \
-  do {                                                   \
-    if (ts != nullptr && threadIdx.x == 0) ts[k] = wall_clock64(); \
-  } while (0)
 __device__ __noinline__ void attention_q_tile(KParams&, float* lds, float* scr, const GraphInfo gi, int g,
                                               const int* rows, float* apart_out, unsigned long long htag,
                                               unsigned long long* ts) {
@@ -1392,7 +1398,7 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
     const int t0 = tiles ? min(ttot, tb * per) : 0, t1 = tiles ? min(ttot, t0 + per) : 0;
     bool nb_ok = false, failed = false;
     // hand-off tag of this step's graph head (unique per launch and step)
-    const unsigned long long htag = ded ? ((unsigned long long)p.launch_seq << 24) | (unsigned)(pstep + 1) : 0ull;
+    const unsigned long long htag = ded ? (unsigned long long)(pstep + 1) : 0ull;
 
     for (int it = 1; it <= BP_ITERS; ++it) {
       MD_PROF(10 + it);
@@ -1441,7 +1447,14 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
           tg0 = wall_clock64();
           atomicMax(p.prof + (size_t)pstep * PROF_SLOTS + 47, tg0);  // latest tile start (it 2)
         }
-        if (it == 1 || t1 - t0 > 1 || !ded) nb_ok = !(p.variant & 16) && build_nb_lists(p, gi, rows, scr);
+        {
+          unsigned long long* ts = nullptr;
+          if (p.prof != nullptr && it == 1 && (int)blockIdx.x == twg0 && t == t0 && pstep < p.prof_cap)
+            ts = p.prof + (size_t)pstep * PROF_SLOTS;
+          TSTAMP(54);
+          if (it == 1 || t1 - t0 > 1 || !ded) nb_ok = !(p.variant & 16) && build_nb_lists(p, gi, rows, scr, ts);
+          TSTAMP(55);
+        }
         if (nb_ok) gather_tile2(p, gi, it, rows, scr);
         else gather_tile(p, gi, it, rows, scr);
         __syncthreads();

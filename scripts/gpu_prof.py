@@ -15,6 +15,13 @@ def prof(name, team):
     eng.load_graphs([(n, z["edges0"], z["edges1"])])
     eng.reset()
     eng.rollout()  # warm
+    kms = []
+    for _ in range(15):  # unprofiled device time per rollout
+        eng.reset()
+        eng.rollout()
+        kms.append(eng.last_timing()[0])
+    print(f"{name}: unprofiled rollout kernel ms: median {np.median(kms):.3f} min {np.min(kms):.3f} "
+          f"-> {np.median(kms) / len(z['seq']) * 1000:.1f} us per removal", flush=True)
     eng.reset()
     eng.profile(512)
     t0 = time.time(); out = eng.rollout(); dt = time.time() - t0
@@ -35,6 +42,8 @@ def prof(name, team):
         tt(11, 23), tt(23, 24), tt(24, 25), tt(12, 26), tt(26, 27), tt(27, 28), tt(13, 29), tt(29, 30), tt(30, 31)), flush=True)
     print("   head it3 (from barrier 2 exit): start %.1f gv %.1f graph_sum %.1f vrow %.1f graph_head %.1f publish %.1f -> done at %.1f us" % (
         tt(8, 48), tt(48, 49), tt(49, 50), tt(50, 51), tt(51, 52), tt(52, 53), tt(8, 53)), flush=True)
+    print("   it1 gather detail: rows %.1f | lists: rowptr %.1f prefix %.1f flags+scan %.1f pass2 %.1f offsets %.1f | gather %.1f us" % (
+        tt(11, 54), tt(54, 60), tt(60, 61), tt(61, 62), tt(62, 63), tt(63, 55), tt(55, 23)), flush=True)
     print("   tile it1: update %.1f normalize %.1f sums+stores %.1f | attn: tanh %.1f dots+gates %.1f mix %.1f norm %.1f head-wait %.1f e-chain %.1f hidden+Q %.1f argmax %.1f us" % (
         tt(23, 36), tt(36, 37), tt(37, 24), tt(29, 38), tt(38, 33), tt(33, 35), tt(35, 39), tt(39, 40), tt(40, 41), tt(41, 42), tt(42, 31)), flush=True)
     print("   slowest tile end (from barrier exit): it1 %.1f it2 %.1f it3 %.1f us" % (tt(11, 43), tt(12, 44), tt(13, 45)), flush=True)
