@@ -78,7 +78,8 @@ struct Params {
   uint8_t* estate[2];
   uint8_t* covered;
   int* deg[2];                     // residual degree per node
-  int* live;                       // compact ascending live-node list per graph
+  int* live;                       // compact ascending live-node list per graph: int4 {node,
+                                   //   CSR begin layer 0, layer 1, extents l0 | l1 << 16}
   float* H[2][2];                  // [layer][buffer] node embeddings, node-major x 64
   float* h0tab[2];                 // [layer] first-layer embedding: by degree (unit) / by node (degree cost)
   float* q;                        // per node (-inf = masked)

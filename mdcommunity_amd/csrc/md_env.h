@@ -125,7 +125,7 @@ struct EnvLayout {
   int cov;                       // byte offset of the covered flags
   int al0, al1, dl;              // byte offsets of the alive-edge lists (ping-pong) and the dead list
   int hdr;                       // word offset of {alive count, dead count, current list}
-  int par0, par1, deg0, deg1, tmp, total;
+  int par0, par1, deg0, deg1, tmp, rp, total;
 };
 __host__ __device__ inline EnvLayout env_layout(int n, int et) {
   EnvLayout L;
@@ -142,7 +142,8 @@ __host__ __device__ inline EnvLayout env_layout(int n, int et) {
   L.deg0 = L.par1 + n;
   L.deg1 = L.deg0 + n;
   L.tmp = ((L.deg1 + n + 3) / 4) * 4;
-  L.total = L.tmp + A_TMP_WORDS;
+  L.rp = L.tmp + A_TMP_WORDS;                 // static CSR row pointers of both layers, n + 1 each
+  L.total = L.rp + 2 * (n + 1);
   return L;
 }
 __host__ __device__ inline bool phase_a_fits_lds(int n, int et) {
@@ -172,6 +173,8 @@ struct EnvView {
   int* tmp;                     // always LDS (generic pointer for the block helpers)
   uint8_t* calive[2];
   const int* epos[2];
+  const int* grp[2];            // static CSR row pointers (global)
+  lds_i32* rp[2];               // LDS mode: their staged copy
 
   __device__ __forceinline__ int layer_of(int e) const { return e < e0 ? 0 : 1; }
   __device__ __forceinline__ int local(int e) const { return e < e0 ? e : e - e0; }
@@ -463,6 +466,7 @@ __device__ int env_step(KParams& p, const GraphInfo& gi, GraphVar& gv, float* ar
     E.gst[l] = p.estate[l] + gi.eoff[l];
     E.calive[l] = p.calive[l] + gi.coff[l];
     E.epos[l] = p.epos[l] + 2 * (size_t)gi.eoff[l];
+    E.grp[l] = p.rowptr[l] + gi.roff[l];
   }
   E.gcov = p.covered + gi.node_off;
   int* ia = (int*)area;
@@ -490,7 +494,13 @@ __device__ int env_step(KParams& p, const GraphInfo& gi, GraphVar& gv, float* ar
     E.al_other = (lds_u16*)(base8 + L.al1);
     E.dl = (lds_u16*)(base8 + L.dl);
     E.hdr = la + L.hdr;
+    E.rp[0] = la + L.rp;
+    E.rp[1] = la + L.rp + n + 1;
     if (!staged) {
+      for (int x = threadIdx.x; x <= n; x += NTHREADS) {
+        E.rp[0][x] = E.grp[0][x];
+        E.rp[1][x] = E.grp[1][x];
+      }
       // batched so every thread keeps 8 independent global loads in flight
       for (int e0b = 0; e0b < et; e0b += 8 * NTHREADS) {
         int uu[8], vv[8], ss[8];
@@ -668,14 +678,26 @@ __device__ int env_step(KParams& p, const GraphInfo& gi, GraphVar& gv, float* ar
     base = before + incl - nlive;
   }
   {
+    // live list entries {node, CSR begin layer 0, layer 1, CSR extents (u16 | u16 << 16)}: a tile
+    // reads its rows and their neighbour ranges with one 16-byte load each
     int k = base;
-    int* lv = p.live + gi.node_off;
-    for (int x = x0; x < x1; ++x)
+    float* lv = (float*)(p.live + 4 * (size_t)gi.node_off);
+    for (int x = x0; x < x1; ++x) {
       if (uf_load(E.deg0, x) > 0) {
-        if (MD_BOK(k < n, 9)) stc(lv + k, x);
+        int b0, e0_, b1, e1_;
+        if constexpr (GL) {
+          b0 = E.grp[0][x]; e0_ = E.grp[0][x + 1]; b1 = E.grp[1][x]; e1_ = E.grp[1][x + 1];
+        } else {
+          b0 = E.rp[0][x]; e0_ = E.rp[0][x + 1]; b1 = E.rp[1][x]; e1_ = E.rp[1][x + 1];
+        }
+        if (MD_BOK(k < n, 9))
+          stc4(lv, k * 16, make_float4(__int_as_float(x), __int_as_float(b0), __int_as_float(b1),
+                                       __int_as_float((e0_ - b0) | ((e1_ - b1) << 16))));
         ++k;
       }
+    }
   }
+
   if (bad && !err) err = ERR_LIVE_MISMATCH;
   const int hd0 = gv.hdmax[0], hd1 = gv.hdmax[1];
   __syncthreads();

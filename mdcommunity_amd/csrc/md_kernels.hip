@@ -589,29 +589,24 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
   lds_i32* hdr = (lds_i32*)(int*)(scr + S_NBH);
   lds_i32* tmp = (lds_i32*)(int*)(scr + S_RED);  // [2][4] wave totals
   lds_u16* nbl = (lds_u16*)(uint16_t*)(scr + S_NBL) + l * NB_CAP;
-  const int* rp = p.rowptr[l] + gi.roff[l];
   const int* adj = p.adj[l] + gi.coff[l];
   const uint8_t* ca = p.calive[l] + gi.coff[l];
-  if (t < 16) {
-    const int v = rows[t];
-    int b = 0, c = 0;
-    if (v >= 0) {
-      b = rp[v];
-      c = rp[v + 1] - b;
-    }
-    hdr[64 + l * 16 + t] = b;
-    hdr[96 + l * 16 + t] = c;
-    hdr[32 + l * 16 + t] = 0;
-  }
-  __syncthreads();
+  // rows' CSR begin / extent are in hdr[64 + 16 l + r] / hdr[96 + 16 l + r] (from the live list)
+  if (t < 16) hdr[32 + l * 16 + t] = 0;
   TSTAMP(60);
   // CSR-extent prefix per row in LDS (a per-thread array indexed at run time would live in
   // scratch memory)
   lds_i32* pre = hdr + 136 + l * 17;
-  if (t < 17) {
-    int a = 0;
-    for (int k = 0; k < t; ++k) a += hdr[96 + l * 16 + k];
-    pre[t] = a;
+  if (t < 16) {
+    // 16-lane inclusive scan of the extents
+    int a = hdr[96 + l * 16 + t];
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const int y = __shfl_up(a, o, 64);
+      if (t >= o) a += y;
+    }
+    pre[t + 1] = a;
+    if (t == 0) pre[0] = 0;
   }
   __syncthreads();
   TSTAMP(61);
@@ -1357,6 +1352,8 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
 
   unsigned target = 0;
   int* bflag = (int*)(lds + L_MISC) + 61;  // barrier error broadcast
+  const int my_gl = (int)threadIdx.x < p.nglist ? p.glist[threadIdx.x] : 0;  // nglist <= G_CAP = NTHREADS
+  const GraphInfo spec_gi = p.ginfo[p.glist[0]];
   int pstep = 0;
   bool have_q = false, staged = false;
   const int ng = p.nglist;
@@ -1380,9 +1377,19 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
     MD_PROF(4);
     if (errA) break;
     // ---------------- tile prefix over the launch's graphs
-    for (int i = threadIdx.x; i < ng; i += NTHREADS) {
-      const GraphVar* gv = p.gvar + p.glist[i];
-      pref[i + 1] = ldc(&gv->status) == ST_RUN ? (ldc(&gv->n_live) + TILE - 1) / TILE : 0;
+    // (one graph, dedicated mode: the rows of tile blockIdx - twg0 are loaded speculatively in
+    // the same round trip; they are this workgroup's tile whenever there are enough workgroups)
+    const bool spec = ded && ng == 1 && !is_env && !is_head && threadIdx.x < TILE;
+    float4 spec_e = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (spec) {
+      const int r = ((int)blockIdx.x - twg0) * TILE + threadIdx.x;
+      spec_e = ldc4((const float*)(p.live + 4 * (size_t)spec_gi.node_off), min(r, spec_gi.n - 1) * 16);
+    }
+    if (threadIdx.x < ng) {
+      const GraphVar* gv = p.gvar + my_gl;
+      const int st = ldc(&gv->status), nl = ldc(&gv->n_live);
+      pref[threadIdx.x + 1] = st == ST_RUN ? (nl + TILE - 1) / TILE : 0;
+      if (threadIdx.x == 0) ((int*)(lds + L_MISC))[62] = nl;  // n_live of the first graph
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1432,12 +1439,30 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
           }
           cur = gl;
         }
-        // rows of the tile (unchanged during a step: a single-tile workgroup keeps them)
-        if ((it == 1 || t1 - t0 > 1) && threadIdx.x < TILE) {
-          const int r = j * TILE + threadIdx.x;
-          const int nl = ldc(&p.gvar[g].n_live);
-          const int lv = ldc(p.live + gi.node_off + min(r, gi.n - 1));
-          rows[threadIdx.x] = r < nl && MD_BOK(lv >= 0 && lv < gi.n && nl <= gi.n, 6) ? lv : -1;
+        // rows of the tile and their CSR ranges (unchanged during a step: a single-tile
+        // workgroup of dedicated mode keeps them; in shared mode the virtual-node chain reuses
+        // that LDS); one 16-byte live-list entry per row
+        if (it == 1 || t1 - t0 > 1 || !ded) {
+          if (threadIdx.x < TILE) {
+            const int r = j * TILE + threadIdx.x;
+            int nl;
+            float4 e;
+            if (spec && it == 1 && t == tb) {
+              nl = ((const int*)(lds + L_MISC))[62];
+              e = spec_e;
+            } else {
+              nl = ldc(&p.gvar[g].n_live);
+              e = ldc4((const float*)(p.live + 4 * (size_t)gi.node_off), min(r, gi.n - 1) * 16);
+            }
+            const bool ok = r < nl && MD_BOK(__float_as_int(e.x) >= 0 && __float_as_int(e.x) < gi.n && nl <= gi.n, 6);
+            const unsigned c = (unsigned)__float_as_int(e.w);
+            lds_i32* hdr = (lds_i32*)(int*)(scr + S_NBH);
+            rows[threadIdx.x] = ok ? __float_as_int(e.x) : -1;
+            hdr[64 + threadIdx.x] = ok ? __float_as_int(e.y) : 0;       // layer 0: CSR begin
+            hdr[96 + threadIdx.x] = ok ? (int)(c & 0xffffu) : 0;        //          CSR extent
+            hdr[64 + 16 + threadIdx.x] = ok ? __float_as_int(e.z) : 0;  // layer 1
+            hdr[96 + 16 + threadIdx.x] = ok ? (int)(c >> 16) : 0;
+          }
         }
         __syncthreads();
         // alive neighbour lists: built at iteration 1, kept for 2 and 3 when this workgroup
