@@ -31,6 +31,10 @@ _u8p = ctypes.POINTER(ctypes.c_uint8)
 _f32p = ctypes.POINTER(ctypes.c_float)
 _f64p = ctypes.POINTER(ctypes.c_double)
 SELECT_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, _f64p, ctypes.c_int, ctypes.c_int, _i32p)
+# the same C type with the row and the output as plain addresses (cheaper to receive: the
+# engine's callback wraps each host buffer as an ndarray once and reuses the view)
+SELECT_CB_ADDR = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_void_p)
 
 _lib = None
 
@@ -58,7 +62,7 @@ def load_library(path=LIB_PATH):
         "md_reset": (ctypes.c_int, [vp, _i32p]),
         "md_predict": (ctypes.c_int, [vp, _f32p, _i32p, _i32p, _f32p]),
         "md_step": (ctypes.c_int, [vp, _i32p, _i32p, _u8p]),
-        "md_rollout": (ctypes.c_int, [vp, ctypes.c_int, _i32p, _i32p, _i32p, SELECT_CB, vp]),
+        "md_rollout": (ctypes.c_int, [vp, ctypes.c_int, _i32p, _i32p, _i32p, SELECT_CB_ADDR, vp]),
         "md_rollout_trace": (ctypes.c_int, [vp, ctypes.c_int, _i32p, _i32p, _i32p, _i32p, _f32p, _f32p, _i32p]),
         "md_get_state": (ctypes.c_int, [vp, ctypes.c_int, _u8p, _u8p, _u8p, _i32p]),
         "md_set_state": (ctypes.c_int, [vp, ctypes.c_int, _u8p, _u8p, _u8p]),
@@ -171,18 +175,29 @@ class Engine:
         ln = np.zeros(len(self.n_nodes), np.int32)
         self._cb_error = None
 
+        views = {}
+
+        def view(addr, n, ct, dt):
+            key = (addr, n, dt)
+            a = views.get(key)
+            if a is None:
+                a = views[key] = np.frombuffer((ct * n).from_address(addr), dtype=dt)
+            return a
+
         def cb(user, g, qp, n, n_out, out):
+            # the row is the library's buffer, valid during the call (the selector must not
+            # keep it); hot path of every tied step, hence the cached views
             try:
-                q = np.ctypeslib.as_array(qp, shape=(n,)).copy()
-                sel = np.asarray(self.selector(q, n_out), dtype=np.int64)
-                for i, a in enumerate(sel[:n_out]):
-                    out[i] = int(a)
+                q = view(qp, n, ctypes.c_double, np.float64)
+                sel = self.selector(q, n_out)
+                o = view(out, n_out, ctypes.c_int32, np.int32)
+                o[:] = sel[:n_out]
                 return 0
             except Exception as ex:  # surfaced after md_rollout returns
                 self._cb_error = ex
                 return 1
 
-        ccb = SELECT_CB(cb)
+        ccb = SELECT_CB_ADDR(cb)
         st = self.lib.md_rollout(self.h, int(step), _ptr(seq, _i32p), _ptr(lm, _i32p), _ptr(ln, _i32p), ccb, None)
         if self._cb_error is not None:
             raise self._cb_error

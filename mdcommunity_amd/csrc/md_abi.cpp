@@ -107,6 +107,7 @@ struct md_ctx {
   HostBuf<unsigned> h_req, h_ans;
   HostBuf<int> h_nact, h_act;
   HostBuf<float> h_q;
+  HostBuf<float> h_chk;
   bool need_gscr = false;
   DevBuf<unsigned long long> prof;
   int prof_cap = 0;
@@ -135,7 +136,7 @@ struct md_ctx {
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
     tr_stat.release(); glist.release(); ctl.release(); q.release(); spart.release();
     apart.release(); ybuf.release(); hbuf.release(); tr_q.release(); node_w.release();
-    h_req.release(); h_ans.release(); h_nact.release(); h_act.release(); h_q.release();
+    h_req.release(); h_ans.release(); h_nact.release(); h_act.release(); h_q.release(); h_chk.release();
     ng = 0;
     hinfo.clear();
     hvar.clear();
@@ -268,8 +269,35 @@ void serve_request(md_ctx* c, Selector* sel, int g, unsigned tag, std::vector<do
     }
   } else {
     qd.resize(gi.n);
-    const float* hq = c->h_q.h + gi.node_off;
-    for (int i = 0; i < gi.n; ++i) qd[i] = std::isinf(hq[i]) ? QMASK : (double)hq[i];
+    const volatile float* hq = c->h_q.h + gi.node_off;
+    // the row must carry the device's own max and tie count (a stale or torn row would
+    // silently change the selection)
+    float mx = -INFINITY;
+    int nt = 0;
+    for (int i = 0; i < gi.n; ++i) {
+      const float x = hq[i];
+      qd[i] = std::isinf(x) ? QMASK : (double)x;
+      if (x > mx) {
+        mx = x;
+        nt = 1;
+      } else if (x == mx) {
+        ++nt;
+      }
+    }
+    const float cmax = c->h_chk.h[2 * g];
+    int cnt;
+    std::memcpy(&cnt, c->h_chk.h + 2 * g + 1, sizeof cnt);
+    if (mx != cmax || nt != cnt) {
+      if (sel->err.empty()) {
+        char b[200];
+        snprintf(b, sizeof b, "graph %d: host Q row (max %.9g, %d at max) disagrees with the device (%.9g, %d)", g,
+                 (double)mx, nt, (double)cmax, cnt);
+        sel->err = b;
+      }
+      c->h_nact.h[g] = -1;
+      __atomic_store_n(c->h_ans.h + g, tag, __ATOMIC_RELEASE);
+      return;
+    }
     const int nout = std::min(sel->step, gi.n);
     acts.assign(nout, -1);
     if (sel->cb(sel->user, g, qd.data(), gi.n, nout, acts.data()) != 0) {
@@ -317,6 +345,7 @@ md_status launch_chunk(md_ctx* c, const int* gl, int ngl, int run_mode, int host
     p.h_nact = c->h_nact.d;
     p.h_act = c->h_act.d;
     p.h_q = c->h_q.d;
+    p.h_chk = c->h_chk.d;
   }
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   HIPCHK(c, launch_rollout(p, c->wimg.p, grid, c->stream));
@@ -325,14 +354,27 @@ md_status launch_chunk(md_ctx* c, const int* gl, int ngl, int run_mode, int host
     // serve selection requests while the launch runs
     std::vector<double> qd;
     std::vector<int32_t> acts;
+    // requests are scanned continuously; the launch's completion event (a runtime call) only
+    // every 20 us, and once more after the last scan that found it complete
+    auto last = std::chrono::steady_clock::now();
+    bool done = false;
     while (true) {
-      const hipError_t q = hipEventQuery(c->ev1);
-      if (q != hipSuccess && q != hipErrorNotReady) HIPCHK(c, q);
+      bool served = false;
       for (int g : v) {
         const unsigned r = __atomic_load_n(c->h_req.h + g, __ATOMIC_ACQUIRE);
-        if (r != 0 && r != __atomic_load_n(c->h_ans.h + g, __ATOMIC_RELAXED)) serve_request(c, sel, g, r, qd, acts);
+        if (r != 0 && r != __atomic_load_n(c->h_ans.h + g, __ATOMIC_RELAXED)) {
+          serve_request(c, sel, g, r, qd, acts);
+          served = true;
+        }
       }
-      if (q == hipSuccess) break;
+      if (done) break;
+      const auto now = std::chrono::steady_clock::now();
+      if (!served && now - last >= std::chrono::microseconds(20)) {
+        last = now;
+        const hipError_t q = hipEventQuery(c->ev1);
+        if (q != hipSuccess && q != hipErrorNotReady) HIPCHK(c, q);
+        done = q == hipSuccess;
+      }
       if (c->poll_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(c->poll_us));
     }
   }
@@ -585,6 +627,7 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->h_nact.alloc((size_t)n_graphs));
   HIPCHK(c, c->h_act.alloc(c->tot_n));
   HIPCHK(c, c->h_q.alloc(c->tot_n));
+  HIPCHK(c, c->h_chk.alloc(2 * (size_t)n_graphs));
   HIPCHK(c, hipMemcpyAsync(c->ginfo.p, info.data(), sizeof(GraphInfo) * n_graphs, hipMemcpyHostToDevice, c->stream));
   if (c->cost_mode == MD_COST_DEGREE) {
     HIPCHK(c, c->node_w.alloc(2 * tn));

@@ -28,7 +28,7 @@ enum WOff : int {
 enum : uint8_t { E_ALIVE = 0, E_COVERED = 1, E_PRUNED = 2 };
 
 // Per-graph run status.
-enum : int { ST_RUN = 0, ST_TERMINAL = 1, ST_NEED_HOST = 2, ST_PAUSED = 3 };
+enum : int { ST_RUN = 0, ST_TERMINAL = 1, ST_NEED_HOST = 2, ST_PAUSED = 3, ST_WAIT_HOST = 4 };
 
 // What a launch does with each graph.
 enum : int { RUN_ROLLOUT = 0, RUN_PREDICT = 1, RUN_STEP = 2 };
@@ -63,6 +63,7 @@ struct GraphVar {            // mutable per-graph state
   int ntie;                  // last prediction: nodes tied at the max
   float qmax, gap;           // last prediction: best Q and top-2 gap
   int hdmax[2];              // dmax the unit-cost first-layer table was built for (0 = none)
+  unsigned long long t_req;  // ST_WAIT_HOST: device wall clock of the pending host request
 };
 
 struct Params {
@@ -101,6 +102,7 @@ struct Params {
   int* h_nact;                     // per graph: actions answered (-1: abort)
   int* h_act;                      // per node slot: answered actions
   float* h_q;                      // per node slot: Q of the request (-inf = masked)
+  float* h_chk;                    // per graph: {max Q, tie count (int bits)} of the request
   const int* glist;                // graphs processed by this launch (<= G_CAP)
   int nglist;
   int n_env;                       // dedicated environment workgroups (0 = shared mode)

@@ -350,36 +350,51 @@ __device__ __forceinline__ void argmax_combine(float& bm, float& bs, int& bi, in
 }
 
 // Host selection hand-shake for graph g (ties at the max Q, or a multi-node step): publish
-// the graph's Q row to mapped host memory, raise the request tag, wait for the host's answer
-// (its selection callback = the reference's np.argsort pick), copy the actions to p.pend.
-// Returns the number of actions (0 on error; the error word is set).
-__device__ __noinline__ int host_handshake(KParams&, const GraphInfo gi, int g, int npred, int* misc) {
+// the graph's Q row, its max and tie count to mapped host memory and raise the request tag;
+// the host answers with its selection callback (the reference's np.argsort pick).  All host
+// memory traffic is system-scope (uncached) and in program order over the link, so no cache
+// write-back / invalidate is needed (those would flush the whole L2 under the running grid).
+__device__ __forceinline__ unsigned host_tag(KParams& p, int npred) {
+  return (p.launch_seq << 16) ^ (unsigned)(npred + 1);
+}
+__device__ __noinline__ void host_request(KParams&, const GraphInfo gi, int g, int npred, float qmax, int ntie) {
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
-  const unsigned tag = (p.launch_seq << 16) ^ (unsigned)(npred + 1);
-  for (int x = threadIdx.x; x < gi.n; x += NTHREADS) p.h_q[gi.node_off + x] = ldc(p.q + gi.node_off + x);
+  for (int x = threadIdx.x; x < gi.n; x += NTHREADS)
+    __hip_atomic_store(p.h_q + gi.node_off + x, ldc(p.q + gi.node_off + x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(p.h_chk + 2 * g, qmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(p.h_chk + 2 * g + 1, __int_as_float(ntie), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(p.h_req + g, host_tag(p, npred), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// Thread 0 only: the host's answer to request `npred` of graph g, copied to p.pend.
+// Returns the number of actions, 0 when not answered yet, -1 on a bad answer.
+__device__ __forceinline__ int host_answer(KParams& p, const GraphInfo& gi, int g, int npred) {
+  if (__hip_atomic_load(p.h_ans + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != host_tag(p, npred)) return 0;
+  const int k = __hip_atomic_load(p.h_nact + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (k <= 0 || k > gi.n) return -1;
+  for (int i = 0; i < k; ++i)
+    __hip_atomic_store(p.pend + gi.node_off + i,
+                       __hip_atomic_load(p.h_act + gi.node_off + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return k;
+}
+// Synchronous form (one graph per launch: nothing else could run meanwhile): request, then
+// wait for the answer.  Returns the number of actions (0 on error; the error word is set).
+__device__ __noinline__ int host_handshake(KParams&, const GraphInfo gi, int g, int npred, float qmax, int ntie, int* misc) {
+  KParams& p = kp();
+  host_request(p, gi, g, npred, qmax, ntie);
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(p.h_req + g, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const unsigned long long t0 = wall_clock64();
-    int k = 0;
-    while (__hip_atomic_load(p.h_ans + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != tag) {
+    int k;
+    while ((k = host_answer(p, gi, g, npred)) == 0) {
       __builtin_amdgcn_s_sleep(2);
       if (wall_clock64() - t0 > HOST_TIMEOUT_TICKS) {
         k = -1;
         break;
       }
-    }
-    if (k == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-      k = __hip_atomic_load(p.h_nact + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (k < 0 || k > gi.n) k = -1;
-      for (int i = 0; i < k; ++i)
-        __hip_atomic_store(p.pend + gi.node_off + i,
-                           __hip_atomic_load(p.h_act + gi.node_off + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (k < 0) raise_err(p, ERR_HOST);
     misc[3] = k;
@@ -398,10 +413,23 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
   // its current GraphVar in LDS (nobody else writes it during a launch)
   if (!(staged && p.n_env > 0)) gv_load(p, g, &gv);
   __syncthreads();
-  if (gv.status != ST_RUN) return staged;
   int pend_n = 0, pend_first = -1;
   bool stop = false;
-  if (have_q) {
+  if (gv.status == ST_WAIT_HOST) {
+    // asynchronous hand-shake (several graphs per launch): the graph sat out the steps since
+    // its request while the others went on; poll the host's answer once per step
+    if (threadIdx.x == 0) {
+      int k = host_answer(p, gi, g, gv.npred);
+      if (k == 0 && wall_clock64() - gv.t_req > HOST_TIMEOUT_TICKS) k = -1;
+      if (k < 0) raise_err(p, ERR_HOST);
+      misc[3] = k;
+    }
+    __syncthreads();
+    if (misc[3] <= 0) return staged;
+    pend_n = misc[3];
+  } else if (gv.status != ST_RUN) {
+    return staged;
+  } else if (have_q) {
     float bm = NEG_INF, bs = NEG_INF;
     int bi = 0x7fffffff, bc = 0;
     if (threadIdx.x < 64) {
@@ -453,8 +481,18 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
       if (false) {
 #endif
         // ask the host without ending the launch; the actions land in p.pend
-        pend_n = host_handshake(p, gi, g, gv.npred, misc);
-        stop = pend_n <= 0;
+        if (p.nglist > 1) {
+          // several graphs: the others keep stepping while the host answers
+          host_request(p, gi, g, gv.npred, gv.qmax, gv.ntie);
+          if (threadIdx.x == 0) {
+            gv.status = ST_WAIT_HOST;
+            gv.t_req = wall_clock64();
+          }
+          stop = true;
+        } else {
+          pend_n = host_handshake(p, gi, g, gv.npred, gv.qmax, gv.ntie, misc);
+          stop = pend_n <= 0;
+        }
       } else {
         if (threadIdx.x == 0) gv.status = ST_NEED_HOST;
         stop = true;
@@ -1385,20 +1423,29 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
       const int r = ((int)blockIdx.x - twg0) * TILE + threadIdx.x;
       spec_e = ldc4((const float*)(p.live + 4 * (size_t)spec_gi.node_off), min(r, spec_gi.n - 1) * 16);
     }
+    bool waiting = false;
     if (threadIdx.x < ng) {
       const GraphVar* gv = p.gvar + my_gl;
       const int st = ldc(&gv->status), nl = ldc(&gv->n_live);
       pref[threadIdx.x + 1] = st == ST_RUN ? (nl + TILE - 1) / TILE : 0;
+      waiting = st == ST_WAIT_HOST;
       if (threadIdx.x == 0) ((int*)(lds + L_MISC))[62] = nl;  // n_live of the first graph
     }
-    __syncthreads();
+    waiting = __syncthreads_or(waiting);
     if (threadIdx.x == 0) {
       pref[0] = 0;
       for (int i = 0; i < ng; ++i) pref[i + 1] += pref[i];
     }
     __syncthreads();
     const int ttot = pref[ng];
-    if (ttot == 0) break;
+    if (ttot == 0) {
+      if (!waiting) break;
+      // only graphs waiting for a host answer: one more barrier (nobody writes a GraphVar
+      // before every workgroup has read the prefix), then phase A polls again
+      if (grid_sync(p, target, bflag)) break;
+      pstep++;
+      continue;
+    }
     const int per = (ttot + ntw - 1) / ntw;
     const int tb = (int)blockIdx.x - twg0;
     const bool tiles = !is_env && !is_head;

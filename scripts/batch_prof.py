@@ -1,0 +1,45 @@
+"""Per-step phase profile of a batched rollout launch (shared mode): workgroup-0 wall-clock
+stamps per removal step, next to the active graphs and live-node tiles of that step."""
+import os, sys, time
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from mdcommunity_amd import _lib, engine, gmm
+
+nb = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+W = engine.load_weights(engine.DEFAULT_UNIT)
+graphs = [(1000,) + gmm.gmm_pair(1000, seed=s) for s in range(nb)]
+eng = _lib.Engine(W)
+eng.load_graphs(graphs)
+eng.reset(); eng.rollout()
+eng.reset()
+t0 = time.time(); out = eng.rollout(); dt = time.time() - t0
+ms, nl = eng.last_timing()
+lens = np.array([len(o[0]) for o in out])
+print(f"batch {nb}: removals {lens.sum()} kernel {ms:.2f} ms wall {dt*1e3:.1f} ms -> {lens.sum()/dt:.0f} rem/s; "
+      f"rollout length min/median/max {lens.min()}/{int(np.median(lens))}/{lens.max()}", flush=True)
+# per-step work from the device traces
+S = lens.max() + 1
+act = np.zeros(S, int); tiles = np.zeros(S, int); nodes = np.zeros(S, int)
+for g in range(nb):
+    tr = eng.trace(g)
+    for t, n_t in enumerate(tr["n_live"]):
+        act[t] += 1; tiles[t] += (int(n_t) + 15) // 16; nodes[t] += int(n_t)
+eng.reset()
+eng.profile(512)
+eng.rollout()
+ms2, _ = eng.last_timing()
+P = eng.profile_read().astype(np.int64)
+eng.profile(0)
+full = P[P[:, 10] > 0]
+d = lambda a, b: (full[:, b] - full[:, a]) / 100.0
+A, bA, i1, i2, i3 = d(0, 3), d(3, 4), d(4, 6), d(6, 8), d(8, 10)
+tot = d(0, 10)
+print(f"profiled kernel {ms2:.2f} ms, steps {len(full)}; sum of step times {tot.sum()/1000:.2f} ms", flush=True)
+print("phase totals ms: A %.2f barA %.2f it1 %.2f it2 %.2f it3 %.2f" % (A.sum()/1e3, bA.sum()/1e3, i1.sum()/1e3, i2.sum()/1e3, i3.sum()/1e3))
+# (profiled steps include the steps where every running graph waited for a host answer, so
+# the work columns are exact only up to the first tie)
+for t in list(range(0, min(len(full), 12))) + list(range(12, len(full), max(1, len(full)//20))):
+    wk = (act[t], tiles[t], nodes[t]) if t < S else (0, 0, 0)
+    print(f"step {t:4d}: active {wk[0]:4d} tiles {wk[1]:6d} nodes {wk[2]:7d} | A {A[t]:7.1f} barA {bA[t]:5.1f} it1 {i1[t]:7.1f} it2 {i2[t]:7.1f} it3 {i3[t]:7.1f} us", flush=True)
+eng.close()
