@@ -26,6 +26,7 @@ int weight_image_floats();
 bool phase_a_fits_lds_host(int n, int edges);
 void build_weight_image(const float* w, float* img);
 hipError_t launch_rollout(const Params& p, const float* wimg, int grid, hipStream_t s);
+hipError_t launch_h0(const float* w, float* tab, int dm_lo, int dm_hi, hipStream_t s);
 hipError_t launch_reset(const Params& p, hipStream_t s);
 hipError_t set_kernel_attrs();
 }  // namespace md
@@ -88,6 +89,9 @@ struct md_ctx {
   int last_launches = 0;
 
   DevBuf<float> w, wimg;
+  DevBuf<float> h0g;  // unit cost: precomputed first-layer tables, dmax 1..h0g_dm
+  int h0g_dm = 0;
+  bool h0g_on = true;  // MD_H0G=0: rebuild the tables in phase A instead (tests)
   // graphs
   int ng = 0;
   std::vector<GraphInfo> hinfo;
@@ -197,6 +201,8 @@ Params make_params(md_ctx* c) {
   p.tr_stat = c->tr_stat.p;
   p.tr_q = c->tr_q.p;
   p.node_w = c->cost_mode == MD_COST_DEGREE ? c->node_w.p : nullptr;
+  p.h0g = c->h0g.p;
+  p.h0g_dm = c->h0g.p ? c->h0g_dm : 0;
   p.bar = (unsigned*)(c->ctl.p + CTL_BAR);
   p.err = c->ctl.p + CTL_ERR;
   p.glist = c->glist.p;
@@ -447,6 +453,7 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_ENV_MODE")) c->env_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_HOST_HANDSHAKE")) c->host_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_POLL_US")) c->poll_us = std::atoi(v);
+  if (const char* v = std::getenv("MD_H0G")) c->h0g_on = std::atoi(v) != 0;
   md_status st = MD_OK;
   do {
     if (hipSetDevice(device) != hipSuccess) { st = MD_EHIP; break; }
@@ -467,6 +474,27 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
 }
 
 void md_destroy(md_ctx* ctx) { delete ctx; }
+
+// Unit cost: the first-layer tables of every dmax up to the largest loaded graph's n - 1
+// (tables of dmax <= H0G_MAX_DM only: 2048 dmax values are 537 MB; larger dmax values are
+// rebuilt in phase A).  Recomputed from scratch when the weights change.
+constexpr int H0G_MAX_DM = 2048;
+md_status ensure_h0g(md_ctx* c, int need, bool weights_changed) {
+  if (c->cost_mode != MD_COST_UNIT || !c->h0g_on) return MD_OK;
+  need = std::min(need, H0G_MAX_DM);
+  if (weights_changed && c->h0g.p) c->h0g_dm = 0;
+  if (need <= c->h0g_dm) return MD_OK;
+  const size_t rows = (size_t)h0g_row(need + 1, 1);
+  if (!c->h0g.p || c->h0g.n < rows * EMB) {
+    c->h0g.release();
+    HIPCHK(c, c->h0g.alloc(rows * EMB));
+    c->h0g_dm = 0;
+  }
+  HIPCHK(c, launch_h0(c->w.p, c->h0g.p, c->h0g_dm + 1, need, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->h0g_dm = need;
+  return MD_OK;
+}
 
 md_status md_set_weights(md_ctx* c, const float* weights, size_t n_floats) {
   if (!c || !weights || n_floats != MD_WEIGHT_FLOATS) return fail(c, MD_EINVAL, "weights: expected %d floats", MD_WEIGHT_FLOATS);
@@ -490,8 +518,14 @@ md_status md_set_weights(md_ctx* c, const float* weights, size_t n_floats) {
     }
   } else if (c->ng > 0) {
     // unit cost: the per-graph degree tables were built from the old weights
+    int maxn = 0;
+    for (const auto& gi : c->hinfo) maxn = std::max(maxn, gi.n);
+    md_status st = ensure_h0g(c, maxn - 1, true);
+    if (st != MD_OK) return st;
     for (auto& v : c->hvar) v.hdmax[0] = v.hdmax[1] = 0;
     return push_vars(c);
+  } else if (c->h0g.p) {
+    c->h0g_dm = 0;
   }
   return MD_OK;
 }
@@ -642,6 +676,12 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
     }
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  {
+    int maxn = 0;
+    for (int g = 0; g < n_graphs; ++g) maxn = std::max(maxn, (int)n_nodes[g]);
+    md_status st = ensure_h0g(c, maxn - 1, false);
+    if (st != MD_OK) return st;
+  }
   return md_reset(c, nullptr);
 }
 

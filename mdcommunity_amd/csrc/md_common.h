@@ -33,6 +33,10 @@ enum : int { ST_RUN = 0, ST_TERMINAL = 1, ST_NEED_HOST = 2, ST_PAUSED = 3, ST_WA
 // What a launch does with each graph.
 enum : int { RUN_ROLLOUT = 0, RUN_PREDICT = 1, RUN_STEP = 2 };
 
+// Row of degree d (1 <= d <= dm) in the precomputed first-layer tables: dmax dm's rows are
+// contiguous, tables in ascending dmax.
+__host__ __device__ inline long long h0g_row(int dm, int d) { return (long long)dm * (dm - 1) / 2 + (d - 1); }
+
 struct GraphInfo {           // immutable after md_load_graphs
   int n;                     // nodes
   int node_off;              // into per-node arrays
@@ -103,6 +107,8 @@ struct Params {
   int* h_act;                      // per node slot: answered actions
   float* h_q;                      // per node slot: Q of the request (-inf = masked)
   float* h_chk;                    // per graph: {max Q, tie count (int bits)} of the request
+  const float* h0g;                // unit cost: first-layer rows of every dmax <= h0g_dm (h0g_row)
+  int h0g_dm;
   const int* glist;                // graphs processed by this launch (<= G_CAP)
   int nglist;
   int n_env;                       // dedicated environment workgroups (0 = shared mode)

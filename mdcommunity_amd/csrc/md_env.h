@@ -727,21 +727,52 @@ __device__ int env_step(KParams& p, const GraphInfo& gi, GraphVar& gv, float* ar
   }
   MD_PROF_A(14);
   // First-layer embedding by degree (unit cost): X = [d/dmax, d/dmax] (net :252-261),
-  // normalize(relu(X . w_n2l)) with the 2-term FMA chain of MKL's sgemm; one wave per row
-  // d = 1..dmax.  The table depends on dmax only, so it is rebuilt only when dmax changed.
+  // normalize(relu(X . w_n2l)) with the 2-term FMA chain of MKL's sgemm; one thread per row
+  // d = 1..dmax (the row recomputed for the norm pass and the store pass; w_n2l arrives as
+  // scalar loads), the norm in torch's order (wave_norm64's).  The table depends on dmax
+  // only, so it is rebuilt only when dmax changed.
   if (p.node_w == nullptr) {
     const float* wn = p.w + W_N2L;
-    const int lane = lane_id(), w = wave_id();
-    const float w0 = wn[lane], w1 = wn[64 + lane];
     for (int l = 0; l < 2; ++l) {
       const int dm = l ? dm1 : dm0;
       if (dm == (l ? hd1 : hd0)) continue;
       float* tab = p.h0tab[l] + (size_t)gi.node_off * EMB;  // degrees <= n-1 fit the graph's rows
-      for (int d = 1 + w; d <= dm; d += NTHREADS / 64) {
+      if (dm <= p.h0g_dm) {
+        // the table of this dmax is precomputed (md_h0_kernel at load): a 16-byte copy
+        const float* src = p.h0g + h0g_row(dm, 1) * EMB;
+        const int nq = 16 * dm;
+        for (int i0 = threadIdx.x; i0 < nq; i0 += 4 * NTHREADS) {
+          float4 x[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (i0 + k * NTHREADS < nq) x[k] = ldc4(src, (i0 + k * NTHREADS) * 16);
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (i0 + k * NTHREADS < nq) stc4(tab, EMB * 4 + (i0 + k * NTHREADS) * 16, x[k]);
+        }
+        continue;
+      }
+      for (int d = 1 + (int)threadIdx.x; d <= dm; d += NTHREADS) {
         const float f = (float)d / (float)dm;
-        const float x = fmaxf(fmaf(f, w1, fmaf(f, w0, 0.f)), 0.f);
-        const float nr = wave_norm64(x);
-        stc(tab + (size_t)d * EMB + lane, x / fmaxf(nr, 1e-12f));
+        float acc[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+        for (int c = 0; c < 64; ++c) {
+          const float x = fmaxf(fmaf(f, wn[64 + c], fmaf(f, wn[c], 0.f)), 0.f);
+          acc[c & 7] = fmaf(x, x, acc[c & 7]);
+        }
+        const float den = fmaxf(sqrtf(sumsq8_finish(acc)), 1e-12f);
+#pragma unroll
+        for (int c4 = 0; c4 < 16; ++c4) {
+          float o[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int c = 4 * c4 + k;
+            o[k] = fmaxf(fmaf(f, wn[64 + c], fmaf(f, wn[c], 0.f)), 0.f) / den;
+          }
+          stc4(tab, d * 256 + c4 * 16, make_float4(o[0], o[1], o[2], o[3]));
+        }
       }
     }
     if (threadIdx.x == 0) {

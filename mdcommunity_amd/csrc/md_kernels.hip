@@ -1606,6 +1606,29 @@ __global__ void __launch_bounds__(NTHREADS, 1) md_env_kernel(Params p, const flo
 }
 
 // Reset every graph in glist to the initial (pre-s0) state.
+// Unit-cost first-layer tables of every dmax 1..dm_max (the per-step rebuild of phase A
+// becomes a copy): block dm, thread per row d, the same expressions as env_step's rebuild.
+__global__ void __launch_bounds__(256) md_h0_kernel(const float* __restrict__ w, float* tab, int dm_lo, int dm_hi) {
+  const int dm = dm_lo + (int)blockIdx.x;
+  if (dm > dm_hi) return;
+  const float* wn = w + W_N2L;
+  for (int d = 1 + (int)threadIdx.x; d <= dm; d += blockDim.x) {
+    const float f = (float)d / (float)dm;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 64; ++c) {
+      const float x = fmaxf(fmaf(f, wn[64 + c], fmaf(f, wn[c], 0.f)), 0.f);
+      acc[c & 7] = fmaf(x, x, acc[c & 7]);
+    }
+    const float den = fmaxf(sqrtf(sumsq8_finish(acc)), 1e-12f);
+    float* row = tab + h0g_row(dm, d) * EMB;
+#pragma unroll
+    for (int c = 0; c < 64; ++c) row[c] = fmaxf(fmaf(f, wn[64 + c], fmaf(f, wn[c], 0.f)), 0.f) / den;
+  }
+}
+
 __global__ void md_reset_kernel(Params p) {
   const int gidx = blockIdx.x;
   if (gidx >= p.nglist) return;
@@ -1674,6 +1697,12 @@ hipError_t launch_rollout(const Params& p, const float* wimg, int grid, hipStrea
     hipLaunchKernelGGL(md_rollout_kernel, dim3(grid), dim3(NTHREADS), lds_bytes(), s, p, wimg);
   else
     hipLaunchKernelGGL(md_env_kernel, dim3(grid), dim3(NTHREADS), lds_bytes(), s, p, wimg);
+  return hipGetLastError();
+}
+
+hipError_t launch_h0(const float* w, float* tab, int dm_lo, int dm_hi, hipStream_t s) {
+  if (dm_hi < dm_lo) return hipSuccess;
+  hipLaunchKernelGGL(md_h0_kernel, dim3(dm_hi - dm_lo + 1), dim3(256), 0, s, w, tab, dm_lo, dm_hi);
   return hipGetLastError();
 }
 

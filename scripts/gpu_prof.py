@@ -37,6 +37,15 @@ def prof(name, team):
     print(f"{name} team={team} variant={os.environ.get('MD_VARIANT', '0')} env_mode={os.environ.get('MD_ENV_MODE', '1')}: removals {len(out[0][0])} wall {dt*1e3:.2f} ms kernel {ms:.2f} ms launches {nl}; "
           f"steps profiled {len(full)} median step {tot:.1f} us", flush=True)
     print("   " + "  ".join(f"{s}={d(a,b):.1f}" for s, a, b in seg), flush=True)
+    dm = lambda a, b: np.mean((full[:, b] - full[:, a])) * 10 / 1000.0
+    print("   mean: " + "  ".join(f"{s}={dm(a,b):.1f}" for s, a, b in seg), flush=True)
+    stp = (full[:, 10] - full[:, 0]) / 100.0
+    print("   sum of step times %.3f ms (kernel %.3f ms); first step %.1f us; top-5 steps %s us at %s" % (
+        stp.sum() / 1000, ms, stp[0], np.round(np.sort(stp)[-5:], 1).tolist(), np.argsort(stp)[-5:].tolist()), flush=True)
+    for t in range(min(12, len(full))):
+        acc_ = full[t, 16:23]
+        print("   step %2d: %s | rounds %d unite %.1f label %.1f prune %.1f" % (t, "  ".join(
+            f"{s}={(full[t, b] - full[t, a]) / 100:.1f}" for s, a, b in seg), acc_[0], acc_[1] / 100, acc_[2] / 100, acc_[3] / 100), flush=True)
     tt = lambda a, b: np.median((full[:, b].astype(np.int64) - full[:, a].astype(np.int64))) / 100.0
     print("   tile wg: p1 gather %.1f upd %.1f end %.1f | p2 gather %.1f upd %.1f end %.1f | p3 gather %.1f upd %.1f attn %.1f us" % (
         tt(11, 23), tt(23, 24), tt(24, 25), tt(12, 26), tt(26, 27), tt(27, 28), tt(13, 29), tt(29, 30), tt(30, 31)), flush=True)

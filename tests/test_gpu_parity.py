@@ -194,3 +194,30 @@ def test_global_memory_environment_mode(monkeypatch):
             assert audc(ranks, int(z["max_rank"]), n) == float(z["score"])
     finally:
         e.close()
+
+
+def test_precomputed_first_layer_tables(monkeypatch):
+    """Unit cost: the first-layer tables of every dmax precomputed at load (md_h0_kernel)
+    give the same rollouts and Q as rebuilding them in phase A (MD_H0G=0), also after the
+    weights are replaced on a loaded context."""
+    w_a = engine.load_weights(engine.DEFAULT_UNIT)
+    w_b = engine.load_weights(engine.DEFAULT_UNIT_REAL)
+    z = load_golden("gmm1000_s2")
+    g = (int(z["n_nodes"]), z["edges0"], z["edges1"])
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MD_H0G", mode)
+        e = _lib.Engine(w_b)
+        try:
+            e.load_graphs([g])
+            e.set_weights(w_a)
+            e.reset()
+            q, _, _, _ = e.predict()
+            out[mode] = (q.copy(), [(s.tolist(), r.tolist()) for s, r in e.rollout()])
+            e.set_weights(w_b)
+            e.reset()
+            out[mode] += ([(s.tolist(), r.tolist()) for s, r in e.rollout()],)
+        finally:
+            e.close()
+    assert np.array_equal(out["1"][0], out["0"][0])
+    assert out["1"][1] == out["0"][1] and out["1"][2] == out["0"][2]
