@@ -276,6 +276,25 @@ __device__ __forceinline__ void for_each_alive(const EnvView<GL>& E, F&& f) {
   }
 }
 
+// Union-pass order: in LDS mode every thread takes a contiguous run of the alive list, so the
+// edges in flight at one time are spread over the graph (few threads contend for the same
+// roots) while each thread's consecutive edges share endpoints (short, compressed paths).
+template <bool GL, class F>
+__device__ __forceinline__ void for_each_alive_runs(const EnvView<GL>& E, F&& f) {
+  if constexpr (GL) {
+    for_each_alive<GL>(E, f);
+  } else {
+    const int na = E.hdr[0];
+    const lds_u16* al = E.hdr[2] ? E.al_other : E.al;
+    const int chunk = (na + NTHREADS - 1) / NTHREADS;
+    const int i0 = min(na, (int)threadIdx.x * chunk), i1 = min(na, i0 + chunk);
+    for (int i = i0; i < i1; ++i) {
+      const int e = al[i];
+      if (E.st[e] == E_ALIVE) f(e, (int)E.u16[e], (int)E.v16[e]);
+    }
+  }
+}
+
 // Builds the alive list from the staged edge states (ascending edge ids).
 template <bool GL>
 __device__ void build_alive(const EnvView<GL>& E) {
@@ -346,7 +365,7 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
   const int n = E.gi->n;
   int pruned0 = 0, pruned1 = 0;
   if (acc != nullptr && threadIdx.x == 0) acc[PA_CALLS] += 1;
-  bool first = true, compacted = cover < 0;
+  bool first = true, dirty = cover >= 0;  // dead entries in the alive list
   while (true) {
     unsigned long long tp = wall_clock64();
     if (acc != nullptr && threadIdx.x == 0) acc[PA_ROUNDS] += 1;
@@ -358,7 +377,7 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
     PACC(acc, PA_INIT, tp);
     int k0 = 0, k1 = 0;
     if (first && cover >= 0) {
-      for_each_alive<GL>(E, [&](int e, int u, int v) {
+      for_each_alive_runs<GL>(E, [&](int e, int u, int v) {
         if (u == cover || v == cover) {
           E.kill(e, E_COVERED);
           if (e < E.e0) k0++; else k1++;
@@ -367,7 +386,7 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
         }
       });
     } else {
-      for_each_alive<GL>(E, [&](int e, int u, int v) { uf_unite(e < E.e0 ? E.par0 : E.par1, u, v); });
+      for_each_alive_runs<GL>(E, [&](int e, int u, int v) { uf_unite(e < E.e0 ? E.par0 : E.par1, u, v); });
     }
     __syncthreads();
     PACC(acc, PA_UNITE, tp);
@@ -413,7 +432,9 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
     PACC(acc, PA_LABEL, tp);
     tp = wall_clock64();
     if (!diff) {
-      if (!compacted) compact_alive<GL>(E);  // the covered edges move to the dead list
+      // the covered / pruned edges leave the alive list for the dead list once, at the end
+      // (later rounds skip them by their state)
+      if (dirty) compact_alive<GL>(E);
       break;
     }
     int c0 = 0, c1 = 0;
@@ -427,8 +448,7 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
     const int2 c = block_sum2(c0, c1, E.tmp);
     pruned0 += c.x;
     pruned1 += c.y;
-    compact_alive<GL>(E);
-    compacted = true;
+    dirty = true;
     PACC(acc, PA_PRUNE, tp);
   }
   const unsigned long long tc = wall_clock64();
