@@ -771,29 +771,49 @@ __device__ __noinline__ void gather_tile2(KParams&, const GraphInfo gi, int it, 
   const int totl = hdr[128 + l];
   const int nbat = (max(hdr[128], hdr[129]) + STG_ROWS - 1) / STG_ROWS;
   float4* stg = (float4*)(scr + S_M) + l * STG_ROWS * 16;
-  for (int b = 0; b < nbat; ++b) {
+  // Batch b's five 16-byte loads per thread go out while batch b - 1 is summed (register
+  // double buffer: the global latency of a batch overlaps the previous batch's adds); the
+  // per-row adds read eight staged rows ahead of their (in-order) accumulation.
+  auto issue = [&](int b, float4 (&x)[5], bool (&ok)[5]) {
     const int base = b * STG_ROWS;
     int src[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
       const int k = t + 256 * i, row = base + (k >> 4);
       src[i] = -1;
-      if (k < STG_ROWS * 16 && row < totl) {
+      if (b < nbat && k < STG_ROWS * 16 && row < totl) {
         const int id = nbl[row];
         src[i] = MD_BOK(id < gi.n, 4) ? (table ? ldc(deg + id) : id) : -1;
         if (!MD_BOK(src[i] < gi.n, 5)) src[i] = -1;
       }
     }
-    float4 x[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      ok[i] = src[i] >= 0;
+      if (ok[i]) x[i] = ldc4(hp, src[i] * 256 + ((t + 256 * i) & 15) * 16);
+    }
+  };
+  auto consume = [&](int b, const float4 (&x)[5], const bool (&ok)[5]) {
+    const int base = b * STG_ROWS;
 #pragma unroll
     for (int i = 0; i < 5; ++i)
-      if (src[i] >= 0) x[i] = ldc4(hp, src[i] * 256 + ((t + 256 * i) & 15) * 16);
-#pragma unroll
-    for (int i = 0; i < 5; ++i)
-      if (src[i] >= 0) stg[t + 256 * i] = x[i];
+      if (ok[i]) stg[t + 256 * i] = x[i];
     __syncthreads();
     const int lo = max(myoff, base), hi = min(myoff + mycnt, base + STG_ROWS);
-    for (int k = lo; k < hi; ++k) {
+    int k = lo;
+    for (; k + 8 <= hi; k += 8) {
+      float4 y[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y[j] = stg[(k + j - base) * 16 + qd];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        acc.x = acc.x + y[j].x;
+        acc.y = acc.y + y[j].y;
+        acc.z = acc.z + y[j].z;
+        acc.w = acc.w + y[j].w;
+      }
+    }
+    for (; k < hi; ++k) {
       const float4 y = stg[(k - base) * 16 + qd];
       acc.x = acc.x + y.x;
       acc.y = acc.y + y.y;
@@ -801,6 +821,16 @@ __device__ __noinline__ void gather_tile2(KParams&, const GraphInfo gi, int it, 
       acc.w = acc.w + y.w;
     }
     __syncthreads();
+  };
+  float4 xa[5], xb[5];
+  bool oka[5], okb[5];
+  if (nbat > 0) issue(0, xa, oka);
+  for (int b = 0; b < nbat; b += 2) {
+    issue(b + 1, xb, okb);
+    consume(b, xa, oka);
+    if (b + 1 >= nbat) break;
+    issue(b + 2, xa, oka);
+    consume(b + 1, xb, okb);
   }
   float* atp = scr + S_P + l * 64 * LDT;
   float* atx = scr + S_X + l * 64 * LDT;
