@@ -249,7 +249,8 @@ int grid_size(md_ctx* c, const std::vector<int>& gl, int n_env) {
   long tiles = 0;
   for (int g : gl) tiles += (c->hinfo[g].n + TILE - 1) / TILE;
   if (c->team_size_req > 0) tiles = c->team_size_req;
-  const long want = n_env > 0 ? 2 * n_env + std::max<long>(1, tiles) : std::max<long>((long)gl.size(), tiles);
+  // dedicated mode: two tile workgroups per tile when they fit (the kernel's layer split)
+  const long want = n_env > 0 ? 2 * n_env + 2 * std::max<long>(1, tiles) : std::max<long>((long)gl.size(), tiles);
   return (int)std::max<long>(2 * n_env + 1, std::min<long>(want, c->cus));
 }
 

@@ -212,6 +212,12 @@ __device__ __forceinline__ float4 ldc4(const float* base, int byte_off) {
   const v4f v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16 /* sc1 */);
   return make_float4(v.x, v.y, v.z, v.w);
 }
+__device__ __forceinline__ float2 ldc2(const float* base, int byte_off) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(base), 0, 0x7fffffff, 0x00020000);
+  typedef float v2f __attribute__((ext_vector_type(2)));
+  const v2f v = __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 16 /* sc1 */);
+  return make_float2(v.x, v.y);
+}
 __device__ __forceinline__ void stc4(float* base, int byte_off, float4 x) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(base), 0, 0x7fffffff, 0x00020000);
   const v4f v = {x.x, x.y, x.z, x.w};
@@ -845,6 +851,175 @@ __device__ __noinline__ void gather_tile2(KParams&, const GraphInfo gi, int it, 
   atx[(c + 3) * LDT + r] = own.w;
 }
 
+// ------------------------------------------------------------------ layer-split tile pieces
+// Dedicated mode with at least two tile workgroups per tile: workgroup (tile, L) runs layer L
+// of iterations 1 and 2 with all eight waves (the two layers only meet in the attention of
+// iteration 3, which the L = 0 workgroup runs for both).  Same arithmetic, same order.
+
+// Gather of layer L from its alive neighbour list: the 512 threads stage up to 2 * STG_ROWS
+// neighbour rows per batch (register double buffer as in gather_tile2), 32 lanes per row add
+// two features each in CSR order.
+__device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it, const int* rows, float* scr, int L) {
+  KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
+  constexpr int SROWS = 2 * STG_ROWS, NLD = (SROWS * 16 + NTHREADS - 1) / NTHREADS;
+  const int w = wave_id(), lane = lane_id(), t = threadIdx.x, l = L;
+  const int q = lane & 31;
+  const int r = 2 * w + (lane >> 5);
+  const int* deg = p.deg[l] + gi.node_off;
+  const float* hp;
+  bool table = false;
+  if (it == 1) {
+    hp = p.h0tab[l] + (size_t)gi.node_off * EMB;
+    table = p.node_w == nullptr;
+  } else {
+    hp = p.H[l][(it - 2) & 1] + (size_t)gi.node_off * EMB;
+  }
+  const lds_i32* hdr = (const lds_i32*)(const int*)(scr + S_NBH);
+  const lds_u16* nbl = (const lds_u16*)(const uint16_t*)(scr + S_NBL) + l * NB_CAP;
+  const int v = rows[r];
+  float2 own = {0.f, 0.f}, acc = {0.f, 0.f};
+  if (v >= 0) {
+    const int ov = table ? ldc(deg + v) : v;
+    if (MD_BOK(v < gi.n && ov >= 0 && ov < gi.n, 1)) own = ldc2(hp, ov * 256 + q * 8);
+  }
+  const int myoff = hdr[l * 16 + r], mycnt = hdr[32 + l * 16 + r];
+  const int totl = hdr[128 + l];
+  const int nbat = (totl + SROWS - 1) / SROWS;
+  float4* stg = (float4*)(scr + S_M);
+  const float2* stg2 = (const float2*)(scr + S_M);
+  auto issue = [&](int b, float4 (&x)[NLD], bool (&ok)[NLD]) {
+    const int base = b * SROWS;
+    int src[NLD];
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int k = t + NTHREADS * i, row = base + (k >> 4);
+      src[i] = -1;
+      if (b < nbat && k < SROWS * 16 && row < totl) {
+        const int id = nbl[row];
+        src[i] = MD_BOK(id < gi.n, 4) ? (table ? ldc(deg + id) : id) : -1;
+        if (!MD_BOK(src[i] < gi.n, 5)) src[i] = -1;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      ok[i] = src[i] >= 0;
+      if (ok[i]) x[i] = ldc4(hp, src[i] * 256 + ((t + NTHREADS * i) & 15) * 16);
+    }
+  };
+  auto consume = [&](int b, const float4 (&x)[NLD], const bool (&ok)[NLD]) {
+    const int base = b * SROWS;
+#pragma unroll
+    for (int i = 0; i < NLD; ++i)
+      if (ok[i]) stg[t + NTHREADS * i] = x[i];
+    __syncthreads();
+    const int lo = max(myoff, base), hi = min(myoff + mycnt, base + SROWS);
+    int k = lo;
+    for (; k + 8 <= hi; k += 8) {
+      float2 y[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y[j] = stg2[(k + j - base) * 32 + q];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        acc.x = acc.x + y[j].x;
+        acc.y = acc.y + y[j].y;
+      }
+    }
+    for (; k < hi; ++k) {
+      const float2 y = stg2[(k - base) * 32 + q];
+      acc.x = acc.x + y.x;
+      acc.y = acc.y + y.y;
+    }
+    __syncthreads();
+  };
+  float4 xa[NLD], xb[NLD];
+  bool oka[NLD], okb[NLD];
+  if (nbat > 0) issue(0, xa, oka);
+  for (int b = 0; b < nbat; b += 2) {
+    issue(b + 1, xb, okb);
+    consume(b, xa, oka);
+    if (b + 1 >= nbat) break;
+    issue(b + 2, xa, oka);
+    consume(b + 1, xb, okb);
+  }
+  float* atp = scr + S_P + l * 64 * LDT;
+  float* atx = scr + S_X + l * 64 * LDT;
+  const int c = 2 * q;
+  atp[(c + 0) * LDT + r] = acc.x;
+  atp[(c + 1) * LDT + r] = acc.y;
+  atx[(c + 0) * LDT + r] = own.x;
+  atx[(c + 1) * LDT + r] = own.y;
+}
+
+// Node update of layer L: waves 0-3 P.P1 (column block w), waves 4-7 X.P2, then waves 0-3
+// relu(M.P3).  Each output's k-chain is update_tile's.
+__device__ __noinline__ void update_tile_split(const float* wi, float* scr, int L) {
+  const int w = wave_id(), cb = w & 3, lane = lane_id();
+  const int ar = lane & 15, ak = lane >> 4;
+  const bool second = w >= 4;
+  const float* at_in = scr + (second ? S_X : S_P) + L * 64 * LDT;
+  float* atm = scr + S_M + L * 128 * LDT;
+  const float* wsrc = wi + (second ? W_IP2 : W_IP1) + cb * 16 * 64;
+  const float* p3 = wi + W_IP3 + cb * 32 * 64;
+  float xa[16], wa[16], wc[32];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    xa[s] = at_in[(4 * s + ak) * LDT + ar];
+    wa[s] = wsrc[s * 64 + lane];
+  }
+  if (!second) {
+#pragma unroll
+    for (int s = 0; s < 32; ++s) wc[s] = p3[s * 64 + lane];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  f4 a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 16; ++s) a1 = mfma16(xa[s], wa[s], a1);
+  const int col = 16 * cb + ar;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) atm[((second ? 64 : 0) + col) * LDT + 4 * ak + r] = a1[r];
+  __syncthreads();
+  if (!second) {
+    float xm[32];
+#pragma unroll
+    for (int s = 0; s < 32; ++s) xm[s] = atm[(4 * s + ak) * LDT + ar];
+    __builtin_amdgcn_sched_barrier(0);
+    f4 a3 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 32; ++s) a3 = mfma16(xm[s], wc[s], a3);
+    float* ate = scr + S_E + L * 64 * LDT;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ate[col * LDT + 4 * ak + r] = fmaxf(a3[r], 0.f);
+  }
+}
+
+// Row-normalise layer L of the transposed tile at `at` in place (normalize_tile's order).
+__device__ __noinline__ void normalize_tile_split(float* at, float* scr, int L) {
+  float* red = scr + S_RED;
+  const int t = threadIdx.x;
+  float* a = at + L * 64 * LDT;
+  if (t < 128) {
+    const int row = t >> 3, j = t & 7;
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float v = a[(8 * i + j) * LDT + row];
+      acc = fmaf(v, v, acc);
+    }
+    red[(L * 16 + row) * 8 + j] = acc;
+  }
+  __syncthreads();
+  const int w = wave_id(), lane = lane_id();
+  if (w < 4) {
+    const int col = 16 * w + (lane & 15), rq = lane >> 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * rq + r;
+      const float den = fmaxf(sqrtf(sumsq8_finish(red + (L * 16 + row) * 8)), 1e-12f);
+      a[col * LDT + row] = a[col * LDT + row] / den;
+    }
+  }
+}
+
 // Node update for one tile: H' = relu([P.P1 | X.P2] . P3) into S_E (normalised separately).
 __device__ __noinline__ void update_tile(const float* wi, float* scr) {
   const int w = wave_id(), l = w >> 2, cb = w & 3, lane = lane_id();
@@ -1449,8 +1624,11 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
     // the same round trip; they are this workgroup's tile whenever there are enough workgroups)
     const bool spec = ded && ng == 1 && !is_env && !is_head && threadIdx.x < TILE;
     float4 spec_e = make_float4(0.f, 0.f, 0.f, 0.f);
+    // layer split (below) is certain for one graph whose every tile fits two workgroups
+    const bool spec_split = 2 * ((spec_gi.n + TILE - 1) / TILE) <= ntw;
+    const int spec_tile = spec_split ? ((int)blockIdx.x - twg0) >> 1 : (int)blockIdx.x - twg0;
     if (spec) {
-      const int r = ((int)blockIdx.x - twg0) * TILE + threadIdx.x;
+      const int r = spec_tile * TILE + threadIdx.x;
       spec_e = ldc4((const float*)(p.live + 4 * (size_t)spec_gi.node_off), min(r, spec_gi.n - 1) * 16);
     }
     bool waiting = false;
@@ -1479,7 +1657,18 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
     const int per = (ttot + ntw - 1) / ntw;
     const int tb = (int)blockIdx.x - twg0;
     const bool tiles = !is_env && !is_head;
-    const int t0 = tiles ? min(ttot, tb * per) : 0, t1 = tiles ? min(ttot, t0 + per) : 0;
+    // Layer split (dedicated mode, two tile workgroups per tile): workgroup (tile, L) runs layer
+    // L of iterations 1 and 2; iteration 3 (attention mixes the layers) runs on L = 0 alone.
+    const bool split = ded && 2 * ttot <= ntw;
+    const int L = split ? (tb & 1) : 0;
+    int t0, t1;
+    if (split) {
+      t0 = tiles ? min(ttot, tb >> 1) : 0;
+      t1 = tiles ? min(ttot, t0 + 1) : 0;
+    } else {
+      t0 = tiles ? min(ttot, tb * per) : 0;
+      t1 = tiles ? min(ttot, t0 + per) : 0;
+    }
     bool nb_ok = false, failed = false;
     // hand-off tag of this step's graph head (unique per launch and step)
     const unsigned long long htag = ded ? (unsigned long long)(pstep + 1) : 0ull;
@@ -1488,7 +1677,9 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
       MD_PROF(10 + it);
       if (is_head && it >= 2) head_iteration(p, lds, scr, p.glist[blockIdx.x - p.n_env], it, htag);
       int cur = ded ? 0x7fffffff : -1;  // graph-list index whose virtual node / graph head is loaded
-      for (int t = t0; t < t1; ++t) {
+      const bool sit = split && it < 3;  // this iteration runs one layer per workgroup
+      const int t1i = (split && it == 3 && L == 1) ? t0 : t1;
+      for (int t = t0; t < t1i; ++t) {
         const int gl = tile_graph(pref, ng, t);
         const int g = p.glist[gl];
         const GraphInfo gi = p.ginfo[g];
@@ -1524,7 +1715,7 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
             const int r = j * TILE + threadIdx.x;
             int nl;
             float4 e;
-            if (spec && it == 1 && t == tb) {
+            if (spec && it == 1 && t == spec_tile) {
               nl = ((const int*)(lds + L_MISC))[62];
               e = spec_e;
             } else {
@@ -1557,20 +1748,26 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
           if (it == 1 || t1 - t0 > 1 || !ded) nb_ok = !(p.variant & 16) && build_nb_lists(p, gi, rows, scr, ts);
           TSTAMP(55);
         }
-        if (nb_ok) gather_tile2(p, gi, it, rows, scr);
-        else gather_tile(p, gi, it, rows, scr);
+        if (nb_ok) {
+          if (sit) gather_tile2s(p, gi, it, rows, scr, L);
+          else gather_tile2(p, gi, it, rows, scr);
+        } else {
+          gather_tile(p, gi, it, rows, scr);
+        }
         __syncthreads();
         if (tg0 != 0) atomicMax(p.prof + (size_t)pstep * PROF_SLOTS + 46, wall_clock64() - tg0);  // longest gather (it 2)
         MD_PROF_T(23 + 3 * (it - 1));
-        update_tile(lds + L_W, scr);
+        if (sit) update_tile_split(lds + L_W, scr, L);
+        else update_tile(lds + L_W, scr);
         __syncthreads();
         if (it == 1) MD_PROF_T(36);
-        normalize_tile(scr + S_E, scr);
+        if (sit) normalize_tile_split(scr + S_E, scr, L);
+        else normalize_tile(scr + S_E, scr);
         __syncthreads();
         if (it == 1) MD_PROF_T(37);
-        if (threadIdx.x < 128) {
+        if (threadIdx.x < (sit ? 64 : 128)) {
           // tile partial sums of the virtual node (rows in ascending compact order from 0)
-          const int l = threadIdx.x >> 6, c = threadIdx.x & 63;
+          const int l = sit ? L : (int)threadIdx.x >> 6, c = threadIdx.x & 63;
           const float* ate = scr + S_E + l * 64 * LDT + c * LDT;
           const float* atx = scr + S_X + l * 64 * LDT + c * LDT;
           float s_new = 0.f, s_old = 0.f;
@@ -1589,12 +1786,12 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
         }
         if (it < 3) {
           // new embeddings to HBM as 16-byte sc1 stores: 16 lanes per row, 4 rows per wave
-          const int w = wave_id(), l = w >> 2, lane = lane_id();
+          const int w = wave_id(), l = sit ? L : w >> 2, lane = lane_id();
           float* hb = p.H[l][(it - 1) & 1] + (size_t)gi.node_off * EMB;
           const int r = 4 * (w & 3) + (lane >> 4), q4 = lane & 15;
           const int v = rows[r];
           const float* e = scr + S_E + l * 64 * LDT + 4 * q4 * LDT + r;
-          if (v >= 0) stc4(hb, v * 256 + q4 * 16, make_float4(e[0], e[LDT], e[2 * LDT], e[3 * LDT]));
+          if (v >= 0 && !(sit && w >= 4)) stc4(hb, v * 256 + q4 * 16, make_float4(e[0], e[LDT], e[2 * LDT], e[3 * LDT]));
         }
         __syncthreads();
         MD_PROF_T(24 + 3 * (it - 1));
