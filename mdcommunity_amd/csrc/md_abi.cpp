@@ -104,6 +104,7 @@ struct md_ctx {
   DevBuf<uint8_t> estate[2], calive[2], covered;
   DevBuf<int> deg[2], live, gscr, pend, tr_action, tr_rank, tr_stat, glist, ctl;
   DevBuf<float> H[2][2], h0tab[2], q, spart, apart, ybuf, hbuf, tr_q, node_w;
+  DevBuf<unsigned long long> xbuf;  // layer-split hand-off of iteration-3 embeddings
   unsigned launch_seq = 0;
   // host selection hand-shake
   int host_mode = 1;
@@ -139,7 +140,7 @@ struct md_ctx {
     }
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
     tr_stat.release(); glist.release(); ctl.release(); q.release(); spart.release();
-    apart.release(); ybuf.release(); hbuf.release(); tr_q.release(); node_w.release();
+    apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); tr_q.release(); node_w.release();
     h_req.release(); h_ans.release(); h_nact.release(); h_act.release(); h_q.release(); h_chk.release();
     ng = 0;
     hinfo.clear();
@@ -195,6 +196,7 @@ Params make_params(md_ctx* c) {
   p.apart = c->apart.p;
   p.ybuf = c->ybuf.p;
   p.hbuf = c->hbuf.p;
+  p.xbuf = c->xbuf.p;
   p.pend = c->pend.p;
   p.tr_action = c->tr_action.p;
   p.tr_rank = c->tr_rank.p;
@@ -334,6 +336,8 @@ md_status launch_chunk(md_ctx* c, const int* gl, int ngl, int run_mode, int host
   // graph-head hand-off granules carry the step as their tag: stale tags from earlier launches
   // must not match
   if (n_env > 0) HIPCHK(c, hipMemsetAsync(c->hbuf.p, 0, sizeof(float) * c->hbuf.n, c->stream));
+  if (n_env > 0)  // the slots a launch of this grid can use (split tiles <= tile workgroups / 2)
+    HIPCHK(c, hipMemsetAsync(c->xbuf.p, 0, sizeof(unsigned long long) * 2048 * std::min(XB_SLOTS, grid / 2 + 1), c->stream));
   Params p = make_params(c);
   p.nglist = ngl;
   p.n_env = n_env;
@@ -657,6 +661,7 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->apart.alloc(tt * 4));
   HIPCHK(c, c->ybuf.alloc((size_t)n_graphs * 128));
   HIPCHK(c, c->hbuf.alloc((size_t)n_graphs * 144 * 2));
+  HIPCHK(c, c->xbuf.alloc((size_t)XB_SLOTS * 2048));  // split tiles of a launch <= CUs / 2 <= XB_SLOTS
   HIPCHK(c, c->h_req.alloc((size_t)n_graphs));
   HIPCHK(c, c->h_ans.alloc((size_t)n_graphs));
   HIPCHK(c, c->h_nact.alloc((size_t)n_graphs));

@@ -15,7 +15,8 @@ constexpr int BP_ITERS = 3;      // max_bp_iter, :62
 constexpr int NTHREADS = 512;    // 8 waves: waves 0-3 work on layer 0, waves 4-7 on layer 1
 constexpr int TILE = 16;         // node rows per MFMA tile (v_mfma_f32_16x16x4_f32)
 constexpr int G_CAP = 512;       // graphs per kernel launch (the host chunks larger batches)
-constexpr int PROF_SLOTS = 64;   // MD_PROF_SLOTS (include/mdroll.h)
+constexpr int PROF_SLOTS = 64;
+constexpr int XB_SLOTS = 256;    // layer-split tiles per launch with an iteration-3 hand-off slot   // MD_PROF_SLOTS (include/mdroll.h)
 
 // Offsets (floats) of each tensor in the packed weight blob (see include/mdroll.h).
 enum WOff : int {
@@ -93,6 +94,7 @@ struct Params {
   float* apart;                    // per tile: arg-max partial {max, second, idx, count}
   float* ybuf;                     // per graph: [2][64] virtual-node embedding after iteration 2
   float* hbuf;                     // per graph: [144][2] graph-head hand-off granules {value, step tag}
+  unsigned long long* xbuf;        // layer split: per launch tile slot [2 layers][1024] E-row granules {tag, value}
   int* pend;                       // per node slot: host-queued actions
   int* tr_action;                  // per node slot: removal order
   int* tr_rank;                    // per node slot: LMCC after each removal

@@ -1289,6 +1289,42 @@ __device__ __forceinline__ void head_receive(KParams& p, float* lds, int g, unsi
   __syncthreads();
 }
 
+// Layer split, iteration 3: workgroup (tile, 1) hands its normalised layer-1 rows (S_E layer 1,
+// 64 x 16) to workgroup (tile, 0) as 1024 data-tagged 8-byte granules in tile slot `slot`
+// (tag = step + 1; the host zeroes the slots before each launch); the receiver polls each
+// granule until its tag matches (one round trip, no flag), as the graph-head hand-off.
+__device__ __forceinline__ void split_publish(KParams& p, const float* scr, int slot, unsigned long long tag) {
+  g_u64* dst = (g_u64*)(p.xbuf + (size_t)slot * 2048 + 1024);
+  const float* e = scr + S_E + 64 * LDT;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = threadIdx.x + NTHREADS * h, c = k >> 4, r = k & 15;
+    __hip_atomic_store(dst + k, (tag << 32) | (unsigned)__float_as_uint(e[c * LDT + r]), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+__device__ __forceinline__ void split_receive(KParams& p, float* scr, int slot, unsigned long long tag) {
+  const g_u64* src = (const g_u64*)(p.xbuf + (size_t)slot * 2048 + 1024);
+  float* e = scr + S_E + 64 * LDT;
+  const unsigned long long t0 = wall_clock64();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = threadIdx.x + NTHREADS * h, c = k >> 4, r = k & 15;
+    unsigned long long gr;
+    while (((gr = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != tag) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > BARRIER_TIMEOUT_TICKS ||
+          (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR)) {
+        raise_err(p, ERR_TIMEOUT);
+        gr = 0;
+        break;
+      }
+    }
+    e[c * LDT + r] = __uint_as_float((unsigned)gr);
+  }
+  __syncthreads();
+}
+
 // One iteration of the graph-head workgroup (dedicated mode) for graph g: it == 2 builds
 // Y1, Y2 from the S0 / S1 tile partials of iteration 1; it == 3 builds Y3 from S2, runs the
 // graph head and publishes it.  Same arithmetic as the shared-mode path in the tile loop.
@@ -1659,7 +1695,7 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
     const bool tiles = !is_env && !is_head;
     // Layer split (dedicated mode, two tile workgroups per tile): workgroup (tile, L) runs layer
     // L of iterations 1 and 2; iteration 3 (attention mixes the layers) runs on L = 0 alone.
-    const bool split = ded && 2 * ttot <= ntw;
+    const bool split = ded && 2 * ttot <= ntw && ttot <= XB_SLOTS;
     const int L = split ? (tb & 1) : 0;
     int t0, t1;
     if (split) {
@@ -1677,9 +1713,8 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
       MD_PROF(10 + it);
       if (is_head && it >= 2) head_iteration(p, lds, scr, p.glist[blockIdx.x - p.n_env], it, htag);
       int cur = ded ? 0x7fffffff : -1;  // graph-list index whose virtual node / graph head is loaded
-      const bool sit = split && it < 3;  // this iteration runs one layer per workgroup
-      const int t1i = (split && it == 3 && L == 1) ? t0 : t1;
-      for (int t = t0; t < t1i; ++t) {
+      const bool sit = split;  // this iteration runs one layer per workgroup
+      for (int t = t0; t < t1; ++t) {
         const int gl = tile_graph(pref, ng, t);
         const int g = p.glist[gl];
         const GraphInfo gi = p.ginfo[g];
@@ -1795,6 +1830,14 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
         }
         __syncthreads();
         MD_PROF_T(24 + 3 * (it - 1));
+        if (it == 3 && sit) {
+          // the layer-1 rows go to the layer-0 workgroup, which runs the attention and Q head
+          if (L == 1) {
+            split_publish(p, scr, t, htag);
+            continue;
+          }
+          split_receive(p, scr, t, htag);
+        }
         if (it == 3) {
           unsigned long long* ts = nullptr;
           if (p.prof != nullptr && (int)blockIdx.x == twg0 && t == t0 && pstep < p.prof_cap)
