@@ -627,9 +627,11 @@ __device__ __noinline__ void gather_tile(KParams&, const GraphInfo gi, int it, c
 // rawc[2][16] (CSR extent), tot[2].  Returns false when a layer has more than NB_CAP alive
 // entries (the tile then uses gather_tile).
 __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const int* rows, float* scr,
-                                            unsigned long long* ts) {
+                                            unsigned long long* ts, int L) {
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
-  const int w = wave_id(), l = w >> 2, lane = lane_id(), t = threadIdx.x & 255;
+  // L < 0: both layers (waves 0-3 layer 0, 4-7 layer 1); L = 0 / 1: that layer, all waves
+  const int NT = L < 0 ? 256 : NTHREADS;
+  const int w = wave_id(), l = L < 0 ? w >> 2 : L, lane = lane_id(), t = L < 0 ? threadIdx.x & 255 : threadIdx.x;
   lds_i32* hdr = (lds_i32*)(int*)(scr + S_NBH);
   lds_i32* tmp = (lds_i32*)(int*)(scr + S_RED);  // [2][4] wave totals
   lds_u16* nbl = (lds_u16*)(uint16_t*)(scr + S_NBL) + l * NB_CAP;
@@ -655,7 +657,7 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
   __syncthreads();
   TSTAMP(61);
   const int T = pre[16];
-  const int chunk = (T + 255) >> 8;
+  const int chunk = (T + NT - 1) / NT;
   const int i0 = min(T, t * chunk), i1 = min(T, i0 + chunk);
   // my entries: alive flags and neighbour ids, the first four of them with all their loads in
   // flight together and kept in registers for the second pass
@@ -704,11 +706,20 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
   __syncthreads();
   TSTAMP(62);
   int base = 0, tot = 0;
+  if (L < 0) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int x = tmp[l * 4 + k];
-    if (k < (w & 3)) base += x;
-    tot += x;
+    for (int k = 0; k < 4; ++k) {
+      const int x = tmp[l * 4 + k];
+      if (k < (w & 3)) base += x;
+      tot += x;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < NTHREADS / 64; ++k) {
+      const int x = tmp[k];
+      if (k < w) base += x;
+      tot += x;
+    }
   }
   int o = base + incl - keep;
   r = r0;
@@ -1780,7 +1791,8 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
           if (p.prof != nullptr && it == 1 && (int)blockIdx.x == twg0 && t == t0 && pstep < p.prof_cap)
             ts = p.prof + (size_t)pstep * PROF_SLOTS;
           TSTAMP(54);
-          if (it == 1 || t1 - t0 > 1 || !ded) nb_ok = !(p.variant & 16) && build_nb_lists(p, gi, rows, scr, ts);
+          if (it == 1 || t1 - t0 > 1 || !ded)
+            nb_ok = !(p.variant & 16) && build_nb_lists(p, gi, rows, scr, ts, sit ? L : -1);
           TSTAMP(55);
         }
         if (nb_ok) {
