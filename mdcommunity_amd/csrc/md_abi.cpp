@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -104,7 +105,9 @@ struct md_ctx {
   DevBuf<uint8_t> estate[2], calive[2], covered;
   DevBuf<int> deg[2], live, gscr, pend, tr_action, tr_rank, tr_stat, glist, ctl;
   DevBuf<float> H[2][2], h0tab[2], q, spart, apart, ybuf, hbuf, tr_q, node_w;
-  DevBuf<unsigned long long> xbuf;  // layer-split hand-off of iteration-3 embeddings
+  DevBuf<unsigned long long> xbuf;
+  DevBuf<int> nbc;  // neighbour-list cache slots (tiles of the largest launch)
+  int nbc_slots = 0;  // layer-split hand-off of iteration-3 embeddings
   unsigned launch_seq = 0;
   // host selection hand-shake
   int host_mode = 1;
@@ -140,7 +143,7 @@ struct md_ctx {
     }
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
     tr_stat.release(); glist.release(); ctl.release(); q.release(); spart.release();
-    apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); tr_q.release(); node_w.release();
+    apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); nbc.release(); tr_q.release(); node_w.release();
     h_req.release(); h_ans.release(); h_nact.release(); h_act.release(); h_q.release(); h_chk.release();
     ng = 0;
     hinfo.clear();
@@ -197,6 +200,8 @@ Params make_params(md_ctx* c) {
   p.ybuf = c->ybuf.p;
   p.hbuf = c->hbuf.p;
   p.xbuf = c->xbuf.p;
+  p.nbc = c->nbc.p;
+  p.nbc_slots = c->nbc_slots;
   p.pend = c->pend.p;
   p.tr_action = c->tr_action.p;
   p.tr_rank = c->tr_rank.p;
@@ -661,7 +666,17 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->apart.alloc(tt * 4));
   HIPCHK(c, c->ybuf.alloc((size_t)n_graphs * 128));
   HIPCHK(c, c->hbuf.alloc((size_t)n_graphs * 144 * 2));
-  HIPCHK(c, c->xbuf.alloc((size_t)XB_SLOTS * 2048));  // split tiles of a launch <= CUs / 2 <= XB_SLOTS
+  HIPCHK(c, c->xbuf.alloc((size_t)XB_SLOTS * 2048));
+  {
+    // cache slots: the tiles of the largest possible launch (the G_CAP graphs with most tiles)
+    std::vector<long> nt(n_graphs);
+    for (int g = 0; g < n_graphs; ++g) nt[g] = (n_nodes[g] + TILE - 1) / TILE;
+    std::sort(nt.begin(), nt.end(), std::greater<long>());
+    long slots = 0;
+    for (int g = 0; g < std::min(n_graphs, G_CAP); ++g) slots += nt[g];
+    c->nbc_slots = (int)slots;
+    HIPCHK(c, c->nbc.alloc((size_t)std::max<long>(1, slots) * NBC_INTS));
+  }  // split tiles of a launch <= CUs / 2 <= XB_SLOTS
   HIPCHK(c, c->h_req.alloc((size_t)n_graphs));
   HIPCHK(c, c->h_ans.alloc((size_t)n_graphs));
   HIPCHK(c, c->h_nact.alloc((size_t)n_graphs));

@@ -16,6 +16,11 @@ constexpr int NTHREADS = 512;    // 8 waves: waves 0-3 work on layer 0, waves 4-
 constexpr int TILE = 16;         // node rows per MFMA tile (v_mfma_f32_16x16x4_f32)
 constexpr int G_CAP = 512;       // graphs per kernel launch (the host chunks larger batches)
 constexpr int PROF_SLOTS = 64;
+constexpr int NB_CAP_ENTRIES = 2052;   // alive neighbour entries per layer kept for a tile (NB_CAP)
+// neighbour-list cache slot: header (off[2][16], cnt[2][16], tot[2], ok) then per layer the u16
+// entries packed two per int
+constexpr int NBC_HDR = 80, NBC_LWORDS = NB_CAP_ENTRIES / 2, NBC_INTS = 2176;
+static_assert(NBC_HDR + 2 * NBC_LWORDS <= NBC_INTS, "cache slot");
 constexpr int XB_SLOTS = 256;    // layer-split tiles per launch with an iteration-3 hand-off slot   // MD_PROF_SLOTS (include/mdroll.h)
 
 // Offsets (floats) of each tensor in the packed weight blob (see include/mdroll.h).
@@ -94,6 +99,9 @@ struct Params {
   float* apart;                    // per tile: arg-max partial {max, second, idx, count}
   float* ybuf;                     // per graph: [2][64] virtual-node embedding after iteration 2
   float* hbuf;                     // per graph: [144][2] graph-head hand-off granules {value, step tag}
+  int* nbc;                        // per launch tile slot: its alive neighbour lists (NBC_INTS ints), built at
+                                   //   iteration 1, reloaded by iterations 2-3 of multi-tile workgroups
+  int nbc_slots;
   unsigned long long* xbuf;        // layer split: per launch tile slot [2 layers][1024] E-row granules {tag, value}
   int* pend;                       // per node slot: host-queued actions
   int* tr_action;                  // per node slot: removal order

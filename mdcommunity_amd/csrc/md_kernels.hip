@@ -70,7 +70,7 @@ constexpr int S_YM = S_YP + 1024;           // [2][128]
 // never gathers, and shared-mode tile workgroups rebuild the lists after each chain.
 constexpr int S_NBH = S_YP;                 // neighbour-list header (ints, see build_nb_lists)
 constexpr int S_NBL = S_NBH + 172;          // [2][NB_CAP] u16 alive neighbour ids, CSR order
-constexpr int NB_CAP = 2052;                // alive neighbour entries per layer kept for a tile
+constexpr int NB_CAP = NB_CAP_ENTRIES;      // alive neighbour entries per layer kept for a tile
 constexpr int S_END = S_NBL + NB_CAP;
 constexpr int STG_ROWS = 68;                // neighbour rows per layer staged per batch ([S_M, S_HID))
 constexpr int L_TOTAL = L_SCR + S_END;      // floats of dynamic LDS per workgroup
@@ -860,6 +860,26 @@ __device__ __noinline__ void gather_tile2(KParams&, const GraphInfo gi, int it, 
   atx[(c + 1) * LDT + r] = own.y;
   atx[(c + 2) * LDT + r] = own.z;
   atx[(c + 3) * LDT + r] = own.w;
+}
+
+// Iteration 1 of a workgroup with several tiles: its tiles' alive neighbour lists and
+// headers go to the tile's cache slot (agent-scope stores), so iterations 2 and 3 reload them
+// in one round trip instead of rebuilding them from the CSR flags.
+__device__ __noinline__ void nbc_store(KParams&, int slot, const float* scr, bool ok) {
+  KParams& p = kp();
+  int* dst = p.nbc + (size_t)slot * NBC_INTS;
+  const lds_i32* hdr = (const lds_i32*)(const int*)(scr + S_NBH);
+  const lds_i32* words = (const lds_i32*)(const int*)(scr + S_NBL);
+  const int t = threadIdx.x;
+  if (t < 64) stc(dst + t, hdr[t]);
+  else if (t < 66) stc(dst + t, hdr[128 + t - 64]);
+  else if (t == 66) stc(dst + t, ok ? 1 : 0);
+  if (!ok) return;
+#pragma unroll
+  for (int l = 0; l < 2; ++l) {
+    const int nw = (hdr[128 + l] + 1) >> 1;
+    for (int i = t; i < nw; i += NTHREADS) stc(dst + NBC_HDR + l * NBC_LWORDS + i, words[l * NBC_LWORDS + i]);
+  }
 }
 
 // ------------------------------------------------------------------ layer-split tile pieces
@@ -1756,6 +1776,17 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
         // rows of the tile and their CSR ranges (unchanged during a step: a single-tile
         // workgroup of dedicated mode keeps them; in shared mode the virtual-node chain reuses
         // that LDS); one 16-byte live-list entry per row
+        // several tiles per workgroup: iteration 1 caches the tile's neighbour lists in HBM
+        // (slot t), iterations 2-3 reload them with the rows (first 256 words per layer
+        // speculatively, the rest only when a layer has more than 512 entries)
+        const bool multi = (t1 - t0 > 1 || !ded) && t < p.nbc_slots && !(p.variant & 16);
+        const bool cached = multi && it > 1;
+        int cw = 0, ch = 0;
+        if (cached) {
+          const int* src = p.nbc + (size_t)t * NBC_INTS;
+          cw = ldc(src + NBC_HDR + (threadIdx.x >> 8) * NBC_LWORDS + (threadIdx.x & 255));
+          if (threadIdx.x < 67) ch = ldc(src + threadIdx.x);
+        }
         if (it == 1 || t1 - t0 > 1 || !ded) {
           if (threadIdx.x < TILE) {
             const int r = j * TILE + threadIdx.x;
@@ -1778,6 +1809,13 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
             hdr[96 + 16 + threadIdx.x] = ok ? (int)(c >> 16) : 0;
           }
         }
+        if (cached) {
+          lds_i32* hdr = (lds_i32*)(int*)(scr + S_NBH);
+          ((lds_i32*)(int*)(scr + S_NBL))[(threadIdx.x >> 8) * NBC_LWORDS + (threadIdx.x & 255)] = cw;
+          if (threadIdx.x < 64) hdr[threadIdx.x] = ch;
+          else if (threadIdx.x < 66) hdr[128 + threadIdx.x - 64] = ch;
+          else if (threadIdx.x == 66) ((int*)(lds + L_MISC))[59] = ch;
+        }
         __syncthreads();
         // alive neighbour lists: built at iteration 1, kept for 2 and 3 when this workgroup
         // has a single tile (its LDS copy is intact)
@@ -1791,8 +1829,21 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
           if (p.prof != nullptr && it == 1 && (int)blockIdx.x == twg0 && t == t0 && pstep < p.prof_cap)
             ts = p.prof + (size_t)pstep * PROF_SLOTS;
           TSTAMP(54);
-          if (it == 1 || t1 - t0 > 1 || !ded)
+          if (cached) {
+            nb_ok = ((const int*)(lds + L_MISC))[59] != 0;
+            const lds_i32* hdr = (const lds_i32*)(const int*)(scr + S_NBH);
+            const int nw0 = (hdr[128] + 1) >> 1, nw1 = (hdr[129] + 1) >> 1;
+            if (nb_ok && (nw0 > 256 || nw1 > 256)) {
+              const int* src = p.nbc + (size_t)t * NBC_INTS + NBC_HDR;
+              lds_i32* words = (lds_i32*)(int*)(scr + S_NBL);
+              for (int i = 256 + (int)threadIdx.x; i < nw0; i += NTHREADS) words[i] = ldc(src + i);
+              for (int i = 256 + (int)threadIdx.x; i < nw1; i += NTHREADS) words[NBC_LWORDS + i] = ldc(src + NBC_LWORDS + i);
+              __syncthreads();
+            }
+          } else if (it == 1 || t1 - t0 > 1 || !ded) {
             nb_ok = !(p.variant & 16) && build_nb_lists(p, gi, rows, scr, ts, sit ? L : -1);
+            if (multi) nbc_store(p, t, scr, nb_ok);
+          }
           TSTAMP(55);
         }
         if (nb_ok) {
