@@ -22,6 +22,7 @@ def prof(name, team):
         kms.append(eng.last_timing()[0])
     print(f"{name}: unprofiled rollout kernel ms: median {np.median(kms):.3f} min {np.min(kms):.3f} "
           f"-> {np.median(kms) / len(z['seq']) * 1000:.1f} us per removal", flush=True)
+    tr_n = eng.trace(0)["n_live"]
     eng.reset()
     eng.profile(512)
     t0 = time.time(); out = eng.rollout(); dt = time.time() - t0
@@ -42,9 +43,11 @@ def prof(name, team):
     stp = (full[:, 10] - full[:, 0]) / 100.0
     print("   sum of step times %.3f ms (kernel %.3f ms); first step %.1f us; top-5 steps %s us at %s" % (
         stp.sum() / 1000, ms, stp[0], np.round(np.sort(stp)[-5:], 1).tolist(), np.argsort(stp)[-5:].tolist()), flush=True)
-    for t in range(min(12, len(full))):
+    stp_ = (full[:, 10] - full[:, 0]) / 100.0
+    show = sorted(set(list(range(min(4, len(full)))) + np.argsort(stp_)[-8:].tolist()))
+    for t in show:
         acc_ = full[t, 16:23]
-        print("   step %2d: %s | rounds %d unite %.1f label %.1f prune %.1f" % (t, "  ".join(
+        print("   step %2d (n_live %d): %s | rounds %d unite %.1f label %.1f prune %.1f" % (t, tr_n[t] if t < len(tr_n) else -1, "  ".join(
             f"{s}={(full[t, b] - full[t, a]) / 100:.1f}" for s, a, b in seg), acc_[0], acc_[1] / 100, acc_[2] / 100, acc_[3] / 100), flush=True)
     tt = lambda a, b: np.median((full[:, b].astype(np.int64) - full[:, a].astype(np.int64))) / 100.0
     print("   tile wg: p1 gather %.1f upd %.1f end %.1f | p2 gather %.1f upd %.1f end %.1f | p3 gather %.1f upd %.1f attn %.1f us" % (
