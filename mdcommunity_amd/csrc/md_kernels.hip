@@ -638,7 +638,6 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
   const int* adj = p.adj[l] + gi.coff[l];
   const uint8_t* ca = p.calive[l] + gi.coff[l];
   // rows' CSR begin / extent are in hdr[64 + 16 l + r] / hdr[96 + 16 l + r] (from the live list)
-  if (t < 16) hdr[32 + l * 16 + t] = 0;
   TSTAMP(60);
   // CSR-extent prefix per row in LDS (a per-thread array indexed at run time would live in
   // scratch memory)
@@ -722,37 +721,38 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
     }
   }
   int o = base + incl - keep;
+  // row offsets without atomics: the owner of a row's first CSR position writes the row's
+  // offset (= alive entries before it); rows starting at T get the total
+  int rs = r0;
+  while (rs > 0 && pre[rs - 1] == i0) --rs;
+  if (rs < 16 && pre[rs] < i0) ++rs;
   r = r0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int i = i0 + k;
     if (i < i1) {
-      while (pre[r + 1] <= i) ++r;
+      while (rs < 16 && pre[rs] == i) hdr[l * 16 + rs++] = o;
       if (fl[k]) {
         if (o < NB_CAP) nbl[o] = (uint16_t)nbv[k];
         ++o;
-        __hip_atomic_fetch_add(hdr + 32 + l * 16 + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
   }
   r = rt;
   for (int i = i0 + 4; i < i1; ++i) {
+    while (rs < 16 && pre[rs] == i) hdr[l * 16 + rs++] = o;
     while (pre[r + 1] <= i) ++r;
     const int pos = hdr[64 + l * 16 + r] + (i - pre[r]);
     if (ldc(ca + pos)) {
       if (o < NB_CAP) nbl[o] = (uint16_t)adj[pos];
       ++o;
-      __hip_atomic_fetch_add(hdr + 32 + l * 16 + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
+  if (t < 16 && pre[t] == T) hdr[l * 16 + t] = tot;
+  if (t == 0) hdr[128 + l] = tot;
   __syncthreads();
   TSTAMP(63);
-  if (t < 16) {
-    int off = 0;
-    for (int k = 0; k < t; ++k) off += hdr[32 + l * 16 + k];
-    hdr[l * 16 + t] = off;
-    if (t == 0) hdr[128 + l] = tot;
-  }
+  if (t < 16) hdr[32 + l * 16 + t] = (t < 15 ? hdr[l * 16 + t + 1] : tot) - hdr[l * 16 + t];
   const int over = __syncthreads_or(tot > NB_CAP);
   return !over;
 }
