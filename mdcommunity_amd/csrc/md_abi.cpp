@@ -107,7 +107,9 @@ struct md_ctx {
   DevBuf<float> H[2][2], h0tab[2], q, spart, apart, ybuf, hbuf, tr_q, node_w;
   DevBuf<unsigned long long> xbuf;
   DevBuf<int> nbc;  // neighbour-list cache slots (tiles of the largest launch)
-  int nbc_slots = 0;  // layer-split hand-off of iteration-3 embeddings
+  int nbc_slots = 0, nbc_gstride = 0;
+  DevBuf<unsigned long long> qslot;  // queue-mode work items
+  DevBuf<int> qg;                    // queue-mode per-graph stage counters  // layer-split hand-off of iteration-3 embeddings
   unsigned launch_seq = 0;
   // host selection hand-shake
   int host_mode = 1;
@@ -143,7 +145,7 @@ struct md_ctx {
     }
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
     tr_stat.release(); glist.release(); ctl.release(); q.release(); spart.release();
-    apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); nbc.release(); tr_q.release(); node_w.release();
+    apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); nbc.release(); qslot.release(); qg.release(); tr_q.release(); node_w.release();
     h_req.release(); h_ans.release(); h_nact.release(); h_act.release(); h_q.release(); h_chk.release();
     ng = 0;
     hinfo.clear();
@@ -171,7 +173,7 @@ md_status fail(md_ctx* c, md_status s, const char* fmt, ...) {
   } while (0)
 
 // Control block layout (ints): [0] barrier counter, [1] error word (zeroed before each launch).
-constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_WORDS = 4;
+constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_Q = 2, CTL_WORDS = 8;
 
 Params make_params(md_ctx* c) {
   Params p{};
@@ -212,6 +214,10 @@ Params make_params(md_ctx* c) {
   p.h0g_dm = c->h0g.p ? c->h0g_dm : 0;
   p.bar = (unsigned*)(c->ctl.p + CTL_BAR);
   p.err = c->ctl.p + CTL_ERR;
+  p.qctl = (unsigned*)(c->ctl.p + CTL_Q);
+  p.qslot = c->qslot.p;
+  p.qg = c->qg.p;
+  p.nbc_gstride = c->nbc_gstride;
   p.glist = c->glist.p;
   p.prof = c->prof_cap > 0 ? c->prof.p : nullptr;
   p.prof_cap = c->prof_cap;
@@ -335,7 +341,10 @@ void serve_request(md_ctx* c, Selector* sel, int g, unsigned tag, std::vector<do
 md_status launch_chunk(md_ctx* c, const int* gl, int ngl, int run_mode, int host_select, Selector* sel) {
   std::vector<int> v(gl, gl + ngl);
   const int n_env = env_workgroups(c, v);
-  const int grid = grid_size(c, v, n_env);
+  // batches of whole rollouts run through the device work queue (MD_VARIANT bit 32: the
+  // lock-step shared mode instead), one workgroup per CU
+  const bool qmode = run_mode == RUN_ROLLOUT && n_env == 0 && !(c->variant & 32);
+  const int grid = qmode ? c->cus : grid_size(c, v, n_env);
   HIPCHK(c, hipMemcpyAsync(c->glist.p, gl, sizeof(int) * ngl, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->ctl.p, 0, sizeof(int) * CTL_WORDS, c->stream));
   // graph-head hand-off granules carry the step as their tag: stale tags from earlier launches
@@ -343,7 +352,12 @@ md_status launch_chunk(md_ctx* c, const int* gl, int ngl, int run_mode, int host
   if (n_env > 0) HIPCHK(c, hipMemsetAsync(c->hbuf.p, 0, sizeof(float) * c->hbuf.n, c->stream));
   if (n_env > 0)  // the slots a launch of this grid can use (split tiles <= tile workgroups / 2)
     HIPCHK(c, hipMemsetAsync(c->xbuf.p, 0, sizeof(unsigned long long) * 2048 * std::min(XB_SLOTS, grid / 2 + 1), c->stream));
+  if (qmode) {
+    HIPCHK(c, hipMemsetAsync(c->qslot.p, 0, sizeof(unsigned long long) * c->qslot.n, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->qg.p, 0, sizeof(int) * c->qg.n, c->stream));
+  }
   Params p = make_params(c);
+  p.qmode = qmode ? 1 : 0;
   p.nglist = ngl;
   p.n_env = n_env;
   p.variant = c->variant;
@@ -669,12 +683,15 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->xbuf.alloc((size_t)XB_SLOTS * 2048));
   {
     // cache slots: the tiles of the largest possible launch (the G_CAP graphs with most tiles)
-    std::vector<long> nt(n_graphs);
-    for (int g = 0; g < n_graphs; ++g) nt[g] = (n_nodes[g] + TILE - 1) / TILE;
-    std::sort(nt.begin(), nt.end(), std::greater<long>());
-    long slots = 0;
-    for (int g = 0; g < std::min(n_graphs, G_CAP); ++g) slots += nt[g];
+    // (queue mode addresses slot = graph slot * max tiles + tile, the lock-step modes the
+    // launch's tile prefix index: both < min(graphs, G_CAP) * max tiles)
+    long maxt = 1;
+    for (int g = 0; g < n_graphs; ++g) maxt = std::max<long>(maxt, (n_nodes[g] + TILE - 1) / TILE);
+    const long slots = (long)std::min(n_graphs, G_CAP) * maxt;
     c->nbc_slots = (int)slots;
+    c->nbc_gstride = (int)maxt;
+    HIPCHK(c, c->qslot.alloc(Q_CAP));
+    HIPCHK(c, c->qg.alloc(2 * G_CAP));
     HIPCHK(c, c->nbc.alloc((size_t)std::max<long>(1, slots) * NBC_INTS));
   }  // split tiles of a launch <= CUs / 2 <= XB_SLOTS
   HIPCHK(c, c->h_req.alloc((size_t)n_graphs));

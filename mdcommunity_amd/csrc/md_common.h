@@ -21,7 +21,8 @@ constexpr int NB_CAP_ENTRIES = 2052;   // alive neighbour entries per layer kept
 // entries packed two per int
 constexpr int NBC_HDR = 80, NBC_LWORDS = NB_CAP_ENTRIES / 2, NBC_INTS = 2176;
 static_assert(NBC_HDR + 2 * NBC_LWORDS <= NBC_INTS, "cache slot");
-constexpr int XB_SLOTS = 256;    // layer-split tiles per launch with an iteration-3 hand-off slot   // MD_PROF_SLOTS (include/mdroll.h)
+constexpr int XB_SLOTS = 256;
+constexpr int Q_CAP = 1 << 18;   // queue-mode ring slots (items in flight << Q_CAP)    // layer-split tiles per launch with an iteration-3 hand-off slot   // MD_PROF_SLOTS (include/mdroll.h)
 
 // Offsets (floats) of each tensor in the packed weight blob (see include/mdroll.h).
 enum WOff : int {
@@ -102,6 +103,11 @@ struct Params {
   int* nbc;                        // per launch tile slot: its alive neighbour lists (NBC_INTS ints), built at
                                    //   iteration 1, reloaded by iterations 2-3 of multi-tile workgroups
   int nbc_slots;
+  int nbc_gstride;                 // queue mode: cache slot = graph slot * nbc_gstride + tile
+  int qmode;                       // 1: batch rollout through the device work queue (queue_loop)
+  unsigned* qctl;                  // queue mode: {head ticket, tail ticket, running graphs}
+  unsigned long long* qslot;       // queue mode: Q_CAP item slots {ticket + 1, item}
+  int* qg;                         // queue mode: per graph slot {tiles done in the stage, tiles}
   unsigned long long* xbuf;        // layer split: per launch tile slot [2 layers][1024] E-row granules {tag, value}
   int* pend;                       // per node slot: host-queued actions
   int* tr_action;                  // per node slot: removal order

@@ -1625,6 +1625,289 @@ __device__ __forceinline__ int tile_graph(const int* pref, int ng, int t) {
   return lo;
 }
 
+// ------------------------------------------------------------------ queue mode (batches)
+// Rollouts of many graphs without lock-step grid barriers: every workgroup pops work items
+// from one device queue and pushes the items they enable, so one graph's environment step,
+// another's virtual node and the tiles of a third run at the same time, and a graph that
+// waits for a host answer or finished early holds nobody up.  Per graph and removal step:
+//   ENV  phase A (arg-max of the last Q, action, mutual-LMCC fixed point, features)
+//   -> TILE(1, j) for its tiles -> TILE(2, j) -> VN (virtual node Y1..Y3 + graph head,
+//   published as tagged granules) -> TILE(3, j) (attention, Q, arg-max partials) -> ENV.
+// The last tile of a stage (per-graph counter) pushes the next stage.  Items are 32-bit
+// {kind, iteration, graph slot, tile} in a ring of 8-byte slots tagged with their ticket + 1:
+// a consumer takes a ticket (atomic add) and polls its slot; a producer reserves tickets and
+// writes the slots after draining its data stores (the fence-free sc1 protocol of the grid
+// barrier).  Every item runs to completion without waiting on another item, so the queue
+// cannot deadlock; when the last graph stops, one EXIT item per workgroup is pushed.
+enum : unsigned { QK_ENV = 1, QK_TILE = 2, QK_VN = 3, QK_EXIT = 4 };
+enum : int { QC_HEAD = 0, QC_TAIL = 1, QC_REM = 2 };
+__device__ __forceinline__ unsigned q_item(unsigned kind, int it, int gl, int j) {
+  return kind | ((unsigned)it << 3) | ((unsigned)gl << 5) | ((unsigned)j << 15);
+}
+// Pushes n items f(0..n-1); every thread of the workgroup calls it.
+template <class F>
+__device__ __forceinline__ void q_push(KParams& p, int n, F&& f, int* bc) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's data stores are done
+  __syncthreads();
+  if (threadIdx.x == 0)
+    bc[0] = (int)__hip_atomic_fetch_add((g_u32*)(p.qctl + QC_TAIL), (unsigned)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const unsigned base = (unsigned)bc[0];
+  for (int i = threadIdx.x; i < n; i += NTHREADS) {
+    const unsigned tk = base + (unsigned)i;
+    const unsigned long long v = ((unsigned long long)(tk + 1u) << 32) | f(i);
+    __hip_atomic_store((g_u64*)(p.qslot + (tk & (Q_CAP - 1))), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ unsigned q_pop(KParams& p, int* bc) {
+  if (threadIdx.x == 0) {
+    // an error anywhere: stop taking work (the grid drains)
+    if (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR) {
+      bc[1] = (int)QK_EXIT;
+      goto done;
+    }
+    {
+    const unsigned tk =
+        __hip_atomic_fetch_add((g_u32*)(p.qctl + QC_HEAD), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const g_u64* slot = (const g_u64*)(p.qslot + (tk & (Q_CAP - 1)));
+    const unsigned long long t0 = wall_clock64();
+    unsigned long long v;
+    while (((v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != (unsigned long long)(tk + 1u)) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR) {
+        v = QK_EXIT;
+        break;
+      }
+      if (wall_clock64() - t0 > (p.h_req != nullptr ? HOST_TIMEOUT_TICKS : BARRIER_TIMEOUT_TICKS)) {
+        raise_err(p, ERR_TIMEOUT);
+        v = QK_EXIT;
+        break;
+      }
+    }
+    bc[1] = (int)(unsigned)v;
+    }
+  }
+done:
+  __syncthreads();
+  const unsigned item = (unsigned)bc[1];
+  __syncthreads();
+  return item;
+}
+
+// One tile of one graph for iteration `it` (queue mode; the same pieces and order as the
+// lock-step tile loop).  Neighbour lists: built and cached at iteration 1, reloaded at 2-3.
+__device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int it, int j) {
+  KParams& p = kp();
+  float* scr = lds + L_SCR;
+  int* rows = (int*)(scr + S_ROW);
+  const GraphInfo gi = p.ginfo[g];
+  lds_i32* hdr = (lds_i32*)(int*)(scr + S_NBH);
+  const int slot = gl * p.nbc_gstride + j;
+  const bool cacheable = slot < p.nbc_slots && !(p.variant & 16);
+  const bool cached = cacheable && it > 1;
+  int cw = 0, ch = 0;
+  if (cached) {
+    const int* src = p.nbc + (size_t)slot * NBC_INTS;
+    cw = ldc(src + NBC_HDR + (threadIdx.x >> 8) * NBC_LWORDS + (threadIdx.x & 255));
+    if (threadIdx.x < 67) ch = ldc(src + threadIdx.x);
+  }
+  if (threadIdx.x < TILE) {
+    const int r = j * TILE + threadIdx.x;
+    const int nl = ldc(&p.gvar[g].n_live);
+    const float4 e = ldc4((const float*)(p.live + 4 * (size_t)gi.node_off), min(r, gi.n - 1) * 16);
+    const bool ok = r < nl && MD_BOK(__float_as_int(e.x) >= 0 && __float_as_int(e.x) < gi.n && nl <= gi.n, 6);
+    const unsigned c = (unsigned)__float_as_int(e.w);
+    rows[threadIdx.x] = ok ? __float_as_int(e.x) : -1;
+    hdr[64 + threadIdx.x] = ok ? __float_as_int(e.y) : 0;
+    hdr[96 + threadIdx.x] = ok ? (int)(c & 0xffffu) : 0;
+    hdr[64 + 16 + threadIdx.x] = ok ? __float_as_int(e.z) : 0;
+    hdr[96 + 16 + threadIdx.x] = ok ? (int)(c >> 16) : 0;
+  }
+  int* misc = (int*)(lds + L_MISC);
+  if (cached) {
+    ((lds_i32*)(int*)(scr + S_NBL))[(threadIdx.x >> 8) * NBC_LWORDS + (threadIdx.x & 255)] = cw;
+    if (threadIdx.x < 64) hdr[threadIdx.x] = ch;
+    else if (threadIdx.x < 66) hdr[128 + threadIdx.x - 64] = ch;
+    else if (threadIdx.x == 66) misc[59] = ch;
+  }
+  __syncthreads();
+  bool nb_ok;
+  if (cached) {
+    nb_ok = misc[59] != 0;
+    const int nw0 = (hdr[128] + 1) >> 1, nw1 = (hdr[129] + 1) >> 1;
+    if (nb_ok && (nw0 > 256 || nw1 > 256)) {
+      const int* src = p.nbc + (size_t)slot * NBC_INTS + NBC_HDR;
+      lds_i32* words = (lds_i32*)(int*)(scr + S_NBL);
+      for (int i = 256 + (int)threadIdx.x; i < nw0; i += NTHREADS) words[i] = ldc(src + i);
+      for (int i = 256 + (int)threadIdx.x; i < nw1; i += NTHREADS) words[NBC_LWORDS + i] = ldc(src + NBC_LWORDS + i);
+      __syncthreads();
+    }
+  } else {
+    nb_ok = !(p.variant & 16) && build_nb_lists(p, gi, rows, scr, nullptr, -1);
+    if (cacheable) nbc_store(p, slot, scr, nb_ok);
+  }
+  if (nb_ok) gather_tile2(p, gi, it, rows, scr);
+  else gather_tile(p, gi, it, rows, scr);
+  __syncthreads();
+  update_tile(lds + L_W, scr);
+  __syncthreads();
+  normalize_tile(scr + S_E, scr);
+  __syncthreads();
+  if (threadIdx.x < 128 && it < 3) {
+    // tile partial sums of the virtual node (rows in ascending compact order from 0)
+    const int l = threadIdx.x >> 6, c = threadIdx.x & 63;
+    const float* ate = scr + S_E + l * 64 * LDT + c * LDT;
+    const float* atx = scr + S_X + l * 64 * LDT + c * LDT;
+    float s_new = 0.f, s_old = 0.f;
+    for (int r = 0; r < TILE; ++r) {
+      if (rows[r] < 0) break;
+      s_new = s_new + ate[r];
+      s_old = s_old + atx[r];
+    }
+    float* sp = p.spart + (size_t)(gi.tile_off + j) * 384;
+    if (it == 1) {
+      stc(sp + l * 64 + c, s_old);        // S0 (first-layer input)
+      stc(sp + 128 + l * 64 + c, s_new);  // S1
+    } else {
+      stc(sp + 256 + l * 64 + c, s_new);  // S2
+    }
+  }
+  if (it < 3) {
+    const int w = wave_id(), l = w >> 2, lane = lane_id();
+    float* hb = p.H[l][(it - 1) & 1] + (size_t)gi.node_off * EMB;
+    const int r = 4 * (w & 3) + (lane >> 4), q4 = lane & 15;
+    const int v = rows[r];
+    const float* e = scr + S_E + l * 64 * LDT + 4 * q4 * LDT + r;
+    if (v >= 0) stc4(hb, v * 256 + q4 * 16, make_float4(e[0], e[LDT], e[2 * LDT], e[3 * LDT]));
+  }
+  __syncthreads();
+  // iteration 3: the graph head was published (tag 1) before this item was pushed
+  if (it == 3) attention_q_tile(p, lds, scr, gi, g, rows, p.apart + (size_t)(gi.tile_off + j) * 4, 1ull, nullptr);
+}
+
+// Virtual-node chain Y1..Y3 from the tile partial sums S0..S2 and the graph head of graph g,
+// published as tagged granules (tag 1) for its iteration-3 tiles.
+__device__ __noinline__ void queue_vn(KParams&, float* lds, int g) {
+  KParams& p = kp();
+  float* scr = lds + L_SCR;
+  const GraphInfo gi = p.ginfo[g];
+  gv_load(p, g, (GraphVar*)(lds + L_GV));
+  __syncthreads();
+  const GraphVar& gv = *(const GraphVar*)(lds + L_GV);
+  const int nt = (gv.n_live + TILE - 1) / TILE;
+  float* sbuf = scr + S_HID;  // [2][64]
+  float* yw = lds + L_YW;
+  if (threadIdx.x < 128) yw[threadIdx.x] = lds[L_Y0 + (threadIdx.x & 63)];
+  for (int k = 0; k < 3; ++k) {
+    graph_sum(p, gi, nt, k, sbuf, scr + S_YP);
+    vrow_update(lds + L_W, scr, sbuf, yw);  // Y(k+1) from S(k)
+  }
+  graph_head(p, lds, scr, gi, gv, false, false);
+  head_publish(p, lds, g, 1ull);
+}
+
+__device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __restrict__ wimg) {
+  KParams& p = kp();
+  int* misc = (int*)(lds + L_MISC);
+  int* bc = misc + 48;
+  const int ng = p.nglist;
+  if (blockIdx.x == 0) {
+    // the running graphs start with an environment step (no prediction yet)
+    int* run = (int*)(lds + L_PREF);
+    const int mine = (int)threadIdx.x < ng && ldc(&p.gvar[p.glist[threadIdx.x]].status) == ST_RUN;
+    int tot = 0;
+    const int at = block_excl_scan(mine, (int*)(lds + L_SCR + S_RED), &tot);
+    if (mine) run[at] = threadIdx.x;
+    if (threadIdx.x == 0)
+      __hip_atomic_store((g_u32*)(p.qctl + QC_REM), (unsigned)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (tot > 0) q_push(p, tot, [&](int i) { return q_item(QK_ENV, 0, run[i], 0); }, bc);
+    else q_push(p, gridDim.x, [&](int) { return (unsigned)QK_EXIT; }, bc);
+  }
+  bool wdirty = false;
+  // diagnostics (md_profile): per item kind, total device ticks and count in prof[kind] /
+  // prof[8 + kind]; ticks waiting for items in prof[16]; weight reloads in prof[17]
+  unsigned long long* qp = p.prof;
+  unsigned long long tq = wall_clock64();
+  if (qp != nullptr && blockIdx.x == 0 && threadIdx.x == 0) qp[0] = 1;  // the record is present
+  while (true) {
+    const unsigned item = q_pop(p, bc);
+    const unsigned kind = item & 7u;
+    unsigned long long ti = 0;
+    if (qp != nullptr && threadIdx.x == 0) {
+      ti = wall_clock64();
+      atomicAdd(qp + 16, ti - tq);
+      atomicAdd(qp + 8 + (kind & 7u), 1ull);
+    }
+    if (kind == QK_EXIT || kind == 0u) break;
+    const int it = (int)((item >> 3) & 3u), gl = (int)((item >> 5) & 1023u), j = (int)(item >> 15);
+    const int g = p.glist[gl];
+    if (kind == QK_ENV) {
+      phase_a(p, g, it != 0, lds, false);
+      wdirty = true;
+      const GraphVar& gv = *(const GraphVar*)(lds + L_GV);
+      const int st = gv.status, nl = gv.n_live;
+      __syncthreads();
+      if (st == ST_RUN && nl <= 0) {
+        // cannot happen (alive edges in both layers imply live nodes); never strand the queue
+        if (threadIdx.x == 0) raise_err(p, ERR_LIVE_MISMATCH);
+        break;
+      }
+      if (st == ST_RUN) {
+        const int nt = (nl + TILE - 1) / TILE;
+        if (threadIdx.x == 0) stc(p.qg + 2 * gl + 1, nt);
+        q_push(p, nt, [&](int i) { return q_item(QK_TILE, 1, gl, i); }, bc);
+      } else if (st == ST_WAIT_HOST) {
+        q_push(p, 1, [&](int) { return q_item(QK_ENV, 1, gl, 0); }, bc);  // poll again later
+      } else {
+        if (threadIdx.x == 0)
+          bc[2] = (int)__hip_atomic_fetch_add((g_u32*)(p.qctl + QC_REM), 0xffffffffu, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (bc[2] == 1) q_push(p, gridDim.x, [&](int) { return (unsigned)QK_EXIT; }, bc);
+      }
+      if (qp != nullptr && threadIdx.x == 0) atomicAdd(qp + kind, (tq = wall_clock64()) - ti);
+      continue;
+    }
+    if (wdirty) {
+      load_weights(lds + L_W, wimg);
+      __syncthreads();
+      wdirty = false;
+      if (qp != nullptr && threadIdx.x == 0) atomicAdd(qp + 17, wall_clock64() - ti);
+    }
+    int next = 0;
+    if (kind == QK_TILE) {
+      queue_tile(p, lds, g, gl, it, j);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const int nt = ldc(p.qg + 2 * gl + 1);
+        const int old = __hip_atomic_fetch_add(p.qg + 2 * gl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == nt - 1) {
+          stc(p.qg + 2 * gl, 0);
+          bc[3] = it;
+        } else {
+          bc[3] = 0;
+        }
+      }
+      __syncthreads();
+      next = bc[3];
+    } else {  // QK_VN
+      queue_vn(p, lds, g);
+      next = 4;
+    }
+    if (next != 0) {
+      const int nt = ldc(p.qg + 2 * gl + 1);
+      if (next == 1) q_push(p, nt, [&](int i) { return q_item(QK_TILE, 2, gl, i); }, bc);
+      else if (next == 2) q_push(p, 1, [&](int) { return q_item(QK_VN, 0, gl, 0); }, bc);
+      else if (next == 3) q_push(p, 1, [&](int) { return q_item(QK_ENV, 1, gl, 0); }, bc);
+      else q_push(p, nt, [&](int i) { return q_item(QK_TILE, 3, gl, i); }, bc);
+    }
+    if (qp != nullptr && threadIdx.x == 0) atomicAdd(qp + (kind == QK_TILE ? 4 + it : kind), (tq = wall_clock64()) - ti);
+  }
+}
+
 // ------------------------------------------------------------------ the kernel
 // One body, two entry points so profiles separate the work: md_rollout_kernel runs whole
 // rollouts (RUN_ROLLOUT); md_env_kernel runs single environment steps and predictions
@@ -1660,6 +1943,10 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
     __syncthreads();
   }
 
+  if (p.qmode) {
+    queue_loop(p, lds, wimg);
+    return;
+  }
   unsigned target = 0;
   int* bflag = (int*)(lds + L_MISC) + 61;  // barrier error broadcast
   const int my_gl = (int)threadIdx.x < p.nglist ? p.glist[threadIdx.x] : 0;  // nglist <= G_CAP = NTHREADS

@@ -31,6 +31,17 @@ eng.rollout()
 ms2, _ = eng.last_timing()
 P = eng.profile_read().astype(np.int64)
 eng.profile(0)
+if len(P) and P[0, 0] == 1 and P[0, 9] > 0:
+    # queue mode: per item kind total device time (summed over workgroups) and counts
+    names = {1: "ENV", 3: "VN", 5: "TILE it1", 6: "TILE it2", 7: "TILE it3"}
+    cnt = {1: P[0, 9], 3: P[0, 11], 5: P[0, 10]}
+    tot = P[0, 16] + P[0, 17] + sum(P[0, k] for k in names)
+    print("queue mode, %.1f WG-ms in total (%d workgroups x %.2f ms)" % (tot / 1e5, 256, ms2 / 1.0))
+    for k, nm in names.items():
+        print("  %-9s %9.1f WG-ms" % (nm, P[0, k] / 1e5))
+    print("  items: ENV %d VN %d TILE %d; waiting for items %.1f WG-ms; weight reloads %.1f WG-ms" % (
+        P[0, 9], P[0, 11], P[0, 10], P[0, 16] / 1e5, P[0, 17] / 1e5))
+    sys.exit(0)
 full = P[P[:, 10] > 0]
 d = lambda a, b: (full[:, b] - full[:, a]) / 100.0
 A, bA, i1, i2, i3 = d(0, 3), d(3, 4), d(4, 6), d(6, 8), d(8, 10)
