@@ -1660,35 +1660,36 @@ __device__ __forceinline__ void q_push(KParams& p, int n, F&& f, int* bc) {
   }
   __syncthreads();
 }
-__device__ __forceinline__ unsigned q_pop(KParams& p, int* bc) {
+// Thread 0 takes the next ticket; it is taken one item ahead (the atomic's latency overlaps
+// the current item), so a workgroup may hold one ticket it never uses when it exits: EXIT
+// items are pushed twice per workgroup.
+__device__ __forceinline__ unsigned q_take(KParams& p) {
+  return threadIdx.x == 0
+             ? __hip_atomic_fetch_add((g_u32*)(p.qctl + QC_HEAD), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+             : 0u;
+}
+__device__ __forceinline__ unsigned q_wait(KParams& p, unsigned tk, int* bc) {
   if (threadIdx.x == 0) {
+    unsigned long long v = QK_EXIT;
     // an error anywhere: stop taking work (the grid drains)
-    if (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR) {
-      bc[1] = (int)QK_EXIT;
-      goto done;
-    }
-    {
-    const unsigned tk =
-        __hip_atomic_fetch_add((g_u32*)(p.qctl + QC_HEAD), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const g_u64* slot = (const g_u64*)(p.qslot + (tk & (Q_CAP - 1)));
-    const unsigned long long t0 = wall_clock64();
-    unsigned long long v;
-    while (((v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != (unsigned long long)(tk + 1u)) {
-      __builtin_amdgcn_s_sleep(2);
-      if (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR) {
-        v = QK_EXIT;
-        break;
-      }
-      if (wall_clock64() - t0 > (p.h_req != nullptr ? HOST_TIMEOUT_TICKS : BARRIER_TIMEOUT_TICKS)) {
-        raise_err(p, ERR_TIMEOUT);
-        v = QK_EXIT;
-        break;
+    if (!(__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR)) {
+      const g_u64* slot = (const g_u64*)(p.qslot + (tk & (Q_CAP - 1)));
+      const unsigned long long t0 = wall_clock64();
+      while (((v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != (unsigned long long)(tk + 1u)) {
+        __builtin_amdgcn_s_sleep(2);
+        if (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR) {
+          v = QK_EXIT;
+          break;
+        }
+        if (wall_clock64() - t0 > (p.h_req != nullptr ? HOST_TIMEOUT_TICKS : BARRIER_TIMEOUT_TICKS)) {
+          raise_err(p, ERR_TIMEOUT);
+          v = QK_EXIT;
+          break;
+        }
       }
     }
     bc[1] = (int)(unsigned)v;
-    }
   }
-done:
   __syncthreads();
   const unsigned item = (unsigned)bc[1];
   __syncthreads();
@@ -1823,7 +1824,7 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
       __hip_atomic_store((g_u32*)(p.qctl + QC_REM), (unsigned)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (tot > 0) q_push(p, tot, [&](int i) { return q_item(QK_ENV, 0, run[i], 0); }, bc);
-    else q_push(p, gridDim.x, [&](int) { return (unsigned)QK_EXIT; }, bc);
+    else q_push(p, 2 * gridDim.x, [&](int) { return (unsigned)QK_EXIT; }, bc);
   }
   bool wdirty = false;
   // diagnostics (md_profile): per item kind, total device ticks and count in prof[kind] /
@@ -1831,8 +1832,10 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
   unsigned long long* qp = p.prof;
   unsigned long long tq = wall_clock64();
   if (qp != nullptr && blockIdx.x == 0 && threadIdx.x == 0) qp[0] = 1;  // the record is present
+  unsigned tk = q_take(p);
   while (true) {
-    const unsigned item = q_pop(p, bc);
+    const unsigned item = q_wait(p, tk, bc);
+    tk = q_take(p);
     const unsigned kind = item & 7u;
     unsigned long long ti = 0;
     if (qp != nullptr && threadIdx.x == 0) {
@@ -1865,7 +1868,7 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
           bc[2] = (int)__hip_atomic_fetch_add((g_u32*)(p.qctl + QC_REM), 0xffffffffu, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
-        if (bc[2] == 1) q_push(p, gridDim.x, [&](int) { return (unsigned)QK_EXIT; }, bc);
+        if (bc[2] == 1) q_push(p, 2 * gridDim.x, [&](int) { return (unsigned)QK_EXIT; }, bc);
       }
       if (qp != nullptr && threadIdx.x == 0) atomicAdd(qp + kind, (tq = wall_clock64()) - ti);
       continue;
