@@ -690,8 +690,6 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
     const long slots = (long)std::min(n_graphs, G_CAP) * maxt;
     c->nbc_slots = (int)slots;
     c->nbc_gstride = (int)maxt;
-    HIPCHK(c, c->qslot.alloc(Q_CAP));
-    HIPCHK(c, c->qg.alloc(2 * G_CAP));
     HIPCHK(c, c->nbc.alloc((size_t)std::max<long>(1, slots) * NBC_INTS));
   }  // split tiles of a launch <= CUs / 2 <= XB_SLOTS
   HIPCHK(c, c->h_req.alloc((size_t)n_graphs));
@@ -714,6 +712,9 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
     }
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  // queue-mode buffers last (allocation order moves the other buffers' addresses)
+  HIPCHK(c, c->qslot.alloc(Q_CAP));
+  HIPCHK(c, c->qg.alloc(2 * G_CAP));
   {
     int maxn = 0;
     for (int g = 0; g < n_graphs; ++g) maxn = std::max(maxn, (int)n_nodes[g]);

@@ -103,11 +103,6 @@ struct Params {
   int* nbc;                        // per launch tile slot: its alive neighbour lists (NBC_INTS ints), built at
                                    //   iteration 1, reloaded by iterations 2-3 of multi-tile workgroups
   int nbc_slots;
-  int nbc_gstride;                 // queue mode: cache slot = graph slot * nbc_gstride + tile
-  int qmode;                       // 1: batch rollout through the device work queue (queue_loop)
-  unsigned* qctl;                  // queue mode: {head ticket, tail ticket, running graphs}
-  unsigned long long* qslot;       // queue mode: Q_CAP item slots {ticket + 1, item}
-  int* qg;                         // queue mode: per graph slot {tiles done in the stage, tiles}
   unsigned long long* xbuf;        // layer split: per launch tile slot [2 layers][1024] E-row granules {tag, value}
   int* pend;                       // per node slot: host-queued actions
   int* tr_action;                  // per node slot: removal order
@@ -135,6 +130,11 @@ struct Params {
   int* err;                        // device error word (nonzero = failure code)
   unsigned long long* prof;        // optional phase timestamps of workgroup 0 (wall clock)
   int prof_cap;                    // steps of 16 timestamp slots available in prof
+  int nbc_gstride;                 // queue mode: cache slot = graph slot * nbc_gstride + tile
+  int qmode;                       // 1: batch rollout through the device work queue (queue_loop)
+  unsigned* qctl;                  // queue mode: {head ticket, tail ticket, running graphs}
+  unsigned long long* qslot;       // queue mode: Q_CAP item slots {ticket + 1, item}
+  int* qg;                         // queue mode: per graph slot {tiles done in the stage, tiles}
 };
 
 }  // namespace md

@@ -471,9 +471,12 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
 // queued node and run the fixed point (s0 first if not done), then residual degrees, the
 // ascending live-node list and the per-layer aggregates, the write-back of edge states and
 // the unit-cost first-layer table.  Returns 0 or an ERR_* code.
+// Not inlined: the environment step has its own register allocation (inlined, it raised the
+// register pressure of the whole rollout loop -- spills in the tile phases).
 template <bool GL>
-__device__ int env_step(KParams& p, const GraphInfo& gi, GraphVar& gv, float* area, int pend_n,
+__device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar& gv, float* area, int pend_n,
                         int pend_first, const float* lds_base, bool staged) {
+  KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   const int n = gi.n, e0 = gi.e[0], e1 = gi.e[1], et = e0 + e1;
   EnvView<GL> E;
   E.gi = &gi;

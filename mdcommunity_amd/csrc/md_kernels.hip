@@ -26,6 +26,14 @@ namespace md {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
+// The dynamic LDS of every kernel here, as a compile-time base: device functions derive their
+// LDS pointers from it instead of from pointer arguments, so their LDS addresses stay
+// constants whichever kernel (and however many call levels) they are reached from.
+__device__ __forceinline__ float* lds_base() {
+  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
+  return lds_dyn;
+}
+
 // ------------------------------------------------------------------ weight image (floats)
 // Weights in MFMA B-fragment order: frag[cb][s][lane] = W[4s + (lane>>4)][16cb + (lane&15)].
 constexpr int W_IP1 = 0;                // 4 x 16 x 64
@@ -544,7 +552,10 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
 // Gather for one tile: waves 0-3 layer 0, 4-7 layer 1; each wave handles rows 4*(w&3)..+3
 // concurrently, one 16-lane group per row, every lane owning 4 features (float4 loads).
 // it == 1: previous embedding = first-layer table (by degree, unit cost) or static input.
-__device__ __noinline__ void gather_tile(KParams&, const GraphInfo gi, int it, const int* rows, float* scr) {
+__device__ __noinline__ void gather_tile(KParams&, const GraphInfo gi, int it, const int*, float*) {
+  const int* const rows = (const int*)(lds_base() + L_SCR + S_ROW);
+  float* const scr = lds_base() + L_SCR;
+
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   const int w = wave_id(), l = w >> 2, lane = lane_id();
   const int grp = lane >> 4, qd = lane & 15;
@@ -626,8 +637,10 @@ __device__ __noinline__ void gather_tile(KParams&, const GraphInfo gi, int it, c
 // step.  Header (ints at S_NBH): off[2][16], cnt[2][16] (alive, per row), rawb[2][16],
 // rawc[2][16] (CSR extent), tot[2].  Returns false when a layer has more than NB_CAP alive
 // entries (the tile then uses gather_tile).
-__device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const int* rows, float* scr,
+__device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const int*, float*,
                                             unsigned long long* ts, int L) {
+  float* const scr = lds_base() + L_SCR;
+
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   // L < 0: both layers (waves 0-3 layer 0, 4-7 layer 1); L = 0 / 1: that layer, all waves
   const int NT = L < 0 ? 256 : NTHREADS;
@@ -762,7 +775,10 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
 // then each 16-lane group adds its row's neighbours in CSR order (the reference's sequential
 // scatter-add order).  Same results as gather_tile; high-degree rows no longer serialise
 // their loads.
-__device__ __noinline__ void gather_tile2(KParams&, const GraphInfo gi, int it, const int* rows, float* scr) {
+__device__ __noinline__ void gather_tile2(KParams&, const GraphInfo gi, int it, const int*, float*) {
+  const int* const rows = (const int*)(lds_base() + L_SCR + S_ROW);
+  float* const scr = lds_base() + L_SCR;
+
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   const int w = wave_id(), l = w >> 2, lane = lane_id(), t = threadIdx.x & 255;
   const int grp = lane >> 4, qd = lane & 15;
@@ -865,7 +881,9 @@ __device__ __noinline__ void gather_tile2(KParams&, const GraphInfo gi, int it, 
 // Iteration 1 of a workgroup with several tiles: its tiles' alive neighbour lists and
 // headers go to the tile's cache slot (agent-scope stores), so iterations 2 and 3 reload them
 // in one round trip instead of rebuilding them from the CSR flags.
-__device__ __noinline__ void nbc_store(KParams&, int slot, const float* scr, bool ok) {
+__device__ __noinline__ void nbc_store(KParams&, int slot, const float*, bool ok) {
+  float* const scr = lds_base() + L_SCR;
+
   KParams& p = kp();
   int* dst = p.nbc + (size_t)slot * NBC_INTS;
   const lds_i32* hdr = (const lds_i32*)(const int*)(scr + S_NBH);
@@ -890,7 +908,10 @@ __device__ __noinline__ void nbc_store(KParams&, int slot, const float* scr, boo
 // Gather of layer L from its alive neighbour list: the 512 threads stage up to 2 * STG_ROWS
 // neighbour rows per batch (register double buffer as in gather_tile2), 32 lanes per row add
 // two features each in CSR order.
-__device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it, const int* rows, float* scr, int L) {
+__device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it, const int*, float*, int L) {
+  const int* const rows = (const int*)(lds_base() + L_SCR + S_ROW);
+  float* const scr = lds_base() + L_SCR;
+
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   constexpr int SROWS = 2 * STG_ROWS, NLD = (SROWS * 16 + NTHREADS - 1) / NTHREADS;
   const int w = wave_id(), lane = lane_id(), t = threadIdx.x, l = L;
@@ -983,7 +1004,10 @@ __device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it,
 
 // Node update of layer L: waves 0-3 P.P1 (column block w), waves 4-7 X.P2, then waves 0-3
 // relu(M.P3).  Each output's k-chain is update_tile's.
-__device__ __noinline__ void update_tile_split(const float* wi, float* scr, int L) {
+__device__ __noinline__ void update_tile_split(const float*, float*, int L) {
+  const float* const wi = lds_base() + L_W;
+  float* const scr = lds_base() + L_SCR;
+
   const int w = wave_id(), cb = w & 3, lane = lane_id();
   const int ar = lane & 15, ak = lane >> 4;
   const bool second = w >= 4;
@@ -1024,7 +1048,10 @@ __device__ __noinline__ void update_tile_split(const float* wi, float* scr, int 
 }
 
 // Row-normalise layer L of the transposed tile at `at` in place (normalize_tile's order).
-__device__ __noinline__ void normalize_tile_split(float* at, float* scr, int L) {
+__device__ __noinline__ void normalize_tile_split(float*, float*, int L) {
+  float* const scr = lds_base() + L_SCR;
+  float* const at = scr + S_E;
+
   float* red = scr + S_RED;
   const int t = threadIdx.x;
   float* a = at + L * 64 * LDT;
@@ -1052,7 +1079,10 @@ __device__ __noinline__ void normalize_tile_split(float* at, float* scr, int L) 
 }
 
 // Node update for one tile: H' = relu([P.P1 | X.P2] . P3) into S_E (normalised separately).
-__device__ __noinline__ void update_tile(const float* wi, float* scr) {
+__device__ __noinline__ void update_tile(const float*, float*) {
+  const float* const wi = lds_base() + L_W;
+  float* const scr = lds_base() + L_SCR;
+
   const int w = wave_id(), l = w >> 2, cb = w & 3, lane = lane_id();
   const int ar = lane & 15, ak = lane >> 4;
   const float* atp = scr + S_P + l * 64 * LDT;
@@ -1100,7 +1130,10 @@ __device__ __noinline__ void update_tile(const float* wi, float* scr) {
 }
 
 // Row-normalise the [2][64][16] transposed tile at `at` in place (torch reduction order).
-__device__ __noinline__ void normalize_tile(float* at, float* scr) {
+__device__ __noinline__ void normalize_tile(float*, float*) {
+  float* const scr = lds_base() + L_SCR;
+  float* const at = scr + S_E;
+
   float* red = scr + S_RED;
   const int t = threadIdx.x;
   if (t < 256) {
@@ -1130,7 +1163,10 @@ __device__ __noinline__ void normalize_tile(float* at, float* scr) {
 // Sum of one graph's per-tile partial sums (slot) -> out[2][64]: four threads per output each
 // add a contiguous quarter of the tiles in order, then the quarters are added in order
 // (a fixed order, identical in every workgroup).
-__device__ void graph_sum(KParams& p, const GraphInfo& gi, int nt, int slot, float* out, float* tmp4) {
+__device__ void graph_sum(KParams& p, const GraphInfo& gi, int nt, int slot, float*, float*) {
+  float* const out = lds_base() + L_SCR + S_HID;
+  float* const tmp4 = lds_base() + L_SCR + S_YP;
+
   const int o = threadIdx.x & 127, qt = threadIdx.x >> 7;
   const int per = (nt + 3) >> 2;
   const int j0 = min(nt, qt * per), j1 = min(nt, j0 + per);
@@ -1152,7 +1188,12 @@ __device__ void graph_sum(KParams& p, const GraphInfo& gi, int nt, int slot, flo
 
 // One virtual-node iteration for both layers: y' = normalize(relu([s.P1 | y.P2] . P3)),
 // computed by the 4 waves of each layer group as 4 partial chains summed in order.
-__device__ __noinline__ void vrow_update(const float* wi, float* scr, const float* s /*[2][64]*/, float* y /*[2][64]*/) {
+__device__ __noinline__ void vrow_update(const float*, float*, const float* /*[2][64]*/, float* /*[2][64]*/) {
+  const float* const wi = lds_base() + L_W;
+  float* const scr = lds_base() + L_SCR;
+  const float* const s = scr + S_HID;
+  float* const y = lds_base() + L_YW;
+
   const int w = wave_id(), l = w >> 2, q = w & 3, lane = lane_id();
   float* yp = scr + S_YP + l * 512;
   float* ym = scr + S_YM + l * 128;
@@ -1227,8 +1268,12 @@ __device__ __forceinline__ void graph_aux(float* gs, const GraphInfo& gi, const 
 
 // Graph rows: y_l from the final virtual-node embeddings E_l = Y3_l (in L_YW), the layer-mix
 // weights softmax(relu(y_l.WL1).WL2) and the aux features (U/PrepareBatchGraph.py:92-101).
-__device__ __noinline__ void graph_head(KParams&, float* lds, float* scr, const GraphInfo gi,
-                                        const GraphVar& gv, bool wl1_resident, bool aux_ready) {
+__device__ __noinline__ void graph_head(KParams&, float*, float*, const GraphInfo gi,
+                                        const GraphVar&, bool wl1_resident, bool aux_ready) {
+  float* const lds = lds_base();
+  float* const scr = lds + L_SCR;
+  const GraphVar& gv = *(const GraphVar*)(lds + L_GV);
+
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   const int w = wave_id(), l = w >> 2, q = w & 3, lane = lane_id();
   const float* wi = lds + L_W;
@@ -1359,8 +1404,11 @@ __device__ __forceinline__ void split_receive(KParams& p, float* scr, int slot, 
 // One iteration of the graph-head workgroup (dedicated mode) for graph g: it == 2 builds
 // Y1, Y2 from the S0 / S1 tile partials of iteration 1; it == 3 builds Y3 from S2, runs the
 // graph head and publishes it.  Same arithmetic as the shared-mode path in the tile loop.
-__device__ __noinline__ void head_iteration(KParams&, float* lds, float* scr, int g, int it,
+__device__ __noinline__ void head_iteration(KParams&, float*, float*, int g, int it,
                                             unsigned long long htag) {
+  float* const lds = lds_base();
+  float* const scr = lds + L_SCR;
+
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   // diagnostics: iteration-3 timestamps of the first graph's head workgroup (slots 48-53)
   unsigned long long* hts = nullptr;
@@ -1410,9 +1458,13 @@ __device__ __noinline__ void head_iteration(KParams&, float* lds, float* scr, in
 
 // Attention + Q head for one tile whose final embeddings are in S_E (both layers).
 // Writes q for valid rows and this tile's arg-max partial.
-__device__ __noinline__ void attention_q_tile(KParams&, float* lds, float* scr, const GraphInfo gi, int g,
-                                              const int* rows, float* apart_out, unsigned long long htag,
+__device__ __noinline__ void attention_q_tile(KParams&, float*, float*, const GraphInfo gi, int g,
+                                              const int*, float* apart_out, unsigned long long htag,
                                               unsigned long long* ts) {
+  float* const lds = lds_base();
+  float* const scr = lds + L_SCR;
+  const int* const rows = (const int*)(scr + S_ROW);
+
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   const float* wi = lds + L_W;
   const int w = wave_id(), l = w >> 2, cb = w & 3, lane = lane_id();
@@ -1946,10 +1998,6 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
     __syncthreads();
   }
 
-  if (p.qmode) {
-    queue_loop(p, lds, wimg);
-    return;
-  }
   unsigned target = 0;
   int* bflag = (int*)(lds + L_MISC) + 61;  // barrier error broadcast
   const int my_gl = (int)threadIdx.x < p.nglist ? p.glist[threadIdx.x] : 0;  // nglist <= G_CAP = NTHREADS
@@ -2220,6 +2268,28 @@ __global__ void __launch_bounds__(NTHREADS, 1) md_rollout_kernel(Params p, const
   engine_body(kp(), wimg);
 }
 
+// Batched rollouts through the device work queue (queue_loop); its own entry point so the
+// lock-step body's register allocation is not shaped by the queue code.
+__global__ void __launch_bounds__(NTHREADS, 1) md_queue_kernel(Params p, const float* __restrict__ wimg) {
+  if (!kargs_layout_ok()) {
+    if (threadIdx.x == 0) __hip_atomic_store(p.err, ERR_ABI, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  KParams& kpp = kp();
+  load_weights(lds + L_W, wimg);
+  __syncthreads();
+  if (wave_id() == 0) {
+    // constant virtual-node input: normalize(relu([1,1] . w_n2l))  (net :247,272-283)
+    const int lane = lane_id();
+    const float x = fmaxf(fmaf(1.f, lds[L_W + W_IWN + 64 + lane], fmaf(1.f, lds[L_W + W_IWN + lane], 0.f)), 0.f);
+    const float nr = wave_norm64(x);
+    lds[L_Y0 + lane] = x / fmaxf(nr, 1e-12f);
+  }
+  __syncthreads();
+  queue_loop(kpp, lds, wimg);
+}
+
 __global__ void __launch_bounds__(NTHREADS, 1) md_env_kernel(Params p, const float* __restrict__ wimg) {
   if (!kargs_layout_ok()) {
     if (threadIdx.x == 0) __hip_atomic_store(p.err, ERR_ABI, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2316,7 +2386,9 @@ void build_weight_image(const float* w, float* img) {
 }
 
 hipError_t launch_rollout(const Params& p, const float* wimg, int grid, hipStream_t s) {
-  if (p.run_mode == RUN_ROLLOUT)
+  if (p.qmode)
+    hipLaunchKernelGGL(md_queue_kernel, dim3(grid), dim3(NTHREADS), lds_bytes(), s, p, wimg);
+  else if (p.run_mode == RUN_ROLLOUT)
     hipLaunchKernelGGL(md_rollout_kernel, dim3(grid), dim3(NTHREADS), lds_bytes(), s, p, wimg);
   else
     hipLaunchKernelGGL(md_env_kernel, dim3(grid), dim3(NTHREADS), lds_bytes(), s, p, wimg);
@@ -2337,6 +2409,8 @@ hipError_t launch_reset(const Params& p, hipStream_t s) {
 hipError_t set_kernel_attrs() {
   hipError_t e = hipFuncSetAttribute((const void*)md_rollout_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      lds_bytes());
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)md_queue_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes());
   if (e != hipSuccess) return e;
   return hipFuncSetAttribute((const void*)md_env_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes());
 }

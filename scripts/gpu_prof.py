@@ -32,7 +32,7 @@ def prof(name, team):
     # slots: 0 startA,1 after mcc,2 after feat,3 endA,4 afterbarA,11 p1 tiles start,5 end p1,6 after bar1,12,7,8,13,9,10
     full = P[(P[:, 10] > 0)]
     d = lambda a, b: np.median((full[:, b] - full[:, a])) * 10 / 1000.0  # us
-    seg = [("A:stage", 0, 1), ("A:apply+mcc", 1, 2), ("A:feat", 2, 14), ("A:h0", 14, 15), ("A:wreload", 15, 3), ("barA", 3, 4), ("pref", 4, 11), ("p1", 11, 5), ("bar1", 5, 6), ("p2", 12, 7),
+    seg = [("A:stage", 0, 1), ("A:apply+mcc", 1, 2), ("A:deg", 2, 32), ("A:live", 32, 34), ("A:wb", 34, 14), ("A:h0", 14, 15), ("A:wreload", 15, 3), ("barA", 3, 4), ("pref", 4, 11), ("p1", 11, 5), ("bar1", 5, 6), ("p2", 12, 7),
            ("bar2", 7, 8), ("p3", 13, 9), ("bar3", 9, 10)]
     tot = np.median(full[:, 10] - full[:, 0]) * 10 / 1000.0
     print(f"{name} team={team} variant={os.environ.get('MD_VARIANT', '0')} env_mode={os.environ.get('MD_ENV_MODE', '1')}: removals {len(out[0][0])} wall {dt*1e3:.2f} ms kernel {ms:.2f} ms launches {nl}; "
