@@ -474,9 +474,13 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
 // Not inlined: the environment step has its own register allocation (inlined, it raised the
 // register pressure of the whole rollout loop -- spills in the tile phases).
 template <bool GL>
-__device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar& gv, float* area, int pend_n,
-                        int pend_first, const float* lds_base, bool staged) {
+__device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, float*, int pend_n,
+                        int pend_first, const float*, bool staged) {
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
+  // LDS from the kernel's dynamic-LDS base (compile-time addresses, ds_* accesses)
+  const float* const lds_base = md::lds_base();
+  GraphVar& gv = *(GraphVar*)(md::lds_base() + L_GV);
+  float* const area = md::lds_base() + L_W;
   const int n = gi.n, e0 = gi.e[0], e1 = gi.e[1], et = e0 + e1;
   EnvView<GL> E;
   E.gi = &gi;
