@@ -64,6 +64,13 @@ typedef struct md_ctx md_ctx;
 typedef int (*md_select_cb)(void* user, int graph, const double* q, int n_nodes, int n_out,
                             int32_t* actions);
 
+/* numpy's own float64 argsort routine (its ArrFuncs argsort[NPY_QUICKSORT] entry, the code
+ * np.argsort(x) runs for a contiguous float64 array; the package's _npsel helper module hands
+ * its address over).  Registered with md_set_tie_argsort, the tie hand-shake computes
+ * np.argsort(-q)[:step] (U/MultiDismantler_torch.py:725,769) on the host thread itself
+ * instead of calling the selection callback; NULL restores the callback. */
+typedef int (*md_argsort_f64)(void* data, int64_t* idx, int64_t n, void* unused);
+
 /* Create a context on HIP device `device`.  `weights` holds MD_WEIGHT_FLOATS floats
  * (replaces MultiDismantler.LoadModel, U/MultiDismantler_torch.py:791-797). */
 md_status md_create(int device, const float* weights, size_t n_floats, int cost_mode, md_ctx** out);
@@ -128,6 +135,9 @@ md_status md_get_state(md_ctx* ctx, int graph, uint8_t* covered, uint8_t* remove
  * nodes and pruned edges; no MCC is run (the reference's Predict runs none). */
 md_status md_set_state(md_ctx* ctx, int graph, const uint8_t* covered, const uint8_t* removed0,
                        const uint8_t* removed1);
+
+/* Host tie selection through numpy's argsort routine (see md_argsort_f64), NULL = callback. */
+md_status md_set_tie_argsort(md_ctx* ctx, md_argsort_f64 fn);
 
 /* Execution geometry override: number of tile workgroups of a launch, 0 = automatic
  * (one per 16-node tile, at most one workgroup per CU).  Results do not depend on it. */

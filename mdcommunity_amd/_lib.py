@@ -23,7 +23,8 @@ PROF_SLOTS = 64  # MD_PROF_SLOTS in include/mdroll.h
 
 EXPORTS = ("md_create", "md_destroy", "md_last_error", "md_set_weights", "md_load_graphs", "md_reset",
            "md_predict", "md_step", "md_rollout", "md_rollout_trace", "md_get_state", "md_set_state",
-           "md_set_team_size", "md_last_timing", "md_profile", "md_profile_read", "md_version")
+           "md_set_team_size", "md_set_tie_argsort", "md_last_timing", "md_profile", "md_profile_read",
+           "md_version")
 
 _i32p = ctypes.POINTER(ctypes.c_int32)
 _i64p = ctypes.POINTER(ctypes.c_int64)
@@ -67,6 +68,7 @@ def load_library(path=LIB_PATH):
         "md_get_state": (ctypes.c_int, [vp, ctypes.c_int, _u8p, _u8p, _u8p, _i32p]),
         "md_set_state": (ctypes.c_int, [vp, ctypes.c_int, _u8p, _u8p, _u8p]),
         "md_set_team_size": (ctypes.c_int, [vp, ctypes.c_int]),
+        "md_set_tie_argsort": (ctypes.c_int, [vp, vp]),
         "md_last_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), _i32p]),
         "md_profile": (ctypes.c_int, [vp, ctypes.c_int]),
         "md_profile_read": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, _i32p]),
@@ -82,6 +84,16 @@ def load_library(path=LIB_PATH):
 
 def _ptr(a, t):
     return a.ctypes.data_as(t) if a is not None else None
+
+
+def _numpy_argsort_ptr():
+    """Address of numpy's own float64 argsort routine (the one np.argsort runs), from the
+    package's _npsel helper; None when the helper is not built (the Python callback is used)."""
+    try:
+        from . import _npsel
+    except ImportError:
+        return None
+    return _npsel.argsort_f64()
 
 
 def _argsort_select(q, n_out):
@@ -169,6 +181,10 @@ class Engine:
         return lm, term.astype(bool)
 
     def rollout(self, step=1):
+        # the default rule np.argsort(-q)[:step] runs on the library's host thread through numpy's
+        # own argsort routine; a custom selector goes through the callback
+        native = _numpy_argsort_ptr() if self.selector is _argsort_select else None
+        self._check(self.lib.md_set_tie_argsort(self.h, native))
         tot = int(self.node_off[-1])
         seq = np.zeros(tot, np.int32)
         lm = np.zeros(tot, np.int32)

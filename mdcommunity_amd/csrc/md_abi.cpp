@@ -113,6 +113,7 @@ struct md_ctx {
   unsigned launch_seq = 0;
   // host selection hand-shake
   int host_mode = 1;
+  md_argsort_f64 tie_argsort = nullptr;  // numpy's float64 argsort (md_set_tie_argsort), else the callback
   int poll_us = 0;    // host poll interval while serving (MD_POLL_US)  // 1: ties / multi-node steps are answered inside the launch (MD_HOST_HANDSHAKE)
   HostBuf<unsigned> h_req, h_ans;
   HostBuf<int> h_nact, h_act;
@@ -276,12 +277,34 @@ struct Selector {
   std::string err;  // first failure, reported after the launch drained
 };
 
+// The reference's pick np.argsort(-q)[:n_out] on the masked float64 row: numpy's own float64
+// argsort routine when the caller registered it (no Python on the hand-shake path), else the
+// selection callback.  Returns 0 on success.
+int select_actions(md_ctx* c, md_select_cb cb, void* user, int g, const std::vector<double>& qd, int n, int nout,
+                   int32_t* acts) {
+  if (c->tie_argsort) {
+    thread_local std::vector<double> neg;
+    thread_local std::vector<int64_t> idx;
+    neg.resize(n);
+    idx.resize(n);
+    for (int i = 0; i < n; ++i) {
+      neg[i] = -qd[i];
+      idx[i] = i;
+    }
+    if (c->tie_argsort(neg.data(), idx.data(), n, nullptr) < 0) return 1;
+    for (int i = 0; i < nout; ++i) acts[i] = (int32_t)idx[i];
+    return 0;
+  }
+  if (!cb) return 1;
+  return cb(user, g, qd.data(), n, nout, acts);
+}
+
 // Answers graph g's request `tag`: Q row (float, -inf = masked) -> the reference's masked
 // double row, the callback's actions into mapped memory, then the answer tag.
 void serve_request(md_ctx* c, Selector* sel, int g, unsigned tag, std::vector<double>& qd, std::vector<int32_t>& acts) {
   const GraphInfo& gi = c->hinfo[g];
   int k = -1;
-  if (!sel->cb) {
+  if (!sel->cb && !c->tie_argsort) {
     if (sel->err.empty()) {
       char b[160];
       snprintf(b, sizeof b, "graph %d: nodes tie at the max Q and no selection callback was given", g);
@@ -320,7 +343,7 @@ void serve_request(md_ctx* c, Selector* sel, int g, unsigned tag, std::vector<do
     }
     const int nout = std::min(sel->step, gi.n);
     acts.assign(nout, -1);
-    if (sel->cb(sel->user, g, qd.data(), gi.n, nout, acts.data()) != 0) {
+    if (select_actions(c, sel->cb, sel->user, g, qd, gi.n, nout, acts.data()) != 0) {
       if (sel->err.empty()) sel->err = "selection callback failed (graph " + std::to_string(g) + ")";
     } else {
       k = 0;
@@ -551,6 +574,12 @@ md_status md_set_weights(md_ctx* c, const float* weights, size_t n_floats) {
   } else if (c->h0g.p) {
     c->h0g_dm = 0;
   }
+  return MD_OK;
+}
+
+md_status md_set_tie_argsort(md_ctx* c, md_argsort_f64 fn) {
+  if (!c) return MD_EINVAL;
+  c->tie_argsort = fn;
   return MD_OK;
 }
 
@@ -840,14 +869,16 @@ md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, i
       GraphVar& v = c->hvar[g];
       if (v.status != ST_NEED_HOST) continue;
       const GraphInfo& gi = c->hinfo[g];
-      if (!cb) return fail(c, MD_ECALLBACK, "graph %d: %d nodes tie at the max Q and no selection callback was given", g, v.ntie);
+      if (!cb && !c->tie_argsort)
+        return fail(c, MD_ECALLBACK, "graph %d: %d nodes tie at the max Q and no selection callback was given", g, v.ntie);
       qrow.resize(gi.n);
       qd.resize(gi.n);
       HIPCHK(c, hipMemcpy(qrow.data(), c->q.p + gi.node_off, sizeof(float) * gi.n, hipMemcpyDeviceToHost));
       for (int i = 0; i < gi.n; ++i) qd[i] = std::isinf(qrow[i]) ? QMASK : (double)qrow[i];
       const int nout = std::min(step, gi.n);
       acts.assign(nout, -1);
-      if (cb(user, g, qd.data(), gi.n, nout, acts.data()) != 0) return fail(c, MD_ECALLBACK, "selection callback failed (graph %d)", g);
+      if (select_actions(c, cb, user, g, qd, gi.n, nout, acts.data()) != 0)
+        return fail(c, MD_ECALLBACK, "selection callback failed (graph %d)", g);
       int k = 0;
       for (int i = 0; i < nout; ++i) {
         if (acts[i] < 0 || acts[i] >= gi.n) return fail(c, MD_ECALLBACK, "callback returned node %d out of range", acts[i]);

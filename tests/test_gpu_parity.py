@@ -221,3 +221,25 @@ def test_precomputed_first_layer_tables(monkeypatch):
             e.close()
     assert np.array_equal(out["1"][0], out["0"][0])
     assert out["1"][1] == out["0"][1] and out["1"][2] == out["0"][2]
+
+
+def test_native_tie_selection_matches_callback():
+    """Ties resolved on the library's host thread with numpy's argsort routine give the same
+    rollouts as the Python selection callback (np.argsort(-q)[:step]), single and batched."""
+    z = load_golden("gmm1000_s0")
+    g = (int(z["n_nodes"]), z["edges0"], z["edges1"])
+    graphs = [g] + [(int(load_golden(nm)["n_nodes"]), load_golden(nm)["edges0"], load_golden(nm)["edges1"])
+                    for nm in ("gmm200_s7", "er100")]
+    e = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
+    try:
+        for batch in ([g], graphs * 6):
+            e.load_graphs(batch)
+            e.reset()
+            native = [(s.tolist(), r.tolist()) for s, r in e.rollout()]
+            e.selector = lambda q, n_out: np.argsort(-q)[:n_out]  # forces the callback path
+            e.reset()
+            cb = [(s.tolist(), r.tolist()) for s, r in e.rollout()]
+            e.selector = _lib._argsort_select
+            assert native == cb
+    finally:
+        e.close()
