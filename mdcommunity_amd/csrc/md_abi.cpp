@@ -361,8 +361,15 @@ void serve_request(md_ctx* c, Selector* sel, int g, unsigned tag, std::vector<do
   __atomic_store_n(c->h_ans.h + g, tag, __ATOMIC_RELEASE);
 }
 
-md_status launch_chunk(md_ctx* c, const int* gl, int ngl, int run_mode, int host_select, Selector* sel) {
-  std::vector<int> v(gl, gl + ngl);
+md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int host_select, Selector* sel) {
+  std::vector<int> v(gl_in, gl_in + ngl);
+  // graphs with more edges first: the queue's first round-robin positions go to the longest
+  // rollouts (the rollout length grows with the edge count), so the launch does not end on a
+  // few long graphs running alone; the graph-slot order has no other meaning
+  std::stable_sort(v.begin(), v.end(), [&](int a, int b) {
+    return (long)c->hinfo[a].e[0] + c->hinfo[a].e[1] > (long)c->hinfo[b].e[0] + c->hinfo[b].e[1];
+  });
+  const int* gl = v.data();
   const int n_env = env_workgroups(c, v);
   // batches of whole rollouts run through the device work queue (MD_VARIANT bit 32: the
   // lock-step shared mode instead), one workgroup per CU
