@@ -1841,20 +1841,27 @@ __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int
 
 // Virtual-node chain Y1..Y3 from the tile partial sums S0..S2 and the graph head of graph g,
 // published as tagged granules (tag 1) for its iteration-3 tiles.
-__device__ __noinline__ void queue_vn(KParams&, float* lds, int g) {
+// Virtual-node chain of graph g in two items: part 1 (Y1, Y2 from the iteration-1 partial sums
+// S0, S1; runs beside the iteration-2 tiles, stored to ybuf) and part 2 (Y3 from S2 and the
+// graph head, published as tagged granules (tag 1) for the iteration-3 tiles).
+__device__ __noinline__ void queue_vn(KParams&, float* lds, int g, int part) {
   KParams& p = kp();
   float* scr = lds + L_SCR;
   const GraphInfo gi = p.ginfo[g];
   gv_load(p, g, (GraphVar*)(lds + L_GV));
+  float* yw = lds + L_YW;
+  if (threadIdx.x < 128) yw[threadIdx.x] = part == 1 ? lds[L_Y0 + (threadIdx.x & 63)] : ldc(p.ybuf + (size_t)g * 128 + threadIdx.x);
   __syncthreads();
   const GraphVar& gv = *(const GraphVar*)(lds + L_GV);
   const int nt = (gv.n_live + TILE - 1) / TILE;
   float* sbuf = scr + S_HID;  // [2][64]
-  float* yw = lds + L_YW;
-  if (threadIdx.x < 128) yw[threadIdx.x] = lds[L_Y0 + (threadIdx.x & 63)];
-  for (int k = 0; k < 3; ++k) {
+  for (int k = part == 1 ? 0 : 2; k < (part == 1 ? 2 : 3); ++k) {
     graph_sum(p, gi, nt, k, sbuf, scr + S_YP);
     vrow_update(lds + L_W, scr, sbuf, yw);  // Y(k+1) from S(k)
+  }
+  if (part == 1) {
+    if (threadIdx.x < 128) stc(p.ybuf + (size_t)g * 128 + threadIdx.x, yw[threadIdx.x]);
+    return;
   }
   graph_head(p, lds, scr, gi, gv, false, false);
   head_publish(p, lds, g, 1ull);
@@ -1883,6 +1890,8 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
   // prof[8 + kind]; ticks waiting for items in prof[16]; weight reloads in prof[17]
   unsigned long long* qp = p.prof;
   unsigned long long tq = wall_clock64();
+  if (threadIdx.x == 0) misc[60] = 1 << 30;  // no per-step phase stamps (MD_PROF_A) in queue mode
+  __syncthreads();
   if (qp != nullptr && blockIdx.x == 0 && threadIdx.x == 0) qp[0] = 1;  // the record is present
   unsigned tk = q_take(p);
   while (true) {
@@ -1932,34 +1941,38 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
       if (qp != nullptr && threadIdx.x == 0) atomicAdd(qp + 17, wall_clock64() - ti);
     }
     int next = 0;
-    if (kind == QK_TILE) {
-      queue_tile(p, lds, g, gl, it, j);
+    if (kind == QK_TILE || (kind == QK_VN && it == 1)) {
+      // a task of a stage: iteration-1/2/3 tiles; stage 2 also counts virtual-node part 1
+      if (kind == QK_TILE) queue_tile(p, lds, g, gl, it, j);
+      else queue_vn(p, lds, g, 1);
+      const int stage = kind == QK_TILE ? it : 2;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0) {
-        const int nt = ldc(p.qg + 2 * gl + 1);
+        const int tasks = ldc(p.qg + 2 * gl + 1) + (stage == 2 ? 1 : 0);
         const int old = __hip_atomic_fetch_add(p.qg + 2 * gl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == nt - 1) {
+        if (old == tasks - 1) {
           stc(p.qg + 2 * gl, 0);
-          bc[3] = it;
+          bc[3] = stage;
         } else {
           bc[3] = 0;
         }
       }
       __syncthreads();
       next = bc[3];
-    } else {  // QK_VN
-      queue_vn(p, lds, g);
+    } else {  // QK_VN part 2
+      queue_vn(p, lds, g, 2);
       next = 4;
     }
     if (next != 0) {
       const int nt = ldc(p.qg + 2 * gl + 1);
-      if (next == 1) q_push(p, nt, [&](int i) { return q_item(QK_TILE, 2, gl, i); }, bc);
-      else if (next == 2) q_push(p, 1, [&](int) { return q_item(QK_VN, 0, gl, 0); }, bc);
+      if (next == 1) {
+        q_push(p, nt + 1, [&](int i) { return i < nt ? q_item(QK_TILE, 2, gl, i) : q_item(QK_VN, 1, gl, 0); }, bc);
+      } else if (next == 2) q_push(p, 1, [&](int) { return q_item(QK_VN, 2, gl, 0); }, bc);
       else if (next == 3) q_push(p, 1, [&](int) { return q_item(QK_ENV, 1, gl, 0); }, bc);
       else q_push(p, nt, [&](int i) { return q_item(QK_TILE, 3, gl, i); }, bc);
     }
-    if (qp != nullptr && threadIdx.x == 0) atomicAdd(qp + (kind == QK_TILE ? 4 + it : kind), (tq = wall_clock64()) - ti);
+    if (qp != nullptr && threadIdx.x == 0) atomicAdd(qp + (kind == QK_TILE ? 4 + it : kind == QK_VN ? 2 + it : kind), (tq = wall_clock64()) - ti);
   }
 }
 

@@ -33,7 +33,7 @@ P = eng.profile_read().astype(np.int64)
 eng.profile(0)
 if len(P) and P[0, 0] == 1 and P[0, 9] > 0:
     # queue mode: per item kind total device time (summed over workgroups) and counts
-    names = {1: "ENV", 3: "VN", 5: "TILE it1", 6: "TILE it2", 7: "TILE it3"}
+    names = {1: "ENV", 3: "VN 1", 4: "VN 2", 5: "TILE it1", 6: "TILE it2", 7: "TILE it3"}
     cnt = {1: P[0, 9], 3: P[0, 11], 5: P[0, 10]}
     tot = P[0, 16] + P[0, 17] + sum(P[0, k] for k in names)
     print("queue mode, %.1f WG-ms in total (%d workgroups x %.2f ms)" % (tot / 1e5, 256, ms2 / 1.0))
