@@ -1692,7 +1692,13 @@ __device__ __forceinline__ int tile_graph(const int* pref, int ng, int t) {
 // barrier).  Every item runs to completion without waiting on another item, so the queue
 // cannot deadlock; when the last graph stops, one EXIT item per workgroup is pushed.
 enum : unsigned { QK_ENV = 1, QK_TILE = 2, QK_VN = 3, QK_EXIT = 4 };
-enum : int { QC_HEAD = 0, QC_TAIL = 1, QC_REM = 2 };
+enum : int { QC_HEAD = 0, QC_TAIL = 1, QC_REM = 2, QC_ADMIT = 3 };
+// Graphs running at once in queue mode: 3/8 of the workgroups (96 on 256 CUs; measured best
+// of 64..192 and all for 256 and 512 GMM N=1000 graphs).  MD_VARIANT bits 16+ override.
+__device__ __forceinline__ int q_admit(KParams& p) {
+  const int v = (int)((unsigned)p.variant >> 16);
+  return v > 0 ? v : max(1, (int)(Q_ADMIT_NUM * gridDim.x) / 8);
+}
 __device__ __forceinline__ unsigned q_item(unsigned kind, int it, int gl, int j) {
   return kind | ((unsigned)it << 3) | ((unsigned)gl << 5) | ((unsigned)j << 15);
 }
@@ -1720,11 +1726,21 @@ __device__ __forceinline__ unsigned q_take(KParams& p) {
              ? __hip_atomic_fetch_add((g_u32*)(p.qctl + QC_HEAD), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
              : 0u;
 }
-__device__ __forceinline__ unsigned q_wait(KParams& p, unsigned tk, int* bc) {
+// Thread 0 reads ticket tk's slot without waiting for it (issued beside an item's last memory
+// round trip, so a slot that is already filled costs no round trip of its own in q_wait).
+__device__ __forceinline__ unsigned long long q_peek(KParams& p, unsigned tk) {
+  return threadIdx.x == 0
+             ? __hip_atomic_load((const g_u64*)(p.qslot + (tk & (Q_CAP - 1))), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+             : 0ull;
+}
+__device__ __forceinline__ unsigned q_wait(KParams& p, unsigned tk, int* bc, unsigned long long pre) {
   if (threadIdx.x == 0) {
-    unsigned long long v = QK_EXIT;
-    // an error anywhere: stop taking work (the grid drains)
-    if (!(__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR)) {
+    unsigned long long v = pre;
+    // an error anywhere: stop taking work (the grid drains).  Checked only when the item is not
+    // there yet: a workgroup that keeps finding work sees the error once the queue runs dry.
+    const bool ready = (v >> 32) == (unsigned long long)(tk + 1u);
+    if (!ready) v = QK_EXIT;
+    if (!ready && !(__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR)) {
       const g_u64* slot = (const g_u64*)(p.qslot + (tk & (Q_CAP - 1)));
       const unsigned long long t0 = wall_clock64();
       while (((v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != (unsigned long long)(tk + 1u)) {
@@ -1879,10 +1895,17 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
     int tot = 0;
     const int at = block_excl_scan(mine, (int*)(lds + L_SCR + S_RED), &tot);
     if (mine) run[at] = threadIdx.x;
-    if (threadIdx.x == 0)
+    // admission: the first q_admit(p) running graphs (graph slots are ordered longest rollout
+    // first) start now; every graph that stops admits the next one, so the long rollouts do
+    // not wait behind the whole batch's backlog at every stage
+    const int first = min(tot, q_admit(p));
+    if (threadIdx.x == 0) {
       __hip_atomic_store((g_u32*)(p.qctl + QC_REM), (unsigned)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((g_u32*)(p.qctl + QC_ADMIT), (unsigned)(first < tot ? run[first] : ng), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
     __syncthreads();
-    if (tot > 0) q_push(p, tot, [&](int i) { return q_item(QK_ENV, 0, run[i], 0); }, bc);
+    if (tot > 0) q_push(p, first, [&](int i) { return q_item(QK_ENV, 0, run[i], 0); }, bc);
     else q_push(p, 2 * gridDim.x, [&](int) { return (unsigned)QK_EXIT; }, bc);
   }
   bool wdirty = false;
@@ -1890,18 +1913,42 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
   // prof[8 + kind]; ticks waiting for items in prof[16]; weight reloads in prof[17]
   unsigned long long* qp = p.prof;
   unsigned long long tq = wall_clock64();
+  const unsigned long long tq0 = tq;
   if (threadIdx.x == 0) misc[60] = 1 << 30;  // no per-step phase stamps (MD_PROF_A) in queue mode
   __syncthreads();
   if (qp != nullptr && blockIdx.x == 0 && threadIdx.x == 0) qp[0] = 1;  // the record is present
   unsigned tk = q_take(p);
+  unsigned long long pre = 0ull;  // thread 0: early read of the next ticket's slot
+  // A single-item stage that a workgroup enables (virtual-node part 2 after the last
+  // iteration-2 task, the environment step after the last iteration-3 tile) runs on that
+  // workgroup right away instead of queueing behind the backlog: one queue wait less on the
+  // graph's critical path per stage (MD_VARIANT bit 256 pushes them instead).
+  const bool inline_cont = !(p.variant & 256);
+  unsigned cont = 0u;
   while (true) {
-    const unsigned item = q_wait(p, tk, bc);
-    tk = q_take(p);
+    unsigned item;
+    if (cont != 0u) {
+      item = cont;
+      cont = 0u;
+    } else {
+      if (qp != nullptr && (p.variant & 8) && threadIdx.x == 0) {
+        // diagnostics (MD_VARIANT bit 8): pops whose slot was already filled at the early read
+        // (slot 18), and the queue's backlog beyond the held ticket summed over pops (slot 19)
+        if ((pre >> 32) == (unsigned long long)(tk + 1u)) atomicAdd(qp + 18, 1ull);
+        const unsigned tl = __hip_atomic_load((g_u32*)(p.qctl + QC_TAIL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd(qp + 19, (unsigned long long)max(0, (int)(tl - tk)));
+      }
+      item = q_wait(p, tk, bc, pre);
+      pre = 0ull;
+      tk = q_take(p);
+    }
     const unsigned kind = item & 7u;
     unsigned long long ti = 0;
     if (qp != nullptr && threadIdx.x == 0) {
       ti = wall_clock64();
       atomicAdd(qp + 16, ti - tq);
+      // waiting time over the launch in 1.31 ms buckets (slots 20..63)
+      atomicAdd(qp + 20 + min(43, (int)((ti - tq0) >> 17)), ti - tq);
       atomicAdd(qp + 8 + (kind & 7u), 1ull);
     }
     if (kind == QK_EXIT || kind == 0u) break;
@@ -1909,6 +1956,7 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
     const int g = p.glist[gl];
     if (kind == QK_ENV) {
       phase_a(p, g, it != 0, lds, false);
+      pre = q_peek(p, tk);
       wdirty = true;
       const GraphVar& gv = *(const GraphVar*)(lds + L_GV);
       const int st = gv.status, nl = gv.n_live;
@@ -1925,10 +1973,19 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
       } else if (st == ST_WAIT_HOST) {
         q_push(p, 1, [&](int) { return q_item(QK_ENV, 1, gl, 0); }, bc);  // poll again later
       } else {
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0) {
           bc[2] = (int)__hip_atomic_fetch_add((g_u32*)(p.qctl + QC_REM), 0xffffffffu, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
+          // admit the next graph that has not started (slots in order, skipping stopped ones)
+          int a;
+          while ((a = (int)__hip_atomic_fetch_add((g_u32*)(p.qctl + QC_ADMIT), 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)) < ng &&
+                 ldc(&p.gvar[p.glist[a]].status) != ST_RUN) {
+          }
+          bc[4] = a < ng ? a : -1;
+        }
         __syncthreads();
+        if (bc[4] >= 0) q_push(p, 1, [&](int) { return q_item(QK_ENV, 0, bc[4], 0); }, bc);
         if (bc[2] == 1) q_push(p, 2 * gridDim.x, [&](int) { return (unsigned)QK_EXIT; }, bc);
       }
       if (qp != nullptr && threadIdx.x == 0) atomicAdd(qp + kind, (tq = wall_clock64()) - ti);
@@ -1946,6 +2003,7 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
       if (kind == QK_TILE) queue_tile(p, lds, g, gl, it, j);
       else queue_vn(p, lds, g, 1);
       const int stage = kind == QK_TILE ? it : 2;
+      pre = q_peek(p, tk);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0) {
@@ -1962,15 +2020,20 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
       next = bc[3];
     } else {  // QK_VN part 2
       queue_vn(p, lds, g, 2);
+      pre = q_peek(p, tk);
       next = 4;
     }
     if (next != 0) {
       const int nt = ldc(p.qg + 2 * gl + 1);
       if (next == 1) {
         q_push(p, nt + 1, [&](int i) { return i < nt ? q_item(QK_TILE, 2, gl, i) : q_item(QK_VN, 1, gl, 0); }, bc);
-      } else if (next == 2) q_push(p, 1, [&](int) { return q_item(QK_VN, 2, gl, 0); }, bc);
-      else if (next == 3) q_push(p, 1, [&](int) { return q_item(QK_ENV, 1, gl, 0); }, bc);
-      else q_push(p, nt, [&](int i) { return q_item(QK_TILE, 3, gl, i); }, bc);
+      } else if (next == 2) {
+        if (inline_cont) cont = q_item(QK_VN, 2, gl, 0);
+        else q_push(p, 1, [&](int) { return q_item(QK_VN, 2, gl, 0); }, bc);
+      } else if (next == 3) {
+        if (inline_cont) cont = q_item(QK_ENV, 1, gl, 0);
+        else q_push(p, 1, [&](int) { return q_item(QK_ENV, 1, gl, 0); }, bc);
+      } else q_push(p, nt, [&](int i) { return q_item(QK_TILE, 3, gl, i); }, bc);
     }
     if (qp != nullptr && threadIdx.x == 0) atomicAdd(qp + (kind == QK_TILE ? 4 + it : kind == QK_VN ? 2 + it : kind), (tq = wall_clock64()) - ti);
   }

@@ -41,6 +41,12 @@ if len(P) and P[0, 0] == 1 and P[0, 9] > 0:
         print("  %-9s %9.1f WG-ms" % (nm, P[0, k] / 1e5))
     print("  items: ENV %d VN %d TILE %d; waiting for items %.1f WG-ms; weight reloads %.1f WG-ms" % (
         P[0, 9], P[0, 11], P[0, 10], P[0, 16] / 1e5, P[0, 17] / 1e5))
+    npop = P[0, 9] + P[0, 10] + P[0, 11]
+    print("  pops with the slot filled at the early read: %d of ~%d; mean backlog beyond the held ticket %.1f items" % (
+        P[0, 18], npop, P[0, 19] / max(1, npop)))
+    wb = P[0, 20:64] / 1e5
+    nb_ = int(np.max(np.nonzero(wb)[0])) + 1 if np.any(wb) else 0
+    print("  idle workgroups per 1.31 ms of the launch: " + " ".join("%.0f" % (w / 1.31) for w in wb[:nb_]))
     sys.exit(0)
 full = P[P[:, 10] > 0]
 d = lambda a, b: (full[:, b] - full[:, a]) / 100.0

@@ -177,6 +177,34 @@ def test_shared_mode_batch_matches_dedicated(eng):
         assert (s.tolist(), r.tolist()) == single[i % 3], i
 
 
+@pytest.mark.parametrize("admit", [1, 4])
+def test_queue_admission_limit_matches_single(monkeypatch, admit):
+    """Queue mode starts only `admit` graphs and admits the next one whenever a graph stops
+    (MD_VARIANT bits 16+ set the limit): every rollout equals its single-graph rollout."""
+    names = ["gmm200_s7", "er100", "er300_dense"]
+    graphs = [(int(z["n_nodes"]), z["edges0"], z["edges1"]) for z in map(load_golden, names)]
+    ref = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
+    single = []
+    try:
+        for g in graphs:
+            ref.load_graphs([g])
+            ref.reset()
+            s, r = ref.rollout()[0]
+            single.append((s.tolist(), r.tolist()))
+    finally:
+        ref.close()
+    monkeypatch.setenv("MD_VARIANT", str(admit << 16))
+    e = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
+    try:
+        e.load_graphs([graphs[i % 3] for i in range(18)])
+        e.reset()
+        out = e.rollout()
+        for i, (s, r) in enumerate(out):
+            assert (s.tolist(), r.tolist()) == single[i % 3], i
+    finally:
+        e.close()
+
+
 def test_global_memory_environment_mode(monkeypatch):
     """Graphs too large for one workgroup's LDS run the environment step on HBM scratch
     (EnvView<true>); MD_VARIANT=64 forces that mode for small graphs: same results."""
