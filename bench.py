@@ -247,7 +247,11 @@ def main():
         tfile = os.path.join(ROOT, "profiles", "traffic_r01.json")
         if os.path.exists(tfile):
             with open(tfile) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                tj = json.load(f)
+            traffic = tj.get("hbm_bytes_per_launch")
+            # measured HBM bytes per md_queue_kernel launch of the 256-graph batch (PMC passes)
+            if batch is not None and args.batch_graphs == 256 and "batch" in tj:
+                batch["roofline"]["traffic"] = tj["batch"].get("hbm_bytes_per_launch")
         line = {
             "metric": METRIC,
             "value": tot_removals / max_elapsed,

@@ -79,6 +79,8 @@ def test_real(variant, output, data_root, datasets, step_ratio=0.0, model=None):
         print("\nTesting dataset %s" % name)
         solution, t, score = dqn.EvaluateRealData(model_file, name + ".edges", save_dir, step_ratio, n, layers,
                                                   data_root=data_root)
+        # the reference's int64 frame takes floats in column j (pandas upcasts it to float64)
+        df[df.columns[j]] = df[df.columns[j]].astype(np.float64)
         df.iloc[0, j] = t
         df.iloc[1, j] = score
         print("Data:%s, time:%.2f, audc:%.6f" % (name, t, score))

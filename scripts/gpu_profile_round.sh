@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round profile on the GPU box: bench line, rocprofv3 kernel-trace stats of the bench command
-# (single-graph workload and batch workload separately), PMC FETCH_SIZE / WRITE_SIZE passes.
+# (single-graph workload and batch workload separately), PMC FETCH_SIZE / WRITE_SIZE passes of both.
 # Usage (from the repo root): bash scripts/gpu_profile_round.sh r01
 set -e
 TAG=${1:-r01}
@@ -19,6 +19,10 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run -- python 
 echo "fetch pass done"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run -- python $R/bench.py --batch-graphs 0 --no-cpu-baseline --steps 2 --warmup 1 > $OUT/pmc_write.log 2>&1
 echo "write pass done"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch_batch -o run -- python $R/bench.py --steps 0 --batch-graphs 256 --batch-steps 1 --no-cpu-baseline > $OUT/pmc_fetch_batch.log 2>&1
+echo "batch fetch pass done"
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write_batch -o run -- python $R/bench.py --steps 0 --batch-graphs 256 --batch-steps 1 --no-cpu-baseline > $OUT/pmc_write_batch.log 2>&1
+echo "batch write pass done"
 cd $R
 python scripts/rocprof_summary.py $OUT > /dev/null
 find $OUT -name "*stats*.csv" | head -20

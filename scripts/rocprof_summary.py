@@ -39,15 +39,36 @@ def kernel_stats(path):
     return out
 
 
-def pmc(path, counter):
+def pmc(path, counter, kernel):
     cur = sqlite3.connect(path).cursor()
     rows = list(cur.execute("select kernel_name, value, dispatch_id from counters_collection where counter_name = ?",
                             (counter,)))
     per = {}
     for name, val, disp in rows:
-        if KERNEL in name:
+        if kernel in name:
             per[disp] = per.get(disp, 0.0) + float(val)  # KB, summed over any per-XCD instances
     return [per[k] for k in sorted(per)]
+
+
+def traffic_of(d, suffix, kernel, lines):
+    traffic = {}
+    for sub, counter in (("pmc_fetch" + suffix, "FETCH_SIZE"), ("pmc_write" + suffix, "WRITE_SIZE")):
+        for path in dbs(os.path.join(d, sub)):
+            vals = pmc(path, counter, kernel)
+            traffic[counter] = vals
+            lines.append(f"== {counter} per {kernel} dispatch (KB, raw): {[round(v, 1) for v in vals]}")
+    if not traffic.get("FETCH_SIZE") or not traffic.get("WRITE_SIZE"):
+        return None
+    f = traffic["FETCH_SIZE"]
+    w = traffic["WRITE_SIZE"]
+    fetch_b = 2.0 * 1024.0 * sum(f) / len(f)   # gfx950: FETCH_SIZE counts half of wide reads
+    write_b = 1024.0 * sum(w) / max(1, len(w))
+    out = {"kernel": kernel, "launches": len(f), "fetch_bytes_per_launch": fetch_b,
+           "write_bytes_per_launch": write_b, "hbm_bytes_per_launch": fetch_b + write_b,
+           "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); WRITE_SIZE as is; "
+                         "access widths other than 16 B/lane are uncalibrated"}
+    lines.append(f"== traffic per {kernel} launch: " + json.dumps(out))
+    return out
 
 
 def main():
@@ -63,24 +84,14 @@ def main():
             for k, v in sorted(st.items(), key=lambda kv: -kv[1]["total_ns"]):
                 lines.append(f"{k[:60]:60s} {v['calls']:6d} {v['total_ns'] / 1e6:10.3f} {v['avg_ns'] / 1e3:10.1f} "
                              f"{v['min_ns'] / 1e3:10.1f} {v['max_ns'] / 1e3:10.1f} {v['workgroups']}")
-    traffic = {}
-    for sub, counter in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
-        for path in dbs(os.path.join(d, sub)):
-            vals = pmc(path, counter)
-            traffic[counter] = vals
-            lines.append(f"== {counter} per {KERNEL} dispatch (KB, raw): {[round(v, 1) for v in vals]}")
-    if "FETCH_SIZE" in traffic and "WRITE_SIZE" in traffic and traffic["FETCH_SIZE"]:
-        f = traffic["FETCH_SIZE"]
-        w = traffic["WRITE_SIZE"]
-        fetch_b = 2.0 * 1024.0 * sum(f) / len(f)   # gfx950: FETCH_SIZE counts half of wide reads
-        write_b = 1024.0 * sum(w) / max(1, len(w))
-        out = {"kernel": KERNEL, "launches": len(f), "fetch_bytes_per_launch": fetch_b,
-               "write_bytes_per_launch": write_b, "hbm_bytes_per_launch": fetch_b + write_b,
-               "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); WRITE_SIZE as is; "
-                             "access widths other than 16 B/lane are uncalibrated"}
+    single = traffic_of(d, "", KERNEL, lines)
+    batch = traffic_of(d, "_batch", "md_queue_kernel", lines)
+    if single is not None:
+        out = dict(single)
+        if batch is not None:
+            out["batch"] = batch
         with open(os.path.join(d, "traffic.json"), "w") as fo:
             json.dump(out, fo, indent=1)
-        lines.append("== traffic per launch: " + json.dumps(out))
     with open(os.path.join(d, "summary.txt"), "w") as fo:
         fo.write("\n".join(lines) + "\n")
     print("\n".join(lines))
