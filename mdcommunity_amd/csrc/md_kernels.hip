@@ -1772,6 +1772,23 @@ __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int
   int* rows = (int*)(scr + S_ROW);
   const GraphInfo gi = p.ginfo[g];
   lds_i32* hdr = (lds_i32*)(int*)(scr + S_NBH);
+  // diagnostics (builds with -DMD_QPROF, md_profile with MD_VARIANT bit 8): per-piece device
+  // ticks of the tile items, summed over items in slots 20.. (8 per iteration)
+#ifdef MD_QPROF
+  unsigned long long* qd = p.prof != nullptr && (p.variant & 8) ? p.prof + 20 + 8 * (it - 1) : nullptr;
+  unsigned long long tqd = qd != nullptr ? wall_clock64() : 0ull;
+#else
+  constexpr unsigned long long* qd = nullptr;
+  unsigned long long tqd = 0ull;
+#endif
+#define QTS(k)                                                    \
+  do {                                                            \
+    if (qd != nullptr && threadIdx.x == 0) {                      \
+      const unsigned long long now_ = wall_clock64();             \
+      atomicAdd(qd + (k), now_ - tqd);                            \
+      tqd = now_;                                                 \
+    }                                                             \
+  } while (0)
   const int slot = gl * p.nbc_gstride + j;
   const bool cacheable = slot < p.nbc_slots && !(p.variant & 16);
   const bool cached = cacheable && it > 1;
@@ -1801,6 +1818,7 @@ __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int
     else if (threadIdx.x == 66) misc[59] = ch;
   }
   __syncthreads();
+  QTS(0);
   bool nb_ok;
   if (cached) {
     nb_ok = misc[59] != 0;
@@ -1816,13 +1834,17 @@ __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int
     nb_ok = !(p.variant & 16) && build_nb_lists(p, gi, rows, scr, nullptr, -1);
     if (cacheable) nbc_store(p, slot, scr, nb_ok);
   }
+  QTS(1);
   if (nb_ok) gather_tile2(p, gi, it, rows, scr);
   else gather_tile(p, gi, it, rows, scr);
   __syncthreads();
+  QTS(2);
   update_tile(lds + L_W, scr);
   __syncthreads();
+  QTS(3);
   normalize_tile(scr + S_E, scr);
   __syncthreads();
+  QTS(4);
   if (threadIdx.x < 128 && it < 3) {
     // tile partial sums of the virtual node (rows in ascending compact order from 0)
     const int l = threadIdx.x >> 6, c = threadIdx.x & 63;
@@ -1851,8 +1873,11 @@ __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int
     if (v >= 0) stc4(hb, v * 256 + q4 * 16, make_float4(e[0], e[LDT], e[2 * LDT], e[3 * LDT]));
   }
   __syncthreads();
+  QTS(5);
   // iteration 3: the graph head was published (tag 1) before this item was pushed
   if (it == 3) attention_q_tile(p, lds, scr, gi, g, rows, p.apart + (size_t)(gi.tile_off + j) * 4, 1ull, nullptr);
+  QTS(6);
+#undef QTS
 }
 
 // Virtual-node chain Y1..Y3 from the tile partial sums S0..S2 and the graph head of graph g,
@@ -1947,8 +1972,9 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
     if (qp != nullptr && threadIdx.x == 0) {
       ti = wall_clock64();
       atomicAdd(qp + 16, ti - tq);
-      // waiting time over the launch in 1.31 ms buckets (slots 20..63)
-      atomicAdd(qp + 20 + min(43, (int)((ti - tq0) >> 17)), ti - tq);
+      // waiting time over the launch in 1.31 ms buckets (slots 20..63; with MD_VARIANT bit 8
+      // those slots hold the tile-item pieces instead)
+      if (!(p.variant & 8)) atomicAdd(qp + 20 + min(43, (int)((ti - tq0) >> 17)), ti - tq);
       atomicAdd(qp + 8 + (kind & 7u), 1ull);
     }
     if (kind == QK_EXIT || kind == 0u) break;

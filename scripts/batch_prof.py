@@ -44,6 +44,13 @@ if len(P) and P[0, 0] == 1 and P[0, 9] > 0:
     npop = P[0, 9] + P[0, 10] + P[0, 11]
     print("  pops with the slot filled at the early read: %d of ~%d; mean backlog beyond the held ticket %.1f items" % (
         P[0, 18], npop, P[0, 19] / max(1, npop)))
+    if os.environ.get("MD_VARIANT", "0") != "0" and int(os.environ["MD_VARIANT"]) & 8:
+        names_t = ["header", "nb lists", "gather", "update", "normalize", "sums+stores", "attn+Q"]
+        for it in range(3):
+            row = P[0, 20 + 8 * it: 27 + 8 * it] / 1e5
+            cnt = max(1, {0: 1, 1: 1, 2: 1}[it])
+            print("  TILE it%d pieces (WG-ms): " % (it + 1) + "  ".join("%s %.1f" % (nm, v) for nm, v in zip(names_t, row)))
+        sys.exit(0)
     wb = P[0, 20:64] / 1e5
     nb_ = int(np.max(np.nonzero(wb)[0])) + 1 if np.any(wb) else 0
     print("  idle workgroups per 1.31 ms of the launch: " + " ".join("%.0f" % (w / 1.31) for w in wb[:nb_]))
