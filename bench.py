@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--batch-graphs", type=int, default=256, help="graphs per GPU of the batch object (0: skip)")
     ap.add_argument("--batch-steps", type=int, default=2)
+    ap.add_argument("--degree-steps", type=int, default=3, help="timed degree-cost rollouts (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-seconds", type=float, default=12.0)
     return ap.parse_args()
@@ -136,6 +137,48 @@ def roofline(flops_per_step, bytes_per_step, kernel_ms_per_step, launches_per_st
         "hbm_achieved_GBs": bytes_per_step / t / 1e9 if t > 0 else 0.0,
         "hbm_frac": (bytes_per_step / t / 1e9) / PEAK_HBM_GBS if t > 0 else 0.0,
     }
+
+
+def degree_object(args, edges):
+    """Degree-cost rollouts (D/MultiDismantler_torch.py GetSol, D/mvc_env.py reward) of the
+    seed-`seed` GMM graph: removals/s over `degree_steps` timed rollouts, the weighted score with the
+    reference's expression, and the match against the reference's own run of this graph
+    (tests/golden/rollout_deg_gmm1000_s0.npz, made by tests/golden/make_golden_degree.py)."""
+    from mdcommunity_amd import _lib, engine, graph as mgraph
+    # the D/ variant's own GMM generator (D/GMM.py, unlike U/GMM.py) made the reference's graph
+    # for this seed; its edges are the fixture
+    gpath = os.path.join(ROOT, "tests", "golden", "rollout_deg_gmm1000_s%d.npz" % args.seed)
+    z = np.load(gpath) if args.n == 1000 and os.path.exists(gpath) else None
+    if z is not None:
+        edges = (z["edges0"], z["edges1"])
+    g = mgraph.Graph_test.from_edges(args.n, edges[0], edges[1])
+    mgraph.ensure_degree_weights(g)
+    eng = _lib.Engine(engine.load_weights(engine.DEFAULT_DEGREE), cost_mode=_lib.MD_COST_DEGREE)
+    eng.load_graphs([(args.n,) + edges], node_w=mgraph.node_weight_array([g]))
+    run_steps(eng, 1)
+    t0 = time.perf_counter()
+    kms, nl, rem, last, _ = run_steps(eng, args.degree_steps)
+    dt = time.perf_counter() - t0
+    mr, outs = last
+    seq, ranks = outs[0]
+    eng.close()
+    tw0, tw1 = sum(g.weights[0].values()), sum(g.weights[1].values())
+    score = 0.0
+    for a, r in zip(seq.tolist(), ranks.tolist()):  # D/mvc_env.py:127-134
+        score += -1 * (-int(r) / int(mr[0]) * (g.weights[0][int(a)] / tw0 + g.weights[1][int(a)] / tw1) / 2.0)
+    out = {"workload": "degree-cost rollout, 2-layer GMM graph N=%d seed %d (%s), checkpoint D/models/"
+                       "nrange_30_50_iter_100000.ckpt" % (args.n, args.seed, "D/GMM.py, fixture" if z is not None
+                                                          else "U/GMM.py"),
+           "value": rem / dt, "unit": "removals/s", "steps": args.degree_steps,
+           "ms_per_step": dt / args.degree_steps * 1e3, "kernel_ms_per_step": kms / args.degree_steps,
+           "removals_per_step": rem / args.degree_steps, "score": score}
+    if z is not None:
+        amb = np.flatnonzero((z["step_stats"][:, 3] > 1) | (z["step_gap"] < 1e-6))
+        k = int(amb[0]) if amb.size else len(z["seq"])
+        out.update(score_match=abs(score - float(z["score"])) <= 1e-12 * max(1.0, abs(float(z["score"]))),
+                   seq_match=seq.tolist()[:k] == z["seq"].tolist()[:k], seq_checked_steps=k,
+                   reference_cpu_seconds_per_rollout=float(z["ref_seconds"]))
+    return out
 
 
 def main():
@@ -234,6 +277,12 @@ def main():
             "roofline": roofline(bflops, bbytes, bk_ms / args.batch_steps, bl / args.batch_steps, None),
         }
 
+    # ---------------- degree-cost variant (configs[3] shape: the D/ agent on a synthetic N=1000
+    # multiplex, the GMM seed-0 graph; real testReal inputs are absent), single graph, rank 0
+    degree = None
+    if rank == 0 and args.degree_steps > 0:
+        degree = degree_object(args, edges)
+
     if rank == 0:
         golden = None
         gpath = os.path.join(ROOT, "tests", "golden", f"rollout_gmm1000_s{args.seed}.npz")
@@ -285,6 +334,7 @@ def main():
             "pcie_inclusive_value": pcie_rate,
             "roofline": roofline(flops, nbytes, kernel_ms / max(1, args.steps), launches / max(1, args.steps), traffic),
             "batch": batch,
+            "degree": degree,
         }
         if world == 1 and not args.no_cpu_baseline and args.steps > 0:
             cb = cpu_baseline(edges, args.n, args.cpu_sample_seconds)
