@@ -23,7 +23,6 @@ constexpr int NBC_HDR = 80, NBC_LWORDS = NB_CAP_ENTRIES / 2, NBC_INTS = 2176;
 static_assert(NBC_HDR + 2 * NBC_LWORDS <= NBC_INTS, "cache slot");
 constexpr int XB_SLOTS = 256;
 constexpr int Q_CAP = 1 << 18;   // queue-mode ring slots (items in flight << Q_CAP)
-constexpr int Q_ADMIT_NUM = 3;  // queue mode: graphs running at once = Q_ADMIT_NUM / 8 of the workgroups
 
 // Offsets (floats) of each tensor in the packed weight blob (see include/mdroll.h).
 enum WOff : int {

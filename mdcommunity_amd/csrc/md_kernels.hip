@@ -1693,14 +1693,31 @@ __device__ __forceinline__ int tile_graph(const int* pref, int ng, int t) {
 // cannot deadlock; when the last graph stops, one EXIT item per workgroup is pushed.
 enum : unsigned { QK_ENV = 1, QK_TILE = 2, QK_VN = 3, QK_EXIT = 4 };
 enum : int { QC_HEAD = 0, QC_TAIL = 1, QC_REM = 2, QC_ADMIT = 3 };
-// Graphs running at once in queue mode: 3/8 of the workgroups (96 on 256 CUs; measured best
-// of 64..192 and all for 256 and 512 GMM N=1000 graphs).  MD_VARIANT bits 16+ override.
+// Graphs running at once in queue mode: the larger of 3/8 of the workgroups and 5/16 of the
+// launch's graphs (sweeps of 64..192 and all: 96 best for 256 GMM N=1000 graphs on 256 CUs,
+// 160 for 512).  MD_VARIANT bits 16+ override.
 __device__ __forceinline__ int q_admit(KParams& p) {
   const int v = (int)((unsigned)p.variant >> 16);
-  return v > 0 ? v : max(1, (int)(Q_ADMIT_NUM * gridDim.x) / 8);
+  return v > 0 ? v : max(1, max((int)(3 * gridDim.x) / 8, (5 * p.nglist) / 16));
 }
 __device__ __forceinline__ unsigned q_item(unsigned kind, int it, int gl, int j) {
   return kind | ((unsigned)it << 3) | ((unsigned)gl << 5) | ((unsigned)j << 15);
+}
+// Tile item i of a stage with nt tiles and tpi tiles per item: first tile j = i * tpi (bits
+// 15-29), the number of further tiles in bits 30-31 (they run back to back on one workgroup:
+// one stage signal and one pop for all of them).
+__device__ __forceinline__ unsigned q_item_tile(int it, int gl, int i, int nt, int tpi) {
+  const int j = i * tpi, extra = min(tpi, nt - j) - 1;
+  return q_item(QK_TILE, it, gl, j) | ((unsigned)extra << 30);
+}
+__device__ __forceinline__ int q_item_j(unsigned item) { return (int)((item >> 15) & 0x7fffu); }
+__device__ __forceinline__ int q_item_extra(unsigned item) { return (int)(item >> 30); }
+// Tiles per item: 2 (MD_VARIANT bits 9-10 = 1..3 override; sweep of 1..4 tiles x admission
+// 96..160 on 256 / 512 graphs: 2 best, -3 % / -5 % against 1).  Per-graph stage size word in
+// qg[2 gl + 1]: items of a tile stage | tiles << 16.
+__device__ __forceinline__ int q_tiles_per_item(KParams& p) {
+  const int f = (p.variant >> 9) & 3;
+  return f == 0 ? 2 : f;
 }
 // Pushes n items f(0..n-1); every thread of the workgroup calls it.
 template <class F>
@@ -1978,7 +1995,7 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
       atomicAdd(qp + 8 + (kind & 7u), 1ull);
     }
     if (kind == QK_EXIT || kind == 0u) break;
-    const int it = (int)((item >> 3) & 3u), gl = (int)((item >> 5) & 1023u), j = (int)(item >> 15);
+    const int it = (int)((item >> 3) & 3u), gl = (int)((item >> 5) & 1023u), j = q_item_j(item);
     const int g = p.glist[gl];
     if (kind == QK_ENV) {
       phase_a(p, g, it != 0, lds, false);
@@ -1993,9 +2010,9 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
         break;
       }
       if (st == ST_RUN) {
-        const int nt = (nl + TILE - 1) / TILE;
-        if (threadIdx.x == 0) stc(p.qg + 2 * gl + 1, nt);
-        q_push(p, nt, [&](int i) { return q_item(QK_TILE, 1, gl, i); }, bc);
+        const int nt = (nl + TILE - 1) / TILE, tpi = q_tiles_per_item(p), ni = (nt + tpi - 1) / tpi;
+        if (threadIdx.x == 0) stc(p.qg + 2 * gl + 1, ni | (nt << 16));
+        q_push(p, ni, [&](int i) { return q_item_tile(1, gl, i, nt, tpi); }, bc);
       } else if (st == ST_WAIT_HOST) {
         q_push(p, 1, [&](int) { return q_item(QK_ENV, 1, gl, 0); }, bc);  // poll again later
       } else {
@@ -2026,14 +2043,17 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
     int next = 0;
     if (kind == QK_TILE || (kind == QK_VN && it == 1)) {
       // a task of a stage: iteration-1/2/3 tiles; stage 2 also counts virtual-node part 1
-      if (kind == QK_TILE) queue_tile(p, lds, g, gl, it, j);
-      else queue_vn(p, lds, g, 1);
+      if (kind == QK_TILE) {
+        for (int k = 0; k <= q_item_extra(item); ++k) queue_tile(p, lds, g, gl, it, j + k);
+      } else {
+        queue_vn(p, lds, g, 1);
+      }
       const int stage = kind == QK_TILE ? it : 2;
       pre = q_peek(p, tk);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0) {
-        const int tasks = ldc(p.qg + 2 * gl + 1) + (stage == 2 ? 1 : 0);
+        const int tasks = (ldc(p.qg + 2 * gl + 1) & 0xffff) + (stage == 2 ? 1 : 0);
         const int old = __hip_atomic_fetch_add(p.qg + 2 * gl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old == tasks - 1) {
           stc(p.qg + 2 * gl, 0);
@@ -2050,16 +2070,16 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
       next = 4;
     }
     if (next != 0) {
-      const int nt = ldc(p.qg + 2 * gl + 1);
+      const int sz = ldc(p.qg + 2 * gl + 1), ni = sz & 0xffff, nt = sz >> 16, tpi = q_tiles_per_item(p);
       if (next == 1) {
-        q_push(p, nt + 1, [&](int i) { return i < nt ? q_item(QK_TILE, 2, gl, i) : q_item(QK_VN, 1, gl, 0); }, bc);
+        q_push(p, ni + 1, [&](int i) { return i < ni ? q_item_tile(2, gl, i, nt, tpi) : q_item(QK_VN, 1, gl, 0); }, bc);
       } else if (next == 2) {
         if (inline_cont) cont = q_item(QK_VN, 2, gl, 0);
         else q_push(p, 1, [&](int) { return q_item(QK_VN, 2, gl, 0); }, bc);
       } else if (next == 3) {
         if (inline_cont) cont = q_item(QK_ENV, 1, gl, 0);
         else q_push(p, 1, [&](int) { return q_item(QK_ENV, 1, gl, 0); }, bc);
-      } else q_push(p, nt, [&](int i) { return q_item(QK_TILE, 3, gl, i); }, bc);
+      } else q_push(p, ni, [&](int i) { return q_item_tile(3, gl, i, nt, tpi); }, bc);
     }
     if (qp != nullptr && threadIdx.x == 0) atomicAdd(qp + (kind == QK_TILE ? 4 + it : kind == QK_VN ? 2 + it : kind), (tq = wall_clock64()) - ti);
   }

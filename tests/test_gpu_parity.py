@@ -177,10 +177,11 @@ def test_shared_mode_batch_matches_dedicated(eng):
         assert (s.tolist(), r.tolist()) == single[i % 3], i
 
 
-@pytest.mark.parametrize("admit", [1, 4])
-def test_queue_admission_limit_matches_single(monkeypatch, admit):
+@pytest.mark.parametrize("admit,tpi", [(1, 2), (4, 1), (4, 3), (64, 2)])
+def test_queue_admission_limit_matches_single(monkeypatch, admit, tpi):
     """Queue mode starts only `admit` graphs and admits the next one whenever a graph stops
-    (MD_VARIANT bits 16+ set the limit): every rollout equals its single-graph rollout."""
+    (MD_VARIANT bits 16+ set the limit), and runs `tpi` tiles per work item (bits 9-10):
+    every rollout equals its single-graph rollout."""
     names = ["gmm200_s7", "er100", "er300_dense"]
     graphs = [(int(z["n_nodes"]), z["edges0"], z["edges1"]) for z in map(load_golden, names)]
     ref = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
@@ -193,7 +194,7 @@ def test_queue_admission_limit_matches_single(monkeypatch, admit):
             single.append((s.tolist(), r.tolist()))
     finally:
         ref.close()
-    monkeypatch.setenv("MD_VARIANT", str(admit << 16))
+    monkeypatch.setenv("MD_VARIANT", str((admit << 16) | (tpi << 9)))
     e = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
     try:
         e.load_graphs([graphs[i % 3] for i in range(18)])
