@@ -299,6 +299,51 @@ int select_actions(md_ctx* c, md_select_cb cb, void* user, int g, const std::vec
   return cb(user, g, qd.data(), n, nout, acts);
 }
 
+// K2 end-game request of graph g (md_kernels.hip, endgame_request): the row holds each live
+// node's partner (int bits), -inf elsewhere.  Runs every remaining step's pick as the per-step
+// protocol would: the masked double row with one common value at the live nodes,
+// np.argsort(-q)[0] by numpy's own routine, then the pick and its partner leave the live set.
+// Writes the picks to h_act and returns their count (-1 on a malformed request).
+int serve_endgame(md_ctx* c, Selector* sel, int g, int nlive, std::vector<double>& qd) {
+  const GraphInfo& gi = c->hinfo[g];
+  const volatile float* hq = c->h_q.h + gi.node_off;
+  thread_local std::vector<int> part;
+  part.assign(gi.n, -1);
+  qd.assign(gi.n, QMASK);
+  int live = 0;
+  for (int i = 0; i < gi.n; ++i) {
+    const float x = hq[i];
+    if (std::isinf(x)) continue;
+    int pt;
+    std::memcpy(&pt, &x, sizeof pt);
+    part[i] = pt;
+    qd[i] = -0.5;  // any common value above the mask: the picks depend only on the live set
+    ++live;
+  }
+  bool ok = live == nlive && live % 2 == 0;
+  for (int i = 0; ok && i < gi.n; ++i)
+    if (part[i] >= 0) ok = part[i] < gi.n && part[i] != i && part[part[i]] == i;
+  if (!ok) {
+    if (sel->err.empty()) sel->err = "graph " + std::to_string(g) + ": malformed end-game request";
+    return -1;
+  }
+  int k = 0;
+  int32_t a = -1;
+  while (live > 0) {
+    if (select_actions(c, sel->cb, sel->user, g, qd, gi.n, 1, &a) != 0 || a < 0 || a >= gi.n || part[a] < 0) {
+      if (sel->err.empty()) sel->err = "graph " + std::to_string(g) + ": end-game selection failed";
+      return -1;
+    }
+    c->h_act.h[gi.node_off + k++] = a;
+    qd[a] = QMASK;
+    qd[part[a]] = QMASK;
+    part[part[a]] = -1;
+    part[a] = -1;
+    live -= 2;
+  }
+  return k;
+}
+
 // Answers graph g's request `tag`: Q row (float, -inf = masked) -> the reference's masked
 // double row, the callback's actions into mapped memory, then the answer tag.
 void serve_request(md_ctx* c, Selector* sel, int g, unsigned tag, std::vector<double>& qd, std::vector<int32_t>& acts) {
@@ -330,6 +375,12 @@ void serve_request(md_ctx* c, Selector* sel, int g, unsigned tag, std::vector<do
     const float cmax = c->h_chk.h[2 * g];
     int cnt;
     std::memcpy(&cnt, c->h_chk.h + 2 * g + 1, sizeof cnt);
+    if (cnt < 0) {
+      k = serve_endgame(c, sel, g, -cnt, qd);
+      c->h_nact.h[g] = k;
+      __atomic_store_n(c->h_ans.h + g, tag, __ATOMIC_RELEASE);
+      return;
+    }
     if (mx != cmax || nt != cnt) {
       if (sel->err.empty()) {
         char b[200];
@@ -406,6 +457,10 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
     p.h_act = c->h_act.d;
     p.h_q = c->h_q.d;
     p.h_chk = c->h_chk.d;
+    // K2 end-games in one hand-shake: single-node steps picked by numpy's own argsort routine
+    // (the callback path keeps one request per step); MD_VARIANT bit 2048 turns it off
+    p.endgame = run_mode == RUN_ROLLOUT && c->tie_argsort != nullptr && sel->step == 1 &&
+                c->cost_mode == MD_COST_UNIT && !(c->variant & 2048);
   }
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   HIPCHK(c, launch_rollout(p, c->wimg.p, grid, c->stream));

@@ -135,6 +135,7 @@ struct Params {
   unsigned* qctl;                  // queue mode: {head ticket, tail ticket, running graphs}
   unsigned long long* qslot;       // queue mode: Q_CAP item slots {ticket + 1, item}
   int* qg;                         // queue mode: per graph slot {tiles done in the stage, tiles}
+  int endgame;                     // 1: the host runs K2 end-games in one hand-shake (see md_kernels.hip)
 };
 
 }  // namespace md

@@ -383,10 +383,15 @@ __device__ __noinline__ void host_request(KParams&, const GraphInfo gi, int g, i
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(p.h_req + g, host_tag(p, npred), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// End-game requests carry bit 15 (n < 32768, so npred + 1 never sets it).
+__device__ __forceinline__ unsigned host_tag_eg(KParams& p, int npred, bool endgame) {
+  return host_tag(p, npred) ^ (endgame ? 0x8000u : 0u);
+}
 // Thread 0 only: the host's answer to request `npred` of graph g, copied to p.pend.
 // Returns the number of actions, 0 when not answered yet, -1 on a bad answer.
-__device__ __forceinline__ int host_answer(KParams& p, const GraphInfo& gi, int g, int npred) {
-  if (__hip_atomic_load(p.h_ans + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != host_tag(p, npred)) return 0;
+__device__ __forceinline__ int host_answer(KParams& p, const GraphInfo& gi, int g, int npred, bool endgame = false) {
+  if (__hip_atomic_load(p.h_ans + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != host_tag_eg(p, npred, endgame))
+    return 0;
   const int k = __hip_atomic_load(p.h_nact + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (k <= 0 || k > gi.n) return -1;
   for (int i = 0; i < k; ++i)
@@ -395,15 +400,59 @@ __device__ __forceinline__ int host_answer(KParams& p, const GraphInfo& gi, int 
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return k;
 }
+// K2 end-game (unit cost): when every live node has residual degree 1 in both layers, the
+// graph is a set of disjoint pairs joined in both layers, every live node's Q is the same
+// number (same inputs, same arithmetic: checked on 676 such states of 40 GMM rollouts,
+// scripts/k2_check.py), and the reference's pick np.argsort(-q)[0] depends only on which
+// nodes are live.  Removing a node isolates its partner and leaves the other pairs as they
+// were, so the host can run every remaining step's pick in one hand-shake (the same numpy
+// routine on the same masked rows, live nodes at one value) instead of one forward pass and
+// one hand-shake per step.  The request row carries each live node's partner (int bits)
+// and -inf elsewhere; the tie-count word carries -n_live.
+__device__ __noinline__ void endgame_request(KParams&, const GraphInfo gi, int g, int npred, int nlive) {
+  KParams& p = kp();
+  const int* rp = p.rowptr[0] + gi.roff[0];
+  const int* adj = p.adj[0] + gi.coff[0];
+  const uint8_t* ca = p.calive[0] + gi.coff[0];
+  const int* deg = p.deg[0] + gi.node_off;
+  for (int x = threadIdx.x; x < gi.n; x += NTHREADS) {
+    float v = NEG_INF;
+    if (ldc(deg + x) > 0) {
+      int part = -1;
+      for (int i = rp[x]; i < rp[x + 1]; ++i)
+        if (ldc(ca + i)) {
+          part = adj[i];
+          break;
+        }
+      v = __int_as_float(part);
+    }
+    __hip_atomic_store(p.h_q + gi.node_off + x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(p.h_chk + 2 * g, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(p.h_chk + 2 * g + 1, __int_as_float(-nlive), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(p.h_req + g, host_tag_eg(p, npred, true), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ bool endgame_state(KParams& p, const GraphInfo& gi, const GraphVar& gv) {
+  return p.endgame && p.node_w == nullptr && gi.n < 32768 && gv.status == ST_RUN && gv.n_live > 0 &&
+         gv.dmax[0] == 1 && gv.dmax[1] == 1;
+}
+
 // Synchronous form (one graph per launch: nothing else could run meanwhile): request, then
 // wait for the answer.  Returns the number of actions (0 on error; the error word is set).
-__device__ __noinline__ int host_handshake(KParams&, const GraphInfo gi, int g, int npred, float qmax, int ntie, int* misc) {
+__device__ __noinline__ int host_handshake(KParams&, const GraphInfo gi, int g, int npred, float qmax, int ntie, int* misc,
+                                           bool endgame = false) {
   KParams& p = kp();
-  host_request(p, gi, g, npred, qmax, ntie);
+  if (endgame) endgame_request(p, gi, g, npred, ntie);
+  else host_request(p, gi, g, npred, qmax, ntie);
   if (threadIdx.x == 0) {
     const unsigned long long t0 = wall_clock64();
     int k;
-    while ((k = host_answer(p, gi, g, npred)) == 0) {
+    while ((k = host_answer(p, gi, g, npred, endgame)) == 0) {
       __builtin_amdgcn_s_sleep(2);
       if (wall_clock64() - t0 > HOST_TIMEOUT_TICKS) {
         k = -1;
@@ -433,7 +482,7 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
     // asynchronous hand-shake (several graphs per launch): the graph sat out the steps since
     // its request while the others went on; poll the host's answer once per step
     if (threadIdx.x == 0) {
-      int k = host_answer(p, gi, g, gv.npred);
+      int k = host_answer(p, gi, g, gv.npred, gv.ntie < 0);  // ntie < 0: an end-game request
       if (k == 0 && wall_clock64() - gv.t_req > HOST_TIMEOUT_TICKS) k = -1;
       if (k < 0) raise_err(p, ERR_HOST);
       misc[3] = k;
@@ -525,8 +574,8 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
     float* area = lds + L_W;
     const bool was_staged = staged && fits;
     staged = fits;
-    const int err = fits ? env_step<false>(p, gi, gv, area, pend_n, pend_first, lds, was_staged)
-                         : env_step<true>(p, gi, gv, area, pend_n, pend_first, lds, false);
+    int err = fits ? env_step<false>(p, gi, gv, area, pend_n, pend_first, lds, was_staged)
+                   : env_step<true>(p, gi, gv, area, pend_n, pend_first, lds, false);
     if (threadIdx.x == 0) {
       gv.npend = 0;
       if (err) raise_err(p, err);
@@ -534,6 +583,29 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
       if (term) gv.status = ST_TERMINAL;
       else if (p.run_mode == RUN_STEP) gv.status = ST_PAUSED;
       else gv.status = ST_RUN;
+    }
+    __syncthreads();
+    if (!err && p.run_mode == RUN_ROLLOUT && p.h_req != nullptr && endgame_state(p, gi, gv)) {
+      // K2 end-game: the host picks every remaining removal in one hand-shake (no forward
+      // pass for these steps, no prediction recorded)
+      if (p.nglist > 1) {
+        endgame_request(p, gi, g, gv.npred, gv.n_live);
+        if (threadIdx.x == 0) {
+          gv.status = ST_WAIT_HOST;
+          gv.ntie = -1;
+          gv.t_req = wall_clock64();
+        }
+      } else {
+        const int k = host_handshake(p, gi, g, gv.npred, 0.f, gv.n_live, misc, true);
+        if (k > 0) {
+          err = fits ? env_step<false>(p, gi, gv, area, k, -1, lds, true)
+                     : env_step<true>(p, gi, gv, area, k, -1, lds, false);
+          if (threadIdx.x == 0) {
+            if (err) raise_err(p, err);
+            gv.status = gv.alive[0] == 0 || gv.alive[1] == 0 ? ST_TERMINAL : ST_RUN;
+          }
+        }
+      }
     }
   }
   __syncthreads();

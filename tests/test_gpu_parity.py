@@ -272,3 +272,36 @@ def test_native_tie_selection_matches_callback():
             assert native == cb
     finally:
         e.close()
+
+
+def test_k2_endgame_in_one_handshake_matches_per_step(monkeypatch):
+    """Unit-cost rollouts that reach a K2 end-game (every live node in a pair joined in both
+    layers) let the host pick all remaining removals in one hand-shake; the rollouts equal the
+    per-step protocol's (MD_VARIANT bit 2048), single graphs and a queue-mode batch."""
+    names = ["gmm1000_s0", "gmm1000_s1", "gmm1000_s2", "er1000", "gmm200_s7", "er100"]
+    graphs = [(int(z["n_nodes"]), z["edges0"], z["edges1"]) for z in map(load_golden, names)]
+
+    def run(variant):
+        monkeypatch.setenv("MD_VARIANT", str(variant))
+        e = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
+        try:
+            out = []
+            for g in graphs:
+                e.load_graphs([g])
+                e.reset()
+                out.append([(s.tolist(), r.tolist()) for s, r in e.rollout()])
+                out.append([len(e.trace(0)["n_live"])])
+            e.load_graphs(graphs * 3)
+            e.reset()
+            out.append([(s.tolist(), r.tolist()) for s, r in e.rollout()])
+            return out
+        finally:
+            e.close()
+
+    fast, slow = run(0), run(2048)
+    for i in range(len(graphs)):
+        assert fast[2 * i] == slow[2 * i], names[i]
+        assert fast[2 * i + 1][0] <= slow[2 * i + 1][0]  # fewer forward passes recorded
+    assert fast[-1] == slow[-1]
+    # the GMM rollouts do end in K2 end-games: the shortcut skipped forward passes
+    assert fast[1][0] < slow[1][0]
