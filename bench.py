@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--batch-steps", type=int, default=2)
     ap.add_argument("--degree-steps", type=int, default=3, help="timed degree-cost rollouts (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-per-step", action="store_true", help="skip the per-step-protocol comparison rollouts")
     ap.add_argument("--cpu-sample-seconds", type=float, default=12.0)
     return ap.parse_args()
 
@@ -236,6 +237,27 @@ def main():
             eng.reset()
             prem += sum(len(o[0]) for o in eng.rollout())
         pcie_rate = prem / (time.perf_counter() - tp)
+    # the same rollouts with the K2 end-game shortcut off (every removal step runs its forward
+    # pass and, on a tie, its own host hand-shake; MD_VARIANT bit 2048): reported beside `value`
+    per_step_rate = None
+    if args.steps > 0 and not args.no_per_step:
+        old_v = os.environ.get("MD_VARIANT")
+        os.environ["MD_VARIANT"] = str(int(old_v or "0") | 2048)
+        try:
+            peng = _lib.Engine(weights, device=local if world > 1 else 0)
+        finally:
+            if old_v is None:
+                del os.environ["MD_VARIANT"]
+            else:
+                os.environ["MD_VARIANT"] = old_v
+        peng.load_graphs([(args.n,) + edges])
+        run_steps(peng, 1)
+        tp = time.perf_counter()
+        _, _, prem, plast, _ = run_steps(peng, args.steps)
+        per_step_rate = prem / (time.perf_counter() - tp)
+        if plast[1][0][0].tolist() != seq.tolist():
+            raise RuntimeError("per-step protocol rollout differs from the end-game shortcut's")
+        peng.close()
     tot_removals, max_elapsed = removals, elapsed
     if dist is not None:
         max_elapsed = parallel.max_over_ranks(dist, elapsed, dev)
@@ -332,6 +354,9 @@ def main():
             "launches_per_step": launches / max(1, args.steps),
             "predictions_per_step": preds,
             "pcie_inclusive_value": pcie_rate,
+            # K2 end-game picks run in one hand-shake; the same rollouts with one
+            # forward pass per removal step, same sequence checked:
+            "per_step_protocol_value": per_step_rate,
             "roofline": roofline(flops, nbytes, kernel_ms / max(1, args.steps), launches / max(1, args.steps), traffic),
             "batch": batch,
             "degree": degree,
