@@ -472,13 +472,22 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
     // requests are scanned continuously; the launch's completion event (a runtime call) only
     // every 20 us, and once more after the last scan that found it complete
     auto last = std::chrono::steady_clock::now();
+    const auto t_launch = last;
+    static const bool host_stats = std::getenv("MD_HOST_STATS") != nullptr;  // diagnostics
+    double serve_s = 0.0;
+    int n_served = 0;
     bool done = false;
     while (true) {
       bool served = false;
       for (int g : v) {
         const unsigned r = __atomic_load_n(c->h_req.h + g, __ATOMIC_ACQUIRE);
         if (r != 0 && r != __atomic_load_n(c->h_ans.h + g, __ATOMIC_RELAXED)) {
+          const auto ts = std::chrono::steady_clock::now();
           serve_request(c, sel, g, r, qd, acts);
+          if (host_stats) {
+            serve_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
+            ++n_served;
+          }
           served = true;
         }
       }
@@ -492,6 +501,9 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
       }
       if (c->poll_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(c->poll_us));
     }
+    if (host_stats)
+      std::fprintf(stderr, "md host: %d requests served in %.3f ms of a %.3f ms launch wait\n", n_served, 1e3 * serve_s,
+                   1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t_launch).count());
   }
   int dev_err = 0;
   HIPCHK(c, hipMemcpyAsync(&dev_err, c->ctl.p + CTL_ERR, sizeof(int), hipMemcpyDeviceToHost, c->stream));
