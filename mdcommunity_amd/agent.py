@@ -52,8 +52,8 @@ class MultiDismantler:
 
     def LoadModel(self, model_path):  # noqa: N802
         """Load a checkpoint (reference .ckpt via torch.load(weights_only=True), or .npz)."""
-        self._weights = _engine.load_weights(model_path)
-        self.model_file = _engine.resolve_model(model_path)
+        self.model_file = _engine.resolve_model(model_path, self.cost_mode)
+        self._weights = _engine.load_weights(self.model_file)
         if self._engine is not None:
             self._engine.set_weights(self._weights)
         print("restore model from file successfully")

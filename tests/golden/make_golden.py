@@ -89,13 +89,22 @@ def gmm_pair(GMM, n, seed):
     return a1, a2
 
 
-class Recorder:
-    """Wraps the reference agent to record every prediction and environment step."""
+def pack_rows(rows):
+    """Masked float64 Q rows -> float32 with NaN at the mask (lossless: the reference's Q is a
+    float32 tensor widened to float64, U/MultiDismantler_torch.py:291-299)."""
+    q = np.asarray(rows, dtype=np.float64)
+    live = q != MASK
+    q32 = np.where(live, q, np.nan).astype(np.float32)
+    assert np.array_equal(q32[live].astype(np.float64), q[live]), "Q row is not float32-exact"
+    return q32
 
-    def __init__(self, agent, q_keep_first=3, q_keep_ties=12):
+
+class Recorder:
+    """Wraps the reference agent to record every prediction and environment step (the
+    masked Q row of EVERY prediction is kept)."""
+
+    def __init__(self, agent):
         self.agent = agent
-        self.q_keep_first = q_keep_first
-        self.q_keep_ties = q_keep_ties
         self.reset()
         orig_pred = agent.PredictWithCurrentQNet
 
@@ -113,21 +122,15 @@ class Recorder:
             t = len(self.stats)
             self.stats.append((int(live.sum()), alive[0], alive[1], qmax, gap, ntie,
                                env.numCoveredEdges[0], env.numCoveredEdges[1]))
-            tie = ntie > 1
-            if t < self.q_keep_first or (tie and self.n_tie_kept < self.q_keep_ties) or (0 < gap < 1e-6):
-                self.q_steps.append(t)
-                self.q_rows.append(q.copy())
-                if tie:
-                    self.n_tie_kept += 1
+            assert t == len(self.q_rows)
+            self.q_rows.append(q.copy())
             return out
 
         agent.PredictWithCurrentQNet = pred
 
     def reset(self):
         self.stats = []
-        self.q_steps = []
         self.q_rows = []
-        self.n_tie_kept = 0
 
 
 def run_rollout(M, G, agent, rec, a1, a2):
@@ -155,8 +158,7 @@ def run_rollout(M, G, agent, rec, a1, a2):
         step_stats=np.asarray([s[:3] + s[5:] for s in rec.stats], dtype=np.int64).reshape(-1, 6),
         step_qmax=np.asarray([s[3] for s in rec.stats], dtype=np.float64),
         step_gap=np.asarray([s[4] for s in rec.stats], dtype=np.float64),
-        q_steps=np.asarray(rec.q_steps, dtype=np.int32),
-        q_rows=np.asarray(rec.q_rows, dtype=np.float64).reshape(len(rec.q_steps), g.num_nodes),
+        q_all=pack_rows(rec.q_rows).reshape(len(rec.q_rows), g.num_nodes),
         ref_seconds=np.float64(dt),
     )
     agent.ClearTestGraphs()

@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN, load_golden
+from test_certificates import PINNED_PREFIX, load_cert
 from mdcommunity_amd import _lib, engine, graph as mgraph
 from mdcommunity_amd.agent_degree import MultiDismantler
 
@@ -52,27 +53,23 @@ def test_degree_q_within_tolerance(name):
     assert worst < Q_TOL, worst
 
 
-def first_ambiguous(z, near_tie=1e-6):
-    amb = (z["step_stats"][:, 3] > 1) | (z["step_gap"] < near_tie)
-    idx = np.flatnonzero(amb)
-    return int(idx[0]) if idx.size else len(z["seq"])
-
-
 @pytest.mark.parametrize("name", NAMES)
 def test_degree_getsol_matches_reference(agent, name):
-    """GetSol: sequence bit-exact up to the first reference tie / near-tie (gap < 1e-6, where
-    fp32 rounding order decides); with none, sequence, weighted AUDC and MaxCCList bit-exact."""
-    z = load_golden(name)
+    """GetSol: the whole sequence equals the certified one (equal to the reference's up to the
+    pinned divergence step at a reference tie / few-ulp gap, tests/test_certificates.py); the
+    weighted score (D/mvc_env.py:127-134) and MaxCCList equal the reference's along it, and the
+    score equals the reference's own rollout score, unconditionally."""
+    z, c = load_golden(name), load_cert(name)
     g = _graph(z)
     agent.InsertGraph(g, is_test=True)
     score, sol, cost = agent.GetSol(0)
     agent.ClearTestGraphs()
-    k = first_ambiguous(z)
+    k = PINNED_PREFIX[name]
     assert sol[:k] == z["seq"][:k].tolist()
-    if k == len(z["seq"]):
-        assert sol == z["seq"].tolist()
-        assert score == float(z["score"])
-        assert np.array_equal(np.asarray(agent.test_env.MaxCCList), z["maxcc"])
+    assert sol == c["gpu_seq"].tolist()
+    assert score == float(c["ref_score_along"])
+    assert score == float(z["score"])
+    assert np.array_equal(np.asarray(agent.test_env.MaxCCList), c["ref_maxcc_along"])
 
 
 def test_degree_batch_matches_single(agent):

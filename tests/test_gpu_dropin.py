@@ -60,7 +60,6 @@ def test_predict_arbitrary_state(agent):
     q = agent.PredictWithCurrentQNet([g], [cov], [rem])[0]
     t = 1
     ref = z["q_rows"][list(z["q_steps"]).index(t)]
-    assert np.array_equal(q == ref, q == ref)
     live = ref != -(2147483647 / 2)
     assert np.array_equal(q != -(2147483647 / 2), live)
     assert np.max(np.abs(q[live] - ref[live])) < 1e-5

@@ -3,6 +3,7 @@ import os
 
 import networkx as nx
 import numpy as np
+import pytest
 
 from conftest import GOLDEN, ROOT
 from mdcommunity_amd import engine, graph as mgraph
@@ -67,8 +68,24 @@ def test_edges_in_nx_order_random():
 
 
 def test_reference_checkpoint_paths_resolve():
-    for key, npz in engine.KNOWN_CKPTS.items():
-        assert engine.resolve_model("./models/" + key).endswith(npz)
+    for (var, key), (npz, cost) in engine.KNOWN_CKPTS.items():
+        assert engine.resolve_model("./" + key).endswith(npz)
+        assert engine.resolve_model("./" + key, cost).endswith(npz)
+        assert engine.resolve_model(f"/somewhere/code/{var}/{key}", cost).endswith(npz)
+    # the degree checkpoint's file name under another variant directory is not it
+    for bad in ("/x/MultiDismantler_unit_cost/models/nrange_30_50_iter_100000.ckpt",
+                "/x/CEMultiDismantler/models/g0.5_TORCH-Model_GMM_30_50/nrange_30_50_iter_100000.ckpt",
+                "elsewhere/nrange_30_50_iter_100000.ckpt", "./models/unknown.ckpt"):
+        with pytest.raises(FileNotFoundError):
+            engine.resolve_model(bad)
+    # a checkpoint of the other cost model is refused, by reference path or shipped file
+    with pytest.raises(ValueError):
+        engine.resolve_model("./models/nrange_30_50_iter_100000.ckpt", engine._lib.MD_COST_UNIT)
+    with pytest.raises(ValueError):
+        engine.resolve_model(engine.DEFAULT_UNIT, engine._lib.MD_COST_DEGREE)
+    assert engine.resolve_model("./models/nrange_30_50_iter_100000.ckpt", engine._lib.MD_COST_DEGREE) == \
+        engine.DEFAULT_DEGREE
+    assert engine.resolve_model(None, engine._lib.MD_COST_DEGREE) == engine.DEFAULT_DEGREE
     w = engine.load_weights("./models/g0.5_TORCH-Model_GMM_30_50/nrange_30_50_iter_100000.ckpt")
     assert w.shape == (31205,) and w.dtype == np.float32
 

@@ -23,7 +23,8 @@ def weights_degree():
     return refmodel.RefWeights.load(engine.DEFAULT_DEGREE)
 
 
-@pytest.mark.parametrize("name", ["er100", "gmm200_s7", "er300_dense", "deg_er100", "deg_gmm200_s7"])
+@pytest.mark.parametrize("name", ["er100", "gmm200_s7", "er300_dense", "gmm1000_s0", "gmm1000_s1", "gmm1000_s2",
+                                  "er1000", "deg_er100", "deg_gmm200_s7", "deg_gmm1000_s0"])
 def test_rollout_matches_reference(weights, weights_degree, name):
     """Unit cost (U/) and degree cost (D/, fixtures of make_golden_degree.py)."""
     z = load_golden(name)
