@@ -160,6 +160,29 @@ md_status md_profile_read(md_ctx* ctx, uint64_t* out, int capacity_steps, int32_
 /* Library build string (arch, version). */
 const char* md_version(void);
 
+/*
+ * Diagnostic environment knobs, read once by md_create.  None changes any result (every
+ * combination is covered by the GPU tests, which check identical rollouts); they select
+ * between equivalent execution strategies for A/B measurement and for exercising fallbacks:
+ *   MD_VARIANT        bit mask, default 0:
+ *                       8     per-piece queue-mode profile stamps (md_profile; qprof build)
+ *                       16    no neighbour-list cache (every tile rebuilds its lists)
+ *                       32    lock-step shared mode instead of the device work queue (> 16 graphs)
+ *                       64    environment state in HBM even when it fits in LDS
+ *                       256   push single-item stages instead of running them inline (queue mode)
+ *                       512..1536 (bits 9-10 = 1..3)  tiles per queue work item (default 2)
+ *                       2048  K2 end-game shortcut off (one forward pass per removal step)
+ *                       bits 16+  queue-mode admission limit (graphs running at once)
+ *   MD_ENV_MODE       0: no dedicated environment workgroups for small batches (shared
+ *                     mode); default 1
+ *   MD_HOST_HANDSHAKE 0: end the launch on a tie and relaunch after the host selection
+ *                     (default 1: in-kernel hand-shake through mapped host memory)
+ *   MD_POLL_US        host-thread polling interval of the hand-shake (µs)
+ *   MD_H0G            0: rebuild the unit-cost first-layer tables per step instead of the
+ *                     precomputed per-dmax tables
+ *   MD_HOST_STATS     set: print hand-shake timing statistics to stderr
+ */
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,13 +1,24 @@
 #!/usr/bin/env python3
 """Summarise the rocprofv3 databases written by scripts/gpu_profile_round.sh.
 
-For each kernel-trace run: per-kernel calls / total / average / min / max duration (the
---stats view) from the rocpd SQLite output.  For the PMC passes: per-dispatch FETCH_SIZE and
-WRITE_SIZE of md_rollout_kernel, with the gfx950 correction of MI355X_MICROARCH.md (FETCH_SIZE
-reports half the bytes of wide coalesced reads: doubled; WRITE_SIZE taken as is), averaged
-per launch -> traffic.json.
+* kernel-trace runs (single/, batch/): per-kernel calls / total / average / min / max duration
+  (the --stats view) from the rocpd SQLite output;
+* PMC passes (pmc_<group>_<workload>/): per-dispatch counter values of the workload's main
+  kernel (md_rollout_kernel for the single graph, md_queue_kernel for the batch), averaged per
+  launch.
 
-Usage: python scripts/rocprof_summary.py gpurun_out/prof_r01
+Derived per launch (written to traffic.json, which bench.py reads when its `src_hash` equals the
+hash of the kernel sources being benchmarked):
+* HBM traffic: FETCH_SIZE x 2 (gfx950: FETCH_SIZE counts half the bytes of wide coalesced
+  reads, MI355X_MICROARCH.md HBM section) + WRITE_SIZE;
+* MFMA busy: SQ_VALU_MFMA_BUSY_CYCLES / (kernel cycles x 256 CUs x 4 SIMDs), kernel cycles =
+  GRBM_GUI_ACTIVE / 8 (rocprofv3 sums it over the 8 XCDs); and the executed MFMA rate
+  SQ_INSTS_VALU_MFMA_MOPS_F32 x 512 FLOP / kernel-trace duration against the 157.3 TFLOP/s
+  fp32 matrix peak (executed, not algorithmic, flops);
+* wave-state split: SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY over SQ_WAVE_CYCLES;
+* LDS bank conflicts: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE.
+
+Usage: python scripts/rocprof_summary.py gpurun_out/prof_r02
 """
 import glob
 import json
@@ -15,7 +26,9 @@ import os
 import sqlite3
 import sys
 
-KERNEL = "md_rollout_kernel"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+KERNELS = {"single": "md_rollout_kernel", "batch": "md_queue_kernel"}
+CUS, SIMDS, XCDS, PEAK_TF = 256, 4, 8, 157.3
 
 
 def dbs(d):
@@ -39,59 +52,86 @@ def kernel_stats(path):
     return out
 
 
-def pmc(path, counter, kernel):
+def pmc(path, kernel):
+    """{counter: [per-dispatch value (summed over instances)]} for dispatches of `kernel`."""
     cur = sqlite3.connect(path).cursor()
-    rows = list(cur.execute("select kernel_name, value, dispatch_id from counters_collection where counter_name = ?",
-                            (counter,)))
+    rows = list(cur.execute("select kernel_name, counter_name, value, dispatch_id from counters_collection"))
     per = {}
-    for name, val, disp in rows:
+    for name, cname, val, disp in rows:
         if kernel in name:
-            per[disp] = per.get(disp, 0.0) + float(val)  # KB, summed over any per-XCD instances
-    return [per[k] for k in sorted(per)]
+            d = per.setdefault(cname, {})
+            d[disp] = d.get(disp, 0.0) + float(val)
+    return {c: [v[k] for k in sorted(v)] for c, v in per.items()}
 
 
-def traffic_of(d, suffix, kernel, lines):
-    traffic = {}
-    for sub, counter in (("pmc_fetch" + suffix, "FETCH_SIZE"), ("pmc_write" + suffix, "WRITE_SIZE")):
-        for path in dbs(os.path.join(d, sub)):
-            vals = pmc(path, counter, kernel)
-            traffic[counter] = vals
-            lines.append(f"== {counter} per {kernel} dispatch (KB, raw): {[round(v, 1) for v in vals]}")
-    if not traffic.get("FETCH_SIZE") or not traffic.get("WRITE_SIZE"):
-        return None
-    f = traffic["FETCH_SIZE"]
-    w = traffic["WRITE_SIZE"]
-    fetch_b = 2.0 * 1024.0 * sum(f) / len(f)   # gfx950: FETCH_SIZE counts half of wide reads
-    write_b = 1024.0 * sum(w) / max(1, len(w))
-    out = {"kernel": kernel, "launches": len(f), "fetch_bytes_per_launch": fetch_b,
-           "write_bytes_per_launch": write_b, "hbm_bytes_per_launch": fetch_b + write_b,
-           "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); WRITE_SIZE as is; "
-                         "access widths other than 16 B/lane are uncalibrated"}
-    lines.append(f"== traffic per {kernel} launch: " + json.dumps(out))
+def mean(x):
+    return sum(x) / len(x) if x else None
+
+
+def workload(d, w, lines):
+    kernel = KERNELS[w]
+    out = {"kernel": kernel}
+    for path in dbs(os.path.join(d, w)):
+        st = kernel_stats(path)
+        lines.append(f"== {w}: kernel trace {os.path.relpath(path, d)}")
+        lines.append(f"{'kernel':60s} {'calls':>6s} {'total_ms':>10s} {'avg_us':>10s} {'min_us':>10s} {'max_us':>10s} workgroups")
+        for k, v in sorted(st.items(), key=lambda kv: -kv[1]["total_ns"]):
+            lines.append(f"{k[:60]:60s} {v['calls']:6d} {v['total_ns'] / 1e6:10.3f} {v['avg_ns'] / 1e3:10.1f} "
+                         f"{v['min_ns'] / 1e3:10.1f} {v['max_ns'] / 1e3:10.1f} {v['workgroups']}")
+            if kernel in k:
+                out["avg_ns"] = v["avg_ns"]
+    vals = {}
+    for group in ("fetch", "write", "sq1", "sq2"):
+        for path in dbs(os.path.join(d, f"pmc_{group}_{w}")):
+            for c, v in pmc(path, kernel).items():
+                vals[c] = v
+                lines.append(f"== {w} {c} per {kernel} dispatch (raw): {[round(x, 1) for x in v]}")
+    m = {c: mean(v) for c, v in vals.items()}
+    if m.get("FETCH_SIZE") is not None and m.get("WRITE_SIZE") is not None:
+        out["fetch_bytes_per_launch"] = 2.0 * 1024.0 * m["FETCH_SIZE"]
+        out["write_bytes_per_launch"] = 1024.0 * m["WRITE_SIZE"]
+        out["hbm_bytes_per_launch"] = out["fetch_bytes_per_launch"] + out["write_bytes_per_launch"]
+        out["correction"] = ("FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); WRITE_SIZE as is; access "
+                             "widths other than 16 B/lane are uncalibrated")
+    if m.get("SQ_VALU_MFMA_BUSY_CYCLES") is not None and m.get("GRBM_GUI_ACTIVE"):
+        cyc = m["GRBM_GUI_ACTIVE"] / XCDS
+        busy = {"mfma_busy_frac": m["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * CUS * SIMDS),
+                "kernel_cycles": cyc,
+                "mfma_busy_cycles": m["SQ_VALU_MFMA_BUSY_CYCLES"],
+                "mfma_f32_insts": m.get("SQ_INSTS_VALU_MFMA_F32"),
+                "mfma_f32_flops_executed": (m.get("SQ_INSTS_VALU_MFMA_MOPS_F32") or 0.0) * 512.0}
+        if out.get("avg_ns"):
+            busy["clock_ghz"] = cyc / out["avg_ns"]
+            tf = busy["mfma_f32_flops_executed"] / (out["avg_ns"] * 1e-9) / 1e12
+            busy["mfma_executed_tflops"] = tf
+            busy["mfma_executed_frac_of_peak"] = tf / PEAK_TF
+        wc = m.get("SQ_WAVE_CYCLES")
+        if wc:
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+                if m.get(c) is not None:
+                    busy[c.lower() + "_frac"] = m[c] / wc
+        if m.get("SQ_LDS_IDX_ACTIVE"):
+            busy["lds_bank_conflict_frac"] = (m.get("SQ_LDS_BANK_CONFLICT") or 0.0) / m["SQ_LDS_IDX_ACTIVE"]
+        for c in ("SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_VALU", "SQ_INSTS_SALU",
+                  "SQ_VALU_MFMA_COEXEC_CYCLES", "SQ_BUSY_CYCLES"):
+            if m.get(c) is not None:
+                busy[c.lower()] = m[c]
+        out["mfma_busy"] = busy
+    lines.append(f"== {w} per-launch summary: " + json.dumps(out))
     return out
 
 
 def main():
+    import bench
     d = sys.argv[1]
-    report = {}
-    lines = []
-    for sub in ("single", "batch"):
-        for path in dbs(os.path.join(d, sub)):
-            st = kernel_stats(path)
-            report[sub] = {k: {kk: vv for kk, vv in v.items()} for k, v in st.items()}
-            lines.append(f"== {sub}: {path}")
-            lines.append(f"{'kernel':60s} {'calls':>6s} {'total_ms':>10s} {'avg_us':>10s} {'min_us':>10s} {'max_us':>10s} workgroups")
-            for k, v in sorted(st.items(), key=lambda kv: -kv[1]["total_ns"]):
-                lines.append(f"{k[:60]:60s} {v['calls']:6d} {v['total_ns'] / 1e6:10.3f} {v['avg_ns'] / 1e3:10.1f} "
-                             f"{v['min_ns'] / 1e3:10.1f} {v['max_ns'] / 1e3:10.1f} {v['workgroups']}")
-    single = traffic_of(d, "", KERNEL, lines)
-    batch = traffic_of(d, "_batch", "md_queue_kernel", lines)
-    if single is not None:
-        out = dict(single)
-        if batch is not None:
-            out["batch"] = batch
-        with open(os.path.join(d, "traffic.json"), "w") as fo:
-            json.dump(out, fo, indent=1)
+    lines = [f"kernel sources hash {bench.kernel_src_hash()}"]
+    report = {w: workload(d, w, lines) for w in ("single", "batch")}
+    out = dict(report["single"])
+    out["batch"] = report["batch"]
+    out["src_hash"] = bench.kernel_src_hash()
+    out["source"] = f"rocprofv3 PMC passes, {os.path.basename(os.path.normpath(d))} (scripts/gpu_profile_round.sh)"
+    with open(os.path.join(d, "traffic.json"), "w") as fo:
+        json.dump(out, fo, indent=1)
     with open(os.path.join(d, "summary.txt"), "w") as fo:
         fo.write("\n".join(lines) + "\n")
     print("\n".join(lines))

@@ -1,0 +1,116 @@
+"""GPU correctness of the batched configurations at full size (BASELINE.json configs[2] and the
+per-GPU slice of configs[4]): 256 and 512 two-layer GMM graphs N=1000 (generator seeds 0..255 /
+0..511, mdcommunity_amd.gmm = the reference's U/GMM.py streams) rolled out in ONE
+md_queue_kernel launch (work queue, admission limit, two tiles per work item, asynchronous tie
+hand-shakes, K2 end-games) — the launch behind bench.py's `batch` object.
+
+Every graph's (removal sequence, LMCC trace) must equal its own single-graph rollout
+(md_rollout_kernel, dedicated mode), and seeds 0-2 must reproduce the certified sequences and
+the reference's bit-exact AUDC (tests/test_certificates.py).  Per-graph semantics are
+single-graph semantics: the reference's Predict batching quirk is not
+replicated.
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from test_certificates import PINNED_PREFIX, load_cert
+from mdcommunity_amd import _lib, engine, gmm
+
+pytestmark = pytest.mark.gpu
+
+N = 1000
+
+
+def audc(ranks, max_rank, n):
+    s = 0.0
+    for r in ranks:
+        s += -1 * (-float(r) / (max_rank * float(n)))  # U/mvc_env.py:86,133-137
+    return s
+
+
+@pytest.fixture(scope="module")
+def graphs():
+    return [(N,) + gmm.gmm_pair(N, seed=s) for s in range(512)]
+
+
+@pytest.fixture(scope="module")
+def weights():
+    return engine.load_weights(engine.DEFAULT_UNIT)
+
+
+@pytest.fixture(scope="module")
+def single(graphs, weights):
+    """Single-graph rollouts (dedicated mode, one launch per graph) of every seed."""
+    eng = _lib.Engine(weights)
+    out = []
+    for g in graphs:
+        eng.load_graphs([g])
+        mr = int(eng.reset()[0])
+        seq, ranks = eng.rollout()[0]
+        out.append((mr, seq.copy(), ranks.copy()))
+    eng.close()
+    return out
+
+
+def batch_rollout(weights, graphs):
+    eng = _lib.Engine(weights)
+    eng.load_graphs(graphs)
+    mr = eng.reset().copy()
+    outs = eng.rollout()
+    _, launches = eng.last_timing()
+    eng.close()
+    return mr, outs, launches
+
+
+def check_against_single(mr, outs, single, lo):
+    bad = []
+    for i, ((seq, ranks), m) in enumerate(zip(outs, mr)):
+        smr, sseq, sranks = single[lo + i]
+        if int(m) != smr or seq.tolist() != sseq.tolist() or ranks.tolist() != sranks.tolist():
+            bad.append(lo + i)
+    assert not bad, f"{len(bad)} graphs differ from their single-graph rollout, seeds {bad[:10]}"
+
+
+def check_goldens(mr, outs):
+    for s in range(3):
+        name = f"gmm1000_s{s}"
+        z, c = load_golden(name), load_cert(name)
+        seq, ranks = outs[s]
+        assert int(mr[s]) == int(z["max_rank"])
+        assert seq.tolist() == c["gpu_seq"].tolist(), name
+        k = 0
+        while k < min(len(seq), len(z["seq"])) and seq[k] == z["seq"][k]:
+            k += 1
+        assert k == PINNED_PREFIX[name]
+        assert ranks.tolist() == c["ref_ranks_along"].tolist()
+        assert audc(ranks, int(mr[s]), N) == float(z["score"])  # bit-exact
+
+
+@pytest.mark.timeout(240)
+def test_c3_256_graphs_one_queue_launch(graphs, weights, single):
+    """configs[2]: 256 graphs in one queue-mode launch == 256 single-graph rollouts."""
+    mr, outs, launches = batch_rollout(weights, graphs[:256])
+    assert launches == 1
+    assert sum(len(s) for s, _ in outs) > 256 * 20
+    check_against_single(mr, outs, single, 0)
+    check_goldens(mr, outs)
+
+
+@pytest.mark.timeout(240)
+def test_c5_slice_512_graphs_one_queue_launch(graphs, weights, single):
+    """configs[4]'s per-GPU slice: 512 graphs (G_CAP) in one launch == single-graph rollouts."""
+    mr, outs, launches = batch_rollout(weights, graphs)
+    assert launches == 1
+    check_against_single(mr, outs, single, 0)
+    check_goldens(mr, outs)
+
+
+@pytest.mark.timeout(240)
+def test_shard_blocks_equal_whole(graphs, weights, single):
+    """A contiguous shard (what rank 1 of 2 owns of the 512-graph C5 slice) rolled out alone
+    gives the same per-graph results as inside the whole batch: no cross-graph coupling."""
+    from mdcommunity_amd import parallel
+    lo, hi = parallel.shard(512, 1, 2)
+    mr, outs, _ = batch_rollout(weights, graphs[lo:hi])
+    check_against_single(mr, outs, single, lo)

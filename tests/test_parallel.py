@@ -82,3 +82,46 @@ def test_gloo_world2_gather_equals_single_process():
     assert rem == [r for _, r in ref]
     assert tot == sum(rem)
     assert mx == 1.0
+
+
+def _bench(*extra):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--cpu-dry-run", "--n", "40", "--steps", "1",
+           "--warmup", "0", "--batch-steps", "1", "--degree-steps", "0", "--no-cpu-baseline"] + list(extra)
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=240, env=env).stdout
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(300)
+def test_bench_launcher_world2_gathers_like_one_process():
+    """`bench.py --gpus 2` (no torchrun) launches two rank processes itself; they shard the
+    batch seeds, gather per-graph AUDC and removal counts and take the max time over ranks —
+    through the bench's own launcher, rank body, shard and gather code (gloo + the host stub
+    engine in place of the device).  The gathered lists must equal a one-process run."""
+    two = _bench("--gpus", "2", "--batch-graphs", "3")
+    one = _bench("--gpus", "1", "--batch-graphs", "6")
+    assert two["n_gpus"] == 2 and two["rccl_world"] == 2 and two["backend"] == "gloo"
+    assert one["n_gpus"] == 1 and one["rccl_world"] == 1
+    b2, b1 = two["batch"], one["batch"]
+    assert b2["graphs"] == 6 and b2["graphs_rank0"] == 3
+    assert b2["audc_all"] == b1["audc_all"] and b2["removals_all"] == b1["removals_all"]
+    assert b2["removals_per_step"] == sum(b1["removals_all"])
+    # weak scaling of the headline: each rank runs its own replica
+    assert two["config"]["removals_per_step"] == 2 * one["config"]["removals_per_step"]
+
+
+@pytest.mark.timeout(300)
+def test_batch_cpu_baseline_pool():
+    """The batch CPU baseline's process pool (P x 1-thread oracle rollouts over the batch's
+    first seeds) runs and reports what it sampled."""
+    import bench
+    cb = bench.cpu_baseline_batch(60, 2, graphs_per_proc=1)
+    assert cb["cores"] == 2 and cb["kind"] == "port" and cb["value"] > 0
+    assert "2 GMM N=60 graphs" in cb["sample"]
