@@ -125,6 +125,13 @@ md_status md_rollout(md_ctx* ctx, int step, int32_t* seq_out, int32_t* lmcc_out,
 md_status md_rollout_trace(md_ctx* ctx, int graph, int32_t* n_live, int32_t* m0, int32_t* m1,
                            int32_t* n_tie, float* qmax, float* gap, int32_t* n_pred);
 
+/* Speculative environment steps of the last md_rollout for graph g: removals whose mutual-LMCC
+ * fixed point was taken from a speculative workgroup (hits) out of all removals.  A
+ * single-graph rollout runs up to MD_SPEC (default 16) extra workgroups on CUs it leaves
+ * free; each runs the next step's fixed point for one likely next removal while the tiles
+ * compute Q.  Results never depend on it (diagnostics). */
+md_status md_spec_stats(md_ctx* ctx, int graph, int32_t* hits, int32_t* removals);
+
 /* Read back the environment state of graph g (MvcEnv attributes, U/mvc_env.py:8-29):
  * covered[n] (0/1), removed_l[e_l] (1 = pruned by MCC, i.e. in remove_edge[l]),
  * counters[6] = {numCoveredEdges[0], numCoveredEdges[1], |removed0|, |removed1|, lmcc, terminal}. */
@@ -149,11 +156,11 @@ md_status md_last_timing(md_ctx* ctx, double* kernel_ms, int32_t* launches);
 
 /* Diagnostics: record device wall-clock (100 MHz) phase timestamps of workgroup 0,
  * MD_PROF_SLOTS slots per removal step (0-15 timestamps, 16-31 accumulated sub-phase
- * durations and counters of the environment step), for up to `steps` steps per launch of the
+ * durations and counters of the environment step, 64-72 speculative-step timeline), for up to `steps` steps per launch of the
  * following calls (0 disables).
  * md_profile_read copies the timestamps accumulated since md_profile was called and returns
  * the number of steps recorded in *n_steps. */
-#define MD_PROF_SLOTS 64
+#define MD_PROF_SLOTS 96
 md_status md_profile(md_ctx* ctx, int steps);
 md_status md_profile_read(md_ctx* ctx, uint64_t* out, int capacity_steps, int32_t* n_steps);
 
@@ -181,6 +188,8 @@ const char* md_version(void);
  *   MD_H0G            0: rebuild the unit-cost first-layer tables per step instead of the
  *                     precomputed per-dmax tables
  *   MD_HOST_STATS     set: print hand-shake timing statistics to stderr
+ *   MD_SPEC           speculative environment workgroups of a single-graph rollout (0..32,
+ *                     default 16, 0 = off; md_spec_stats)
  */
 
 #ifdef __cplusplus

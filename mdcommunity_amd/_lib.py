@@ -19,12 +19,12 @@ MD_WEIGHT_FLOATS = 31205
 STATUS_NAMES = {1: "MD_EINVAL", 2: "MD_EHIP", 3: "MD_EOOM", 4: "MD_ESTATE", 5: "MD_ETIMEOUT", 6: "MD_ECALLBACK"}
 
 # Every symbol include/mdroll.h declares (checked by tests/test_abi.py).
-PROF_SLOTS = 64  # MD_PROF_SLOTS in include/mdroll.h
+PROF_SLOTS = 96  # MD_PROF_SLOTS in include/mdroll.h
 
 EXPORTS = ("md_create", "md_destroy", "md_last_error", "md_set_weights", "md_load_graphs", "md_reset",
            "md_predict", "md_step", "md_rollout", "md_rollout_trace", "md_get_state", "md_set_state",
            "md_set_team_size", "md_set_tie_argsort", "md_last_timing", "md_profile", "md_profile_read",
-           "md_version")
+           "md_version", "md_spec_stats")
 
 _i32p = ctypes.POINTER(ctypes.c_int32)
 _i64p = ctypes.POINTER(ctypes.c_int64)
@@ -65,6 +65,7 @@ def load_library(path=LIB_PATH):
         "md_step": (ctypes.c_int, [vp, _i32p, _i32p, _u8p]),
         "md_rollout": (ctypes.c_int, [vp, ctypes.c_int, _i32p, _i32p, _i32p, SELECT_CB_ADDR, vp]),
         "md_rollout_trace": (ctypes.c_int, [vp, ctypes.c_int, _i32p, _i32p, _i32p, _i32p, _f32p, _f32p, _i32p]),
+        "md_spec_stats": (ctypes.c_int, [vp, ctypes.c_int, _i32p, _i32p]),
         "md_get_state": (ctypes.c_int, [vp, ctypes.c_int, _u8p, _u8p, _u8p, _i32p]),
         "md_set_state": (ctypes.c_int, [vp, ctypes.c_int, _u8p, _u8p, _u8p]),
         "md_set_team_size": (ctypes.c_int, [vp, ctypes.c_int]),
@@ -234,6 +235,13 @@ class Engine:
                                               _ptr(gp, _f32p), ctypes.byref(npred)))
         k = npred.value
         return dict(n_live=arrs[0][:k], m0=arrs[1][:k], m1=arrs[2][:k], n_tie=arrs[3][:k], qmax=qm[:k], gap=gp[:k])
+
+    def spec_stats(self, g):
+        """(removals whose fixed point came from a speculative workgroup, removals) of graph g
+        in the last rollout (diagnostics; md_spec_stats)."""
+        hits, rem = ctypes.c_int32(), ctypes.c_int32()
+        self._check(self.lib.md_spec_stats(self.h, int(g), ctypes.byref(hits), ctypes.byref(rem)))
+        return hits.value, rem.value
 
     def get_state(self, g):
         n = int(self.n_nodes[g])

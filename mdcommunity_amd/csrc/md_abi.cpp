@@ -25,6 +25,7 @@ namespace md {
 int lds_bytes();
 int weight_image_floats();
 bool phase_a_fits_lds_host(int n, int edges);
+bool spec_fits_lds_host(int n, int edges);
 void build_weight_image(const float* w, float* img);
 hipError_t launch_rollout(const Params& p, const float* wimg, int grid, hipStream_t s);
 hipError_t launch_h0(const float* w, float* tab, int dm_lo, int dm_hi, hipStream_t s);
@@ -109,7 +110,13 @@ struct md_ctx {
   DevBuf<int> nbc;  // neighbour-list cache slots (tiles of the largest launch)
   int nbc_slots = 0, nbc_gstride = 0;
   DevBuf<unsigned long long> qslot;  // queue-mode work items
-  DevBuf<int> qg;                    // queue-mode per-graph stage counters  // layer-split hand-off of iteration-3 embeddings
+  DevBuf<int> qg;                    // queue-mode per-graph stage counters
+  // speculative environment steps (single-graph rollouts): result slots, Q of the last two
+  // predictions; spec_n workgroups per launch when the CUs are free (MD_SPEC, default 16, 0 = off)
+  DevBuf<int> sres;
+  DevBuf<float> qspec;
+  int sres_stride = 0;
+  int spec_n = 16;  // layer-split hand-off of iteration-3 embeddings
   unsigned launch_seq = 0;
   // host selection hand-shake
   int host_mode = 1;
@@ -147,6 +154,7 @@ struct md_ctx {
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
     tr_stat.release(); glist.release(); ctl.release(); q.release(); spart.release();
     apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); nbc.release(); qslot.release(); qg.release(); tr_q.release(); node_w.release();
+    sres.release(); qspec.release();
     h_req.release(); h_ans.release(); h_nact.release(); h_act.release(); h_q.release(); h_chk.release();
     ng = 0;
     hinfo.clear();
@@ -174,7 +182,8 @@ md_status fail(md_ctx* c, md_status s, const char* fmt, ...) {
   } while (0)
 
 // Control block layout (ints): [0] barrier counter, [1] error word (zeroed before each launch).
-constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_Q = 2, CTL_WORDS = 8;
+constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_Q = 2, CTL_SPEC = 8, CTL_WORDS = 12;
+constexpr int SPEC_MAX = 32;  // speculative workgroups per launch at most  // CTL_SPEC: u64 request word
 
 Params make_params(md_ctx* c) {
   Params p{};
@@ -426,6 +435,12 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
   // lock-step shared mode instead), one workgroup per CU
   const bool qmode = run_mode == RUN_ROLLOUT && n_env == 0 && !(c->variant & 32);
   const int grid = qmode ? c->cus : grid_size(c, v, n_env);
+  // speculative environment workgroups on the CUs a single-graph rollout leaves free
+  // (single-node steps only: step > 1 takes several removals per prediction)
+  const int n_spec = run_mode == RUN_ROLLOUT && n_env == 1 && ngl == 1 && !host_select && c->sres.p != nullptr &&
+                             spec_fits_lds_host(c->hinfo[gl[0]].n, c->hinfo[gl[0]].e[0] + c->hinfo[gl[0]].e[1])
+                         ? std::max(0, std::min(c->spec_n, c->cus - grid))
+                         : 0;
   HIPCHK(c, hipMemcpyAsync(c->glist.p, gl, sizeof(int) * ngl, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->ctl.p, 0, sizeof(int) * CTL_WORDS, c->stream));
   // graph-head hand-off granules carry the step as their tag: stale tags from earlier launches
@@ -438,6 +453,15 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
     HIPCHK(c, hipMemsetAsync(c->qg.p, 0, sizeof(int) * c->qg.n, c->stream));
   }
   Params p = make_params(c);
+  p.n_main = grid;
+  p.n_spec = n_spec;
+  if (n_spec > 0) {
+    p.spec_req = (unsigned long long*)(c->ctl.p + CTL_SPEC);
+    p.sres = c->sres.p;
+    p.sres_stride = c->sres_stride;
+    p.qspec = c->qspec.p;
+    p.qspec_n = (int)c->tot_n;
+  }
   p.qmode = qmode ? 1 : 0;
   p.nglist = ngl;
   p.n_env = n_env;
@@ -463,7 +487,7 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
                 c->cost_mode == MD_COST_UNIT && !(c->variant & 2048);
   }
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-  HIPCHK(c, launch_rollout(p, c->wimg.p, grid, c->stream));
+  HIPCHK(c, launch_rollout(p, c->wimg.p, grid + n_spec, c->stream));
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
   if (hs) {
     // serve selection requests while the launch runs
@@ -575,6 +599,7 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_HOST_HANDSHAKE")) c->host_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_POLL_US")) c->poll_us = std::atoi(v);
   if (const char* v = std::getenv("MD_H0G")) c->h0g_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MD_SPEC")) c->spec_n = std::max(0, std::min(SPEC_MAX, std::atoi(v)));
   md_status st = MD_OK;
   do {
     if (hipSetDevice(device) != hipSuccess) { st = MD_EHIP; break; }
@@ -819,6 +844,15 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->qslot.alloc(Q_CAP));
   HIPCHK(c, c->qg.alloc(2 * G_CAP));
   {
+    // speculative-step slots: killed-edge lists of one graph (LDS-mode graphs only)
+    int maxe = 0;
+    for (int g = 0; g < n_graphs; ++g) maxe = std::max(maxe, info[g].e[0] + info[g].e[1]);
+    c->sres_stride = ((SRES_HDR + maxe + 63) / 64) * 64;
+    HIPCHK(c, c->sres.alloc((size_t)SPEC_MAX * c->sres_stride));
+    HIPCHK(c, hipMemset(c->sres.p, 0, sizeof(int) * (size_t)SPEC_MAX * c->sres_stride));
+    HIPCHK(c, c->qspec.alloc(2 * tn));
+  }
+  {
     int maxn = 0;
     for (int g = 0; g < n_graphs; ++g) maxn = std::max(maxn, (int)n_nodes[g]);
     md_status st = ensure_h0g(c, maxn - 1, false);
@@ -970,6 +1004,13 @@ md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, i
   if (lmcc_out) HIPCHK(c, hipMemcpy(lmcc_out, c->tr_rank.p, sizeof(int) * c->tot_n, hipMemcpyDeviceToHost));
   if (seq_len)
     for (int g = 0; g < c->ng; ++g) seq_len[g] = c->hvar[g].steps;
+  return MD_OK;
+}
+
+md_status md_spec_stats(md_ctx* c, int graph, int32_t* hits, int32_t* removals) {
+  if (!c || graph < 0 || graph >= c->ng) return MD_EINVAL;
+  if (hits) *hits = c->hvar[graph].spec_hits;
+  if (removals) *removals = c->hvar[graph].steps;
   return MD_OK;
 }
 

@@ -15,7 +15,7 @@ constexpr int BP_ITERS = 3;      // max_bp_iter, :62
 constexpr int NTHREADS = 512;    // 8 waves: waves 0-3 work on layer 0, waves 4-7 on layer 1
 constexpr int TILE = 16;         // node rows per MFMA tile (v_mfma_f32_16x16x4_f32)
 constexpr int G_CAP = 512;       // graphs per kernel launch (the host chunks larger batches)
-constexpr int PROF_SLOTS = 64;
+constexpr int PROF_SLOTS = 96;
 constexpr int NB_CAP_ENTRIES = 2052;   // alive neighbour entries per layer kept for a tile (NB_CAP)
 // neighbour-list cache slot: header (off[2][16], cnt[2][16], tot[2], ok) then per layer the u16
 // entries packed two per int
@@ -75,6 +75,7 @@ struct GraphVar {            // mutable per-graph state
   float qmax, gap;           // last prediction: best Q and top-2 gap
   int hdmax[2];              // dmax the unit-cost first-layer table was built for (0 = none)
   unsigned long long t_req;  // ST_WAIT_HOST: device wall clock of the pending host request
+  int spec_hits;             // removals whose fixed point came from a speculative workgroup
 };
 
 struct Params {
@@ -136,6 +137,26 @@ struct Params {
   unsigned long long* qslot;       // queue mode: Q_CAP item slots {ticket + 1, item}
   int* qg;                         // queue mode: per graph slot {tiles done in the stage, tiles}
   int endgame;                     // 1: the host runs K2 end-games in one hand-shake (see md_kernels.hip)
+  // speculative environment steps (single-graph rollouts, md_kernels.hip spec_loop): workgroups
+  // [n_main, n_main + n_spec) precompute the next step's mutual-LMCC cascade for the likely
+  // next removals while the tiles compute Q; the grid barrier counts the n_main others only
+  int n_main;                      // workgroups taking part in the grid barrier
+  int n_spec;                      // speculative workgroups after them (0: off)
+  unsigned long long* spec_req;    // request {previous-Q buffer << 32 | request tag}; SPEC_EXIT ends the loop
+  int* sres;                       // per speculative workgroup: result slot of sres_stride ints
+  int sres_stride;
+  float* qspec;                    // [2][qspec_n]: Q of the last two predictions (never masked)
+  int qspec_n;                     // total nodes of the loaded batch
 };
+
+// Speculative-step result slot (ints): [0..1] u64 done tag {nd << 48 | candidate << 32 |
+// request tag} written last; [2] LMCC, [3..4] pruned edges per layer, [5..6] covered edges per
+// layer, [7] killed edges nd; [8..9] u64 started tag {candidate << 32 | request tag} written
+// when the workgroup takes its candidate; [16 .. 16 + nd) killed edge (LDS id) | state << 16.
+constexpr int SRES_HDR = 16, SRES_STARTED = 8;
+constexpr unsigned long long SPEC_EXIT = ~0ull;
+__host__ __device__ inline unsigned spec_tag(unsigned launch_seq, int steps) {
+  return ((launch_seq & 0xffffu) << 16) | ((unsigned)steps & 0xffffu);
+}
 
 }  // namespace md

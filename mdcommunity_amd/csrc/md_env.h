@@ -473,14 +473,10 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
 // the unit-cost first-layer table.  Returns 0 or an ERR_* code.
 // Not inlined: the environment step has its own register allocation (inlined, it raised the
 // register pressure of the whole rollout loop -- spills in the tile phases).
+// View of graph gi's environment arrays: LDS mode places them in the phase-A area `ia`
+// (env_layout), global mode uses the HBM arrays (and gscr for the union-find / degrees).
 template <bool GL>
-__device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, float*, int pend_n,
-                        int pend_first, const float*, bool staged) {
-  KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
-  // LDS from the kernel's dynamic-LDS base (compile-time addresses, ds_* accesses)
-  const float* const lds_base = md::lds_base();
-  GraphVar& gv = *(GraphVar*)(md::lds_base() + L_GV);
-  float* const area = md::lds_base() + L_W;
+__device__ __forceinline__ EnvView<GL> env_view(KParams& p, const GraphInfo& gi, int* ia) {
   const int n = gi.n, e0 = gi.e[0], e1 = gi.e[1], et = e0 + e1;
   EnvView<GL> E;
   E.gi = &gi;
@@ -496,7 +492,6 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
     E.grp[l] = p.rowptr[l] + gi.roff[l];
   }
   E.gcov = p.covered + gi.node_off;
-  int* ia = (int*)area;
   if constexpr (GL) {
     int* gs = p.gscr + 4 * (size_t)gi.node_off;
     E.par0 = gs;
@@ -523,39 +518,168 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
     E.hdr = la + L.hdr;
     E.rp[0] = la + L.rp;
     E.rp[1] = la + L.rp + n + 1;
-    if (!staged) {
-      for (int x = threadIdx.x; x <= n; x += NTHREADS) {
-        E.rp[0][x] = E.grp[0][x];
-        E.rp[1][x] = E.grp[1][x];
-      }
-      // batched so every thread keeps 8 independent global loads in flight
-      for (int e0b = 0; e0b < et; e0b += 8 * NTHREADS) {
-        int uu[8], vv[8], ss[8];
+  }
+  return E;
+}
+
+// LDS mode: stage the graph's static arrays (edge endpoints, CSR row pointers) from HBM.
+__device__ __forceinline__ void env_stage_static(const EnvView<false>& E, int n) {
+  const int et = E.et, e0 = E.e0;
+  for (int x = threadIdx.x; x <= n; x += NTHREADS) {
+    E.rp[0][x] = E.grp[0][x];
+    E.rp[1][x] = E.grp[1][x];
+  }
+  // batched so every thread keeps 8 independent global loads in flight
+  for (int e0b = 0; e0b < et; e0b += 8 * NTHREADS) {
+    int uu[8], vv[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int e = e0b + k * NTHREADS + threadIdx.x;
-          if (e < et) {
-            const int l = e < e0 ? 0 : 1, kk = e < e0 ? e : e - e0;
-            uu[k] = E.gu[l][kk];
-            vv[k] = E.gv[l][kk];
-            ss[k] = ldc(E.gst[l] + kk);
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int e = e0b + k * NTHREADS + threadIdx.x;
-          if (e < et) {
-            E.u16[e] = (uint16_t)uu[k];
-            E.v16[e] = (uint16_t)vv[k];
-            E.st[e] = (uint8_t)ss[k];
-          }
-        }
+    for (int k = 0; k < 8; ++k) {
+      const int e = e0b + k * NTHREADS + threadIdx.x;
+      if (e < et) {
+        const int l = e < e0 ? 0 : 1, kk = e < e0 ? e : e - e0;
+        uu[k] = E.gu[l][kk];
+        vv[k] = E.gv[l][kk];
       }
-      for (int x = threadIdx.x; x < n; x += NTHREADS) E.cov8[x] = E.gcov[x];
-      __syncthreads();
-      build_alive<GL>(E);
     }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int e = e0b + k * NTHREADS + threadIdx.x;
+      if (e < et) {
+        E.u16[e] = (uint16_t)uu[k];
+        E.v16[e] = (uint16_t)vv[k];
+      }
+    }
+  }
+}
+
+// LDS mode: stage the dynamic state (edge states, covered flags: the last write-back) from HBM,
+// sixteen independent loads per thread in flight.
+__device__ __forceinline__ void env_stage_dynamic(const EnvView<false>& E, int n) {
+  const int et = E.et, e0 = E.e0;
+  for (int e0b = 0; e0b < et; e0b += 16 * NTHREADS) {
+    int ss[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = e0b + k * NTHREADS + threadIdx.x;
+      if (e < et) ss[k] = ldc(E.gst[e < e0 ? 0 : 1] + (e < e0 ? e : e - e0));
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = e0b + k * NTHREADS + threadIdx.x;
+      if (e < et) E.st[e] = (uint8_t)ss[k];
+    }
+  }
+  for (int x = threadIdx.x; x < n; x += NTHREADS) E.cov8[x] = ldc(E.gcov + x);
+}
+
+// LDS mode: the whole environment of the last write-back, and its alive-edge list.
+__device__ __forceinline__ void env_stage_lds(const EnvView<false>& E, int n) {
+  env_stage_static(E, n);
+  env_stage_dynamic(E, n);
+  __syncthreads();
+  build_alive<false>(E);
+}
+
+// Applies a speculative workgroup's result (spec_loop, md_kernels.hip) in place of the
+// fixed point: the killed edges get their new states and leave the alive list exactly as
+// mcc_fixed_point's final compaction would move them.  The caller has covered the node.
+__device__ __forceinline__ int env_apply_spec(const EnvView<false>& E, const int* slot, int nd, int* pr, int* cc) {
+  for (int i = threadIdx.x; i < nd; i += NTHREADS) {
+    const int v = ldc(slot + SRES_HDR + i);
+    E.st[v & 0xffff] = (uint8_t)(v >> 16);
+  }
+  int lm = 0;
+  if (threadIdx.x == 0) {
+    lm = ldc(slot + 2);
+    pr[0] = ldc(slot + 3);
+    pr[1] = ldc(slot + 4);
+    cc[0] = ldc(slot + 5);
+    cc[1] = ldc(slot + 6);
+    E.tmp[A_TMP_WORDS - 8] = lm;
+    E.tmp[A_TMP_WORDS - 7] = pr[0];
+    E.tmp[A_TMP_WORDS - 6] = pr[1];
+    E.tmp[A_TMP_WORDS - 5] = cc[0];
+    E.tmp[A_TMP_WORDS - 4] = cc[1];
+  }
+  __syncthreads();
+  lm = E.tmp[A_TMP_WORDS - 8];
+  pr[0] = E.tmp[A_TMP_WORDS - 7];
+  pr[1] = E.tmp[A_TMP_WORDS - 6];
+  cc[0] = E.tmp[A_TMP_WORDS - 5];
+  cc[1] = E.tmp[A_TMP_WORDS - 4];
+  if (nd > 0) compact_alive<false>(E);
+  return lm;
+}
+
+// ------------------------------------------------------------------ the environment step
+// Everything phase A does for one graph once the actions to apply are known: cover each
+// queued node and run the fixed point (s0 first if not done), then residual degrees, the
+// ascending live-node list and the per-layer aggregates, the write-back of edge states and
+// the unit-cost first-layer table.  Returns 0 or an ERR_* code.
+// Not inlined: the environment step has its own register allocation (inlined, it raised the
+// register pressure of the whole rollout loop -- spills in the tile phases).
+template <bool GL>
+__device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, float*, int pend_n,
+                        int pend_first, const float*, bool staged) {
+  KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
+  // LDS from the kernel's dynamic-LDS base (compile-time addresses, ds_* accesses)
+  const float* const lds_base = md::lds_base();
+  GraphVar& gv = *(GraphVar*)(md::lds_base() + L_GV);
+  float* const area = md::lds_base() + L_W;
+  const int n = gi.n, e0 = gi.e[0], et = e0 + gi.e[1];
+  (void)et;  // bounds checks only
+  int* ia = (int*)area;
+  const EnvView<GL> E = env_view<GL>(p, gi, ia);
+  if constexpr (!GL) {
+    if (!staged) env_stage_lds(E, n);
     __syncthreads();
+  }
+  // a speculative workgroup may already have run this step's fixed point for the chosen node
+  // (single-node steps picked by the device or the host; results are tagged with the launch,
+  // the removals so far and the node)
+  int spec_slot = -1, spec_nd = 0;
+  if constexpr (!GL) {
+    if (p.n_spec > 0 && pend_n == 1 && gv.s0_done) {
+      const int a = pend_first >= 0 ? pend_first : __hip_atomic_load(p.pend + gi.node_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned want = spec_tag(p.launch_seq, gv.steps);
+      const int ps = ((volatile int*)(lds_base + L_MISC))[60] - 1;  // the request's step
+      unsigned long long* sts = p.prof != nullptr && ps >= 0 && ps < p.prof_cap ? p.prof + (size_t)ps * PROF_SLOTS : nullptr;
+      if (sts != nullptr && threadIdx.x == 0) sts[69] = wall_clock64();
+      if (threadIdx.x == 0) E.tmp[A_TMP_WORDS - 1] = -1;
+      __syncthreads();
+      if ((int)threadIdx.x < p.n_spec) {
+        // done, or taken and still running: a taken fixed point started earlier than this one
+        // could, so waiting for it is never slower than computing it here
+        const g_u64* tp = (const g_u64*)(p.sres + (size_t)threadIdx.x * p.sres_stride);
+        unsigned long long v = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long st = __hip_atomic_load(tp + SRES_STARTED / 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool done = (unsigned)v == want && (int)((v >> 32) & 0xffffu) == a;
+        if (!done && (unsigned)st == want && (int)(st >> 32) == a) {
+          const unsigned long long t0 = wall_clock64();
+          while (true) {
+            v = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((unsigned)v == want && (int)((v >> 32) & 0xffffu) == a) { done = true; break; }
+            if (wall_clock64() - t0 > BARRIER_TIMEOUT_TICKS ||
+                (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR))
+              break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        if (done) {
+          E.tmp[A_TMP_WORDS - 1] = threadIdx.x;
+          E.tmp[A_TMP_WORDS - 2] = (int)(v >> 48);  // killed edges
+          if (sts != nullptr) {
+            sts[70] = threadIdx.x + 1;
+            sts[72] = __hip_atomic_load(tp + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+      }
+      __syncthreads();
+      if (sts != nullptr && threadIdx.x == 0) sts[71] = wall_clock64();
+      spec_slot = E.tmp[A_TMP_WORDS - 1];
+      spec_nd = E.tmp[A_TMP_WORDS - 2];
+      __syncthreads();
+    }
   }
   MD_PROF_A(1);
   unsigned long long* acc = nullptr;
@@ -582,7 +706,17 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
     __syncthreads();
     PACC(acc, PA_COVER, tcv);
     int pr[2], c[2];
-    const int lm = mcc_fixed_point<GL>(E, pr, acc, a, c);
+    int lm;
+    if constexpr (!GL) {
+      if (k == 0 && spec_slot >= 0) {
+        lm = env_apply_spec(E, p.sres + (size_t)spec_slot * p.sres_stride, spec_nd, pr, c);
+        if (threadIdx.x == 0) gv.spec_hits += 1;
+      } else {
+        lm = mcc_fixed_point<GL>(E, pr, acc, a, c);
+      }
+    } else {
+      lm = mcc_fixed_point<GL>(E, pr, acc, a, c);
+    }
     if (threadIdx.x == 0) {
       gv.counter[0] += c[0];
       gv.counter[1] += c[1];

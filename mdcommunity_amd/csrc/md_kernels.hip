@@ -267,7 +267,7 @@ __device__ __forceinline__ bool md_bok(bool ok, int site) {
 __device__ __forceinline__ bool grid_sync(KParams& p, unsigned& target, int* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  target += gridDim.x;
+  target += p.n_main;  // speculative workgroups (if any) are not part of the barrier
   if (threadIdx.x == 0) {
     __hip_atomic_fetch_add((g_u32*)p.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long t0 = wall_clock64();
@@ -611,6 +611,18 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
   __syncthreads();
   gv_store(p, g, &gv);
   __syncthreads();
+  if (p.n_spec > 0 && have_q && gv.status == ST_RUN) {
+    // the state after this step is in HBM (every store drained): ask the speculative
+    // workgroups for the next step's fixed point of the likely next removals
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __hip_atomic_store((g_u64*)p.spec_req,
+                         ((unsigned long long)(unsigned)misc[60] << 32) | spec_tag(p.launch_seq, gv.steps),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (p.prof != nullptr && misc[60] < p.prof_cap) p.prof[(size_t)misc[60] * PROF_SLOTS + 64] = wall_clock64();
+    }
+  }
   return staged;
 }
 
@@ -1685,6 +1697,8 @@ __device__ __noinline__ void attention_q_tile(KParams&, float*, float*, const Gr
       if (v >= 0) {
         const float qq = gs[0] * ql[lane] + gs[1] * ql[16 + lane];
         stc(p.q + gi.node_off + v, qq);
+        if (p.qspec != nullptr)  // this step's Q for the speculative workgroups (buffer = step & 1)
+          stc(p.qspec + (size_t)(((const int*)(lds + L_MISC))[60] & 1) * p.qspec_n + gi.node_off + v, qq);
         bm = qq;
         bi = v;
         bc = 1;
@@ -2157,6 +2171,183 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
   }
 }
 
+// ------------------------------------------------------------------ speculative steps
+// Single-graph rollouts leave most CUs idle.  Workgroups [n_main, n_main + n_spec) of such a
+// launch run the NEXT step's environment for likely next removals while the tiles compute Q:
+// after phase A of step t publishes its state (spec_req), speculative workgroup k takes the
+// live node of rank k in the previous prediction Q(t-1) (the next pick is among the top 8 in
+// ~90 % of GMM steps), stages the state of step t from HBM into its own LDS, covers that
+// node and runs the same mutual-LMCC fixed point (mcc_fixed_point, bit-identical: the result
+// is unique and the code is the same), and publishes the killed edges, pruned / covered
+// counts and LMCC, tagged {node, launch, removals so far}.  Phase A of step t + 1 uses a result
+// only when its tag equals {the chosen node, this launch, the current removal count}: read
+// before that phase A writes anything back, such a result was computed from step t's state.
+// The workgroups take no part in the grid barrier and never write graph state; they stop at
+// SPEC_EXIT (end of the launch), on an error anywhere, or after the host time-out.
+// LDS words the candidate ranking needs beyond the environment: Q of the live nodes, group
+// maxima, the candidate list.
+constexpr int SPEC_CL = 256;
+__host__ __device__ inline int spec_rank_words(int n) { return ((n + 15) & ~15) + ((n + 15) >> 4) + SPEC_CL + 16; }
+
+__device__ __noinline__ void spec_loop(KParams&) {
+  KParams& p = kp();
+  float* const lds = lds_base();
+  int* misc = (int*)(lds + L_MISC);
+  const int k = (int)blockIdx.x - p.n_main;
+  const GraphInfo gi = p.ginfo[p.glist[0]];
+  const int n = gi.n, et = gi.e[0] + gi.e[1];
+  int* slot = p.sres + (size_t)k * p.sres_stride;
+  int* ia = (int*)(lds + L_W);
+  const EnvView<false> E = env_view<false>(p, gi, ia);
+  // ranking scratch after the environment: qv[n] (Q of live nodes, -inf otherwise), gmx[G]
+  // (maxima of 16-node groups), cl[SPEC_CL] (candidate list)
+  float* qv = (float*)(ia + env_layout(n, et).total);
+  const int G = (n + 15) >> 4;
+  float* gmx = qv + ((n + 15) & ~15);
+  int* cl = (int*)(gmx + G);
+  env_stage_static(E, n);  // endpoints and row pointers: once per launch
+  unsigned long long last = 0ull;
+  while (true) {
+    if (threadIdx.x == 0) {
+      const unsigned long long t0 = wall_clock64();
+      unsigned long long v;
+      int stop = 0;
+      while (true) {
+        v = __hip_atomic_load((const g_u64*)p.spec_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v == SPEC_EXIT) { stop = 1; break; }
+        if (v != 0ull && v != last && ((unsigned)v >> 16) == (p.launch_seq & 0xffffu)) break;
+        if (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR) { stop = 1; break; }
+        if (wall_clock64() - t0 > HOST_TIMEOUT_TICKS) { stop = 1; break; }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      misc[0] = stop;
+      misc[1] = (int)(unsigned)v;
+      misc[2] = (int)(unsigned)(v >> 32);
+      misc[3] = -1;
+      misc[4] = __float_as_int(NEG_INF);
+      misc[5] = 0;
+    }
+    __syncthreads();
+    if (misc[0]) return;
+    const unsigned tag = (unsigned)misc[1];
+    const int qb = (misc[2] - 1) & 1;  // buffer of the previous prediction
+    last = ((unsigned long long)(unsigned)misc[2] << 32) | tag;
+    // diagnostics (md_profile): workgroup 0's timeline in the request step's slots 65-68
+    unsigned long long* ts = p.prof != nullptr && k == 0 && misc[2] < p.prof_cap ? p.prof + (size_t)misc[2] * PROF_SLOTS : nullptr;
+    TSTAMP(65);
+    // step t's state and the previous prediction Q(t-1), loads batched; nodes live now were
+    // live then, so their entries are that prediction's
+    {
+      const int e0 = E.e0, span = max(et, n);
+      for (int b = 0; b < span; b += 8 * NTHREADS) {
+        int ss[8], cv[8], dd[8];
+        float qq[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = b + u * NTHREADS + threadIdx.x;
+          if (i < et) ss[u] = ldc(E.gst[i < e0 ? 0 : 1] + (i < e0 ? i : i - e0));
+          if (i < n) {
+            cv[u] = ldc(E.gcov + i);
+            dd[u] = ldc(p.deg[0] + gi.node_off + i);
+            qq[u] = ldc(p.qspec + (size_t)qb * p.qspec_n + gi.node_off + i);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = b + u * NTHREADS + threadIdx.x;
+          if (i < et) E.st[i] = (uint8_t)ss[u];
+          if (i < n) {
+            E.cov8[i] = (uint8_t)cv[u];
+            qv[i] = dd[u] > 0 ? qq[u] : NEG_INF;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    build_alive<false>(E);
+    TSTAMP(73);
+    // candidate: the live node of rank k (descending Q, ties by ascending id).  The top
+    // n_spec all have Q >= T, the n_spec-th largest maximum of the 16-node groups (those
+    // maxima are n_spec nodes at >= T), so only the nodes at >= T are ranked.
+    for (int r0 = 0; r0 < n; r0 += NTHREADS) {
+      const int x = r0 + (int)threadIdx.x;
+      float v = x < n ? qv[x] : NEG_INF;
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 16));
+      if ((threadIdx.x & 15) == 0 && x < n) gmx[x >> 4] = v;
+    }
+    __syncthreads();
+    const int K = p.n_spec;
+    for (int gq = threadIdx.x; gq < G; gq += NTHREADS) {
+      const float v = gmx[gq];
+      int r = 0;
+      for (int h = 0; h < G; ++h) {
+        const float w = gmx[h];
+        r += (w > v) || (w == v && h < gq);
+      }
+      if (r == K - 1) misc[4] = __float_as_int(v);
+    }
+    __syncthreads();
+    const float T = __int_as_float(misc[4]);
+    for (int x = threadIdx.x; x < n; x += NTHREADS) {
+      const float v = qv[x];
+      if (v != NEG_INF && v >= T) {
+        const int at = atomicAdd(&misc[5], 1);
+        if (at < SPEC_CL) cl[at] = x;
+      }
+    }
+    __syncthreads();
+    const int m = misc[5];
+    if (m <= SPEC_CL && (int)threadIdx.x < m) {
+      const int x = cl[threadIdx.x];
+      const float v = qv[x];
+      int r = 0;
+      for (int i = 0; i < m; ++i) {
+        const int y = cl[i];
+        const float w = qv[y];
+        r += (w > v) || (w == v && y < x);
+      }
+      if (r == k) misc[3] = x;
+    }
+    __syncthreads();
+    const int c = misc[3];
+    __syncthreads();
+    if (c < 0) continue;
+    TSTAMP(66);
+    // taken: phase A of the next step waits for this result instead of recomputing it
+    if (threadIdx.x == 0) {
+      __hip_atomic_store((g_u64*)(slot + SRES_STARTED), ((unsigned long long)(unsigned)c << 32) | tag,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      E.cov8[c] = 1;  // c is live, hence not covered
+    }
+    __syncthreads();
+    TSTAMP(67);
+    int pr[2], cc[2];
+    const int lm = mcc_fixed_point<false>(E, pr, nullptr, c, cc);
+    const int nd = E.hdr[1];
+    for (int i = threadIdx.x; i < nd; i += NTHREADS) {
+      const int e = E.dl[i];
+      stc(slot + SRES_HDR + i, e | ((int)E.st[e] << 16));
+    }
+    if (threadIdx.x == 0) {
+      stc(slot + 2, lm);
+      stc(slot + 3, pr[0]);
+      stc(slot + 4, pr[1]);
+      stc(slot + 5, cc[0]);
+      stc(slot + 6, cc[1]);
+      stc(slot + 7, nd);
+      const unsigned long long tdone = wall_clock64();
+      __hip_atomic_store((g_u64*)(slot + 10), tdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ts != nullptr) ts[68] = tdone;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)  // {killed edges << 48 | node << 32 | request tag}, one 8-byte granule
+      __hip_atomic_store((g_u64*)slot, ((unsigned long long)(unsigned)(c | (nd << 16)) << 32) | tag,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // ------------------------------------------------------------------ the kernel
 // One body, two entry points so profiles separate the work: md_rollout_kernel runs whole
 // rollouts (RUN_ROLLOUT); md_env_kernel runs single environment steps and predictions
@@ -2173,11 +2364,15 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
   // remaining workgroups own the weight image and do tiles.
   // Shared mode: every workgroup runs phase A for graphs b, b + grid, ... and then tiles
   // (the tile workgroups compute the virtual-node chain of the graphs they touch).
+  if ((int)blockIdx.x >= p.n_main) {
+    spec_loop(p);
+    return;
+  }
   const bool ded = p.n_env > 0;
   const bool is_env = ded && (int)blockIdx.x < p.n_env;
   const bool is_head = ded && !is_env && (int)blockIdx.x < 2 * p.n_env;
   const int twg0 = ded ? 2 * p.n_env : 0;
-  const int ntw = gridDim.x - twg0;
+  const int ntw = p.n_main - twg0;
   if (!is_env) {
     load_weights(lds + L_W, wimg);
     if (is_head) stage_wl1(p, scr);  // graph_head's w_layer1, resident for the launch
@@ -2208,7 +2403,7 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
       if (is_env) staged = phase_a(p, p.glist[blockIdx.x], have_q, lds, staged);
     } else {
       bool wdirty = false;
-      for (int gi = blockIdx.x; gi < ng; gi += gridDim.x) {
+      for (int gi = blockIdx.x; gi < ng; gi += p.n_main) {
         phase_a(p, p.glist[gi], have_q, lds, false);
         wdirty = true;
       }
@@ -2452,6 +2647,8 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
     have_q = true;
     pstep++;
   }
+  if (p.n_spec > 0 && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store((g_u64*)p.spec_req, SPEC_EXIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void __launch_bounds__(NTHREADS, 1) md_rollout_kernel(Params p, const float* __restrict__ wimg) {
@@ -2544,6 +2741,10 @@ namespace md {
 int lds_bytes() { return L_TOTAL * 4; }
 int weight_image_floats() { return W_IEND; }
 bool phase_a_fits_lds_host(int n, int et) { return phase_a_fits_lds(n, et); }
+// speculative workgroups: the environment plus the candidate ranking keys in LDS
+bool spec_fits_lds_host(int n, int et) {
+  return phase_a_fits_lds(n, et) && env_layout(n, et).total + spec_rank_words(n) <= A_WORDS;
+}
 
 // Host-side permutation of the reference-layout weight blob into the LDS image.
 void build_weight_image(const float* w, float* img) {

@@ -315,3 +315,34 @@ def test_k2_endgame_in_one_handshake_matches_per_step(monkeypatch):
     assert fast[-1] == slow[-1]
     # the GMM rollouts do end in K2 end-games: the shortcut skipped forward passes
     assert fast[1][0] < slow[1][0]
+
+
+@pytest.mark.parametrize("name", ["gmm1000_s0", "gmm1000_s2", "er1000", "er300_dense"])
+def test_speculative_steps_match_plain(monkeypatch, name):
+    """Speculative environment workgroups (MD_SPEC, single-graph rollouts) change nothing:
+    the same removal sequence and LMCC trace as without them, with most removals served by a
+    speculative result, for the per-step protocol and the K2 end-game alike."""
+    z = load_golden(name)
+    n = int(z["n_nodes"])
+    w = engine.load_weights(engine.DEFAULT_UNIT)
+    out = {}
+    for spec in ("0", "16"):
+        for variant in ("0", "2048"):
+            monkeypatch.setenv("MD_SPEC", spec)
+            monkeypatch.setenv("MD_VARIANT", variant)
+            e = _lib.Engine(w)
+            e.load_graphs([(n, z["edges0"], z["edges1"])])
+            for rep in range(2):
+                e.reset()
+                seq, ranks = e.rollout()[0]
+                out.setdefault((spec, variant), []).append((seq.tolist(), ranks.tolist(), e.spec_stats(0)))
+            e.close()
+    base = out[("0", "0")][0]
+    for key, runs in out.items():
+        for seq, ranks, (hits, rem) in runs:
+            assert seq == base[0] and ranks == base[1], key
+            assert rem == len(seq)
+            if key[0] == "0":
+                assert hits == 0
+            else:
+                assert hits >= len(seq) // 2, (key, hits, len(seq))
