@@ -70,13 +70,14 @@ def kernel_src_hash():
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--batch-graphs", type=int, default=256, help="graphs per GPU of the batch object (0: skip)")
     ap.add_argument("--batch-steps", type=int, default=2)
     ap.add_argument("--degree-steps", type=int, default=3, help="timed degree-cost rollouts (0: skip)")
+    ap.add_argument("--real-steps", type=int, default=1, help="timed rollouts of the testReal-sized object (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-step", action="store_true", help="skip the per-step-protocol comparison rollouts")
     ap.add_argument("--cpu-sample-seconds", type=float, default=12.0)
@@ -360,6 +361,49 @@ def degree_object(args, edges, make_engine):
     return out
 
 
+def real_scale_object(args, make_engine, tmpdir):
+    """configs[3] at the reference's real sizes: the testReal harness's rollout of an
+    N = 18 000 two-layer multiplex shaped like homo_genetic_multiplex (mdcommunity_amd.synth;
+    the real files are absent), read by the drop-in reader, environment in HBM: degree cost
+    with stepRatio 0 and unit cost with stepRatio 0.01 (180 removals per prediction through the
+    host hand-shake).  Timed like `value` (inputs resident in HBM)."""
+    from mdcommunity_amd import _lib, agent, engine, graph as mgraph, synth
+    n = 18000
+    path = os.path.join(tmpdir, "real_like_multiplex.edges")
+    synth.write_real_like(path, n, seed=0)
+    a = agent.MultiDismantler.__new__(agent.MultiDismantler)
+    _, gl = agent.MultiDismantler.read_multiplex(a, path, n)
+    e0, e1 = np.asarray(gl[0], np.int32), np.asarray(gl[1], np.int32)
+    g = mgraph.Graph_test.from_edges(n, e0, e1)
+    mgraph.ensure_degree_weights(g)
+    out = {"workload": "testReal-shaped 2-layer multiplex N=%d (mdcommunity_amd.synth seed 0: heavy-tailed, "
+                       "%d / %d edges, hubs ~1100), HBM environment" % (n, len(e0), len(e1))}
+    for key, cost, ckpt, step in (("degree_step1", _lib.MD_COST_DEGREE, engine.DEFAULT_DEGREE, 1),
+                                  ("unit_step_ratio_0.01", _lib.MD_COST_UNIT, engine.DEFAULT_UNIT_REAL,
+                                   max(int(0.01 * n), 1))):
+        eng = make_engine(engine.load_weights(ckpt), cost_mode=cost)
+        eng.load_graphs([(n, e0, e1)], node_w=mgraph.node_weight_array([g]) if cost == _lib.MD_COST_DEGREE else None)
+        eng.reset()
+        eng.rollout(step=step)  # warm
+        t0 = time.perf_counter()
+        kms = 0.0
+        rem = 0
+        for _ in range(max(1, args.real_steps)):
+            mr = eng.reset()
+            seq, ranks = eng.rollout(step=step)[0]
+            kms += eng.last_timing()[0]
+            rem += len(seq)
+        dt = time.perf_counter() - t0
+        eng.close()
+        k = max(1, args.real_steps)
+        out[key] = {"value": rem / dt, "unit": "removals/s", "removals_per_rollout": rem // k, "step": step,
+                    "ms_per_rollout": dt / k * 1e3, "kernel_ms_per_rollout": kms / k, "max_rank": int(mr[0]),
+                    "audc": audc_of(ranks, mr[0], n) if cost == _lib.MD_COST_UNIT else None}
+    out["reference_note"] = ("the reference's committed homo_genetic_multiplex run (N=18222, unit cost, stepRatio 0): "
+                             "2081 removals in 1582.6 s (results/unitcost/MultiDismantler_real/StepRatio_0.0000)")
+    return out
+
+
 # ------------------------------------------------------------------ one rank
 def rank_main(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -507,6 +551,11 @@ def rank_main(args):
     degree = None
     if rank == 0 and args.degree_steps > 0 and not args.cpu_dry_run:
         degree = degree_object(args, edges, make_engine)
+    real = None
+    if rank == 0 and args.real_steps > 0 and not args.cpu_dry_run:
+        import tempfile
+        with tempfile.TemporaryDirectory() as td:
+            real = real_scale_object(args, make_engine, td)
 
     if rank == 0:
         golden = None
@@ -571,6 +620,7 @@ def rank_main(args):
             "roofline": rl,
             "batch": batch,
             "degree": degree,
+            "real_scale": real,
             "kernel_src_hash": kernel_src_hash(),
         }
         line["cpu_baseline"] = None

@@ -16,8 +16,8 @@ if [ "$2" != "--no-bench" ]; then
   timeout -k 10 500 python $R/bench.py > $OUT/bench.json 2> $OUT/bench.err
   echo "bench done"
 fi
-SINGLE="--batch-graphs 0 --no-cpu-baseline --degree-steps 0 --no-per-step"
-BATCH="--steps 0 --batch-graphs 256 --no-cpu-baseline --degree-steps 0 --no-per-step"
+SINGLE="--batch-graphs 0 --no-cpu-baseline --degree-steps 0 --no-per-step --real-steps 0"
+BATCH="--steps 0 --batch-graphs 256 --no-cpu-baseline --degree-steps 0 --no-per-step --real-steps 0"
 SQ1="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_F32 SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT"
 SQ2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_VALU SQ_INSTS_SALU SQ_VALU_MFMA_COEXEC_CYCLES"
 cd /tmp

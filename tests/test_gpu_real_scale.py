@@ -1,0 +1,122 @@
+"""testReal at the reference's real sizes (BASELINE.json configs[3]).
+
+The reference's real multiplex files are absent; mdcommunity_amd.synth writes an N = 18 000
+two-layer file shaped like homo_genetic_multiplex (N = 18 222, heavy-tailed degrees, hubs of
+degree ~1 100, nodes missing from a layer, duplicate edges and self-loops for the reader to
+drop).  It is read through the drop-in reader (MultiDismantler.read_multiplex, networkx edge
+order) and rolled out on the GPU with the environment in HBM (the graph is far beyond one
+workgroup's LDS), unit and degree cost, stepRatio 0 and 0.01 (180 removals per prediction
+through the host hand-shake).  Checked against the oracle:
+* MvcEnv.s0's max_rank and Q at s0 (within 1e-5);
+* the LMCC after removal k of the device's own sequence for the first 12 removals (the
+  oracle environment stepped along it) and at sampled later k (the mutual-LMCC fixed point of
+  the graph without the first k + 1 removed nodes, computed from scratch: the fixed point
+  only gets finer as nodes are removed, so it does not depend on the path);
+* the sequence is a permutation prefix that ends terminal, and with stepRatio 0.01 each
+  prediction's picks are the host's np.argsort(-q)[:180] of the device's own Q.
+"""
+import numpy as np
+import pytest
+
+from mdcommunity_amd import _lib, agent, engine, graph as mgraph, synth
+from oracle import refenv, refmodel
+
+pytestmark = pytest.mark.gpu
+N = 18000
+
+
+@pytest.fixture(scope="module")
+def real(tmp_path_factory):
+    path = str(tmp_path_factory.mktemp("real") / "real_like_multiplex.edges")
+    synth.write_real_like(path, N, seed=0)
+    a = agent.MultiDismantler.__new__(agent.MultiDismantler)
+    _, gl = agent.MultiDismantler.read_multiplex(a, path, N)
+    e0, e1 = np.asarray(gl[0], np.int32), np.asarray(gl[1], np.int32)
+    return e0, e1, refenv.RefGraph(N, e0, e1)
+
+
+def prefix_lmcc(g, seq, k):
+    g1, g2 = g.nx_layers()
+    cov = [int(a) for a in seq[: k + 1]]
+    g1.remove_nodes_from(cov)
+    g2.remove_nodes_from(cov)
+    return refenv.lmcc_size(refenv.mutual_components(g1, g2, [set(), set()]))
+
+
+def check_sequence(g, seq, ranks, cost):
+    assert len(seq) == len(set(seq.tolist())) > 0
+    env = refenv.RefEnv(g, cost)
+    for a, r in zip(seq[:12].tolist(), ranks[:12].tolist()):
+        assert env.step(int(a)) == int(r)
+    rng = np.random.default_rng(1)
+    ks = sorted(set(rng.integers(12, len(seq), size=6).tolist()) | {len(seq) - 1})
+    for k in ks:
+        assert prefix_lmcc(g, seq, k) == int(ranks[k]), k
+    # terminal after the last removal: some layer has no alive edge left
+    g1, g2 = g.nx_layers()
+    g1.remove_nodes_from(seq.tolist())
+    g2.remove_nodes_from(seq.tolist())
+    refenv.mutual_components(g1, g2, [set(), set()])
+    assert g1.number_of_edges() == 0 or g2.number_of_edges() == 0
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("cost", ["unit", "degree"])
+def test_real_scale_s0_q_and_rollout(real, cost):
+    e0, e1, g = real
+    deg = cost == "degree"
+    ckpt = engine.DEFAULT_DEGREE if deg else engine.DEFAULT_UNIT_REAL
+    eng = _lib.Engine(engine.load_weights(ckpt), cost_mode=_lib.MD_COST_DEGREE if deg else _lib.MD_COST_UNIT)
+    try:
+        nw = None
+        if deg:
+            gg = mgraph.Graph_test.from_edges(N, e0, e1)
+            mgraph.ensure_degree_weights(gg)
+            nw = mgraph.node_weight_array([gg])
+        eng.load_graphs([(N, e0, e1)], node_w=nw)
+        mr = int(eng.reset()[0])
+        assert mr == g.max_rank
+        q, _, _, _ = eng.predict()
+        env = refenv.RefEnv(g, cost)
+        q_ref = refenv.predict(refmodel.RefWeights.load(ckpt), g, set(), env.removed, cost)
+        live = q_ref != refenv.MASK
+        assert np.array_equal(np.isfinite(q), live)
+        dq = float(np.max(np.abs(q[live].astype(np.float64) - q_ref[live])))
+        assert dq < 1e-5, dq
+        eng.reset()
+        seq, ranks = eng.rollout()[0]
+        check_sequence(g, seq, ranks, cost)
+    finally:
+        eng.close()
+
+
+@pytest.mark.timeout(600)
+def test_real_scale_step_ratio(real):
+    """stepRatio = 0.01 (U/MultiDismantler_torch.py:676-679,725): 180 removals per prediction,
+    every prediction answered by the host's np.argsort(-q)[:180] through the hand-shake."""
+    e0, e1, g = real
+    step = max(int(0.01 * N), 1)
+    eng = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT_REAL))
+    rows = []
+    base = eng.selector
+
+    def sel(qrow, n_out):  # the default rule, recording each request's row
+        rows.append(qrow.copy())
+        return base(qrow, n_out)
+
+    try:
+        eng.load_graphs([(N, e0, e1)])
+        eng.reset()
+        q0, _, _, _ = eng.predict()
+        eng.reset()
+        eng.selector = sel
+        seq, ranks = eng.rollout(step=step)[0]
+        check_sequence(g, seq, ranks, "unit")
+        assert len(rows) == (len(seq) + step - 1) // step
+        # the first request is the s0 prediction; every request's picks are its argsort
+        assert np.array_equal(np.isfinite(q0), rows[0] > refenv.MASK)
+        for t, r in enumerate(rows):
+            picks = np.argsort(-r)[:step].tolist()
+            assert seq[t * step:(t + 1) * step].tolist() == picks[: len(seq[t * step:(t + 1) * step])], t
+    finally:
+        eng.close()

@@ -90,7 +90,7 @@ def _bench(*extra):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, os.path.join(root, "bench.py"), "--cpu-dry-run", "--n", "40", "--steps", "1",
-           "--warmup", "0", "--batch-steps", "1", "--degree-steps", "0", "--no-cpu-baseline"] + list(extra)
+           "--warmup", "0", "--batch-steps", "1", "--degree-steps", "0", "--no-cpu-baseline", "--real-steps", "0"] + list(extra)
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
     out = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=240, env=env).stdout
