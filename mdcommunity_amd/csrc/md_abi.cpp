@@ -845,9 +845,9 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->qg.alloc(2 * G_CAP));
   {
     // speculative-step slots: killed-edge lists of one graph (LDS-mode graphs only)
-    int maxe = 0;
-    for (int g = 0; g < n_graphs; ++g) maxe = std::max(maxe, info[g].e[0] + info[g].e[1]);
-    c->sres_stride = ((SRES_HDR + maxe + 63) / 64) * 64;
+    int maxw = 0;
+    for (int g = 0; g < n_graphs; ++g) maxw = std::max(maxw, sres_words(info[g].e[0] + info[g].e[1], info[g].n));
+    c->sres_stride = ((maxw + 63) / 64) * 64;
     HIPCHK(c, c->sres.alloc((size_t)SPEC_MAX * c->sres_stride));
     HIPCHK(c, hipMemset(c->sres.p, 0, sizeof(int) * (size_t)SPEC_MAX * c->sres_stride));
     HIPCHK(c, c->qspec.alloc(2 * tn));

@@ -149,11 +149,20 @@ struct Params {
   int qspec_n;                     // total nodes of the loaded batch
 };
 
-// Speculative-step result slot (ints): [0..1] u64 done tag {nd << 48 | candidate << 32 |
-// request tag} written last; [2] LMCC, [3..4] pruned edges per layer, [5..6] covered edges per
-// layer, [7] killed edges nd; [8..9] u64 started tag {candidate << 32 | request tag} written
-// when the workgroup takes its candidate; [16 .. 16 + nd) killed edge (LDS id) | state << 16.
-constexpr int SRES_HDR = 16, SRES_STARTED = 8;
+// Speculative-step result slot (ints):
+//   [0..1] u64 done tag {nd << 48 | candidate << 32 | request tag}, written last
+//   [2] LMCC  [3..4] pruned edges per layer  [5..6] covered edges per layer  [7] killed edges nd
+//   [8..9] u64 started tag {candidate << 32 | request tag}, written when the candidate is taken
+//   [10..11] u64 device time of the result (diagnostics)
+//   [12] live nodes  [13..14] dmax per layer  [15..16] degree sums  [17] live-set mismatch
+//   [18..21] two-hop sums (2 x i64)  [22..23] u64 features tag {candidate << 32 | request tag},
+//   written after the degrees, live list and aggregates (later than the done tag)
+//   [SRES_HDR, +3 nd) killed edges {edge (LDS id) | new state << 16, CSR slot, CSR slot}
+//   [sres_deg, +2 n) residual degrees per layer; [sres_live, +4 n) live-list entries
+constexpr int SRES_HDR = 32, SRES_STARTED = 8, SRES_FEAT = 22;
+__host__ __device__ inline int sres_deg(int et) { return SRES_HDR + 3 * et; }
+__host__ __device__ inline int sres_live(int et, int n) { return (sres_deg(et) + 2 * n + 3) & ~3; }
+__host__ __device__ inline int sres_words(int et, int n) { return sres_live(et, n) + 4 * n; }
 constexpr unsigned long long SPEC_EXIT = ~0ull;
 __host__ __device__ inline unsigned spec_tag(unsigned launch_seq, int steps) {
   return ((launch_seq & 0xffffu) << 16) | ((unsigned)steps & 0xffffu);

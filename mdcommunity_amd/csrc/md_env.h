@@ -466,6 +466,187 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
   return best;
 }
 
+// Aggregates of one environment state (U/PrepareBatchGraph.py:35-74).
+struct EnvAgg {
+  int nlive, dm0, dm1, sd0, sd1, bad;
+  long long th0, th1;
+};
+
+// Residual degrees (edge-parallel atomics over the alive edges), then the ascending live list,
+// the degrees and the per-layer aggregates of the current state, stored to (gdeg0, gdeg1, lv)
+// -- the graph's HBM arrays (phase A) or a speculative result slot -- and q = -inf for every
+// node when q is given.  One fused block exchange for the scan and all reductions.
+template <bool GL>
+__device__ EnvAgg env_features(const EnvView<GL>& E, int n, int* gdeg0, int* gdeg1, float* lv, float* q) {
+  const int e0 = E.e0;
+  // residual degrees by edge-parallel atomics
+  for (int x = threadIdx.x; x < n; x += NTHREADS) {
+    uf_store(E.deg0, x, 0);
+    uf_store(E.deg1, x, 0);
+  }
+  __syncthreads();
+  for_each_alive<GL>(E, [&](int e, int u, int v) {
+    auto d = e < e0 ? E.deg0 : E.deg1;
+    uf_add(d, u, 1);
+    uf_add(d, v, 1);
+  });
+  __syncthreads();
+  // live list (ascending ids), per-layer aggregates (U/PrepareBatchGraph.py:35-74): one
+  // fused block exchange for the scan and all reductions
+  const int chunk = (n + NTHREADS - 1) / NTHREADS;
+  const int x0 = min(n, (int)threadIdx.x * chunk), x1 = min(n, x0 + chunk);
+  int nlive = 0, dm0 = 0, dm1 = 0, sd0 = 0, sd1 = 0, bad = 0;
+  long long th0 = 0, th1 = 0;
+  for (int x = x0; x < x1; ++x) {
+    const int d0 = uf_load(E.deg0, x), d1 = uf_load(E.deg1, x);
+    stc(gdeg0 + x, d0);
+    stc(gdeg1 + x, d1);
+    if (q != nullptr) stc(q + x, NEG_INF);
+    bad |= ((d0 > 0) != (d1 > 0));
+    if (d0 > 0) {
+      nlive++;
+      dm0 = max(dm0, d0);
+      dm1 = max(dm1, d1);
+      th0 += (long long)d0 * (d0 - 1) / 2;
+      th1 += (long long)d1 * (d1 - 1) / 2;
+    }
+    sd0 += d0;
+    sd1 += d1;
+  }
+  int tot = 0, base = 0;
+  {
+    const int lane = lane_id(), w = wave_id();
+    int incl = nlive;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    int r_nl = nlive, r_m0 = dm0, r_m1 = dm1, r_s0 = sd0, r_s1 = sd1, r_bad = bad;
+    long long r_t0 = th0, r_t1 = th1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      r_nl += __shfl_xor(r_nl, o, 64);
+      r_m0 = max(r_m0, __shfl_xor(r_m0, o, 64));
+      r_m1 = max(r_m1, __shfl_xor(r_m1, o, 64));
+      r_s0 += __shfl_xor(r_s0, o, 64);
+      r_s1 += __shfl_xor(r_s1, o, 64);
+      r_bad |= __shfl_xor(r_bad, o, 64);
+      r_t0 += __shfl_xor(r_t0, o, 64);
+      r_t1 += __shfl_xor(r_t1, o, 64);
+    }
+    __syncthreads();
+    lds_i32* t = (lds_i32*)E.tmp;  // 12 words per wave
+    if (lane == 0) {
+      t[12 * w + 0] = r_nl;
+      t[12 * w + 1] = r_m0;
+      t[12 * w + 2] = r_m1;
+      t[12 * w + 3] = r_s0;
+      t[12 * w + 4] = r_s1;
+      t[12 * w + 5] = r_bad;
+      t[12 * w + 6] = (int)(r_t0 & 0xffffffffll);
+      t[12 * w + 7] = (int)(r_t0 >> 32);
+      t[12 * w + 8] = (int)(r_t1 & 0xffffffffll);
+      t[12 * w + 9] = (int)(r_t1 >> 32);
+    }
+    __syncthreads();
+    dm0 = dm1 = sd0 = sd1 = bad = 0;
+    th0 = th1 = 0;
+    int before = 0;
+#pragma unroll
+    for (int i = 0; i < NTHREADS / 64; ++i) {
+      const int nl_i = t[12 * i];
+      if (i < w) before += nl_i;
+      tot += nl_i;
+      dm0 = max(dm0, (int)t[12 * i + 1]);
+      dm1 = max(dm1, (int)t[12 * i + 2]);
+      sd0 += t[12 * i + 3];
+      sd1 += t[12 * i + 4];
+      bad |= t[12 * i + 5];
+      th0 += (long long)(((unsigned long long)(unsigned)t[12 * i + 7] << 32) | (unsigned)t[12 * i + 6]);
+      th1 += (long long)(((unsigned long long)(unsigned)t[12 * i + 9] << 32) | (unsigned)t[12 * i + 8]);
+    }
+    base = before + incl - nlive;
+  }
+  {
+    // live list entries {node, CSR begin layer 0, layer 1, CSR extents (u16 | u16 << 16)}: a tile
+    // reads its rows and their neighbour ranges with one 16-byte load each
+    int k = base;
+    for (int x = x0; x < x1; ++x) {
+      if (uf_load(E.deg0, x) > 0) {
+        int b0, e0_, b1, e1_;
+        if constexpr (GL) {
+          b0 = E.grp[0][x]; e0_ = E.grp[0][x + 1]; b1 = E.grp[1][x]; e1_ = E.grp[1][x + 1];
+        } else {
+          b0 = E.rp[0][x]; e0_ = E.rp[0][x + 1]; b1 = E.rp[1][x]; e1_ = E.rp[1][x + 1];
+        }
+        if (MD_BOK(k < n, 9))
+          stc4(lv, k * 16, make_float4(__int_as_float(x), __int_as_float(b0), __int_as_float(b1),
+                                       __int_as_float((e0_ - b0) | ((e1_ - b1) << 16))));
+        ++k;
+      }
+    }
+  }
+
+  EnvAgg ag;
+  ag.nlive = tot;
+  ag.dm0 = dm0;
+  ag.dm1 = dm1;
+  ag.sd0 = sd0;
+  ag.sd1 = sd1;
+  ag.bad = bad;
+  ag.th0 = th0;
+  ag.th1 = th1;
+  return ag;
+}
+
+// Phase A's copy of a speculative slot's degrees, live list and aggregates (env_features of
+// the same state) to the graph's HBM arrays; q = -inf for every node.
+__device__ __forceinline__ EnvAgg env_copy_features(const int* slot, int n, int et, int* gdeg0, int* gdeg1, float* lv,
+                                                    float* q) {
+  const int* sd = slot + sres_deg(et);
+  const float* sl = (const float*)(slot + sres_live(et, n));
+  // every load in one round trip: the header words, the degrees and the live entries up to n
+  // (the first n_live of them are used)
+  int h[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) h[i] = ldc(slot + 12 + i);
+  constexpr int U = 4;
+  int d0[U], d1[U];
+  float4 le[U];
+  for (int x0 = threadIdx.x; x0 < n; x0 += U * NTHREADS) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int x = x0 + u * NTHREADS;
+      if (x < n) {
+        d0[u] = ldc(sd + x);
+        d1[u] = ldc(sd + n + x);
+        le[u] = ldc4(sl, x * 16);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int x = x0 + u * NTHREADS;
+      if (x < n) {
+        stc(gdeg0 + x, d0[u]);
+        stc(gdeg1 + x, d1[u]);
+        stc(q + x, NEG_INF);
+        if (x < h[0]) stc4(lv, x * 16, le[u]);
+      }
+    }
+  }
+  EnvAgg ag;
+  ag.nlive = h[0];
+  ag.dm0 = h[1];
+  ag.dm1 = h[2];
+  ag.sd0 = h[3];
+  ag.sd1 = h[4];
+  ag.bad = h[5];
+  ag.th0 = (long long)(((unsigned long long)(unsigned)h[7] << 32) | (unsigned)h[6]);
+  ag.th1 = (long long)(((unsigned long long)(unsigned)h[9] << 32) | (unsigned)h[8]);
+  return ag;
+}
+
 // ------------------------------------------------------------------ the environment step
 // Everything phase A does for one graph once the actions to apply are known: cover each
 // queued node and run the fixed point (s0 first if not done), then residual degrees, the
@@ -582,32 +763,55 @@ __device__ __forceinline__ void env_stage_lds(const EnvView<false>& E, int n) {
 
 // Applies a speculative workgroup's result (spec_loop, md_kernels.hip) in place of the
 // fixed point: the killed edges get their new states and leave the alive list exactly as
-// mcc_fixed_point's final compaction would move them.  The caller has covered the node.
+// mcc_fixed_point's final compaction would move them, and their write-back to HBM (edge
+// state, both CSR flags) is issued here.  The caller has covered the node.
 __device__ __forceinline__ int env_apply_spec(const EnvView<false>& E, const int* slot, int nd, int* pr, int* cc) {
-  for (int i = threadIdx.x; i < nd; i += NTHREADS) {
-    const int v = ldc(slot + SRES_HDR + i);
-    E.st[v & 0xffff] = (uint8_t)(v >> 16);
-  }
-  int lm = 0;
+  // the header (and whether the features are published too) in the kill list's round trip
+  int h[5] = {0, 0, 0, 0, 0};
+  unsigned long long ft = 0ull, dt = 0ull;
   if (threadIdx.x == 0) {
-    lm = ldc(slot + 2);
-    pr[0] = ldc(slot + 3);
-    pr[1] = ldc(slot + 4);
-    cc[0] = ldc(slot + 5);
-    cc[1] = ldc(slot + 6);
-    E.tmp[A_TMP_WORDS - 8] = lm;
-    E.tmp[A_TMP_WORDS - 7] = pr[0];
-    E.tmp[A_TMP_WORDS - 6] = pr[1];
-    E.tmp[A_TMP_WORDS - 5] = cc[0];
-    E.tmp[A_TMP_WORDS - 4] = cc[1];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) h[i] = ldc(slot + 2 + i);
+    ft = __hip_atomic_load((const g_u64*)(slot + SRES_FEAT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    dt = __hip_atomic_load((const g_u64*)slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (int i0 = threadIdx.x; i0 < nd; i0 += 4 * NTHREADS) {
+    int v[4], c0[4], c1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * NTHREADS;
+      if (i < nd) {
+        v[u] = ldc(slot + SRES_HDR + 3 * i);
+        c0[u] = ldc(slot + SRES_HDR + 3 * i + 1);
+        c1[u] = ldc(slot + SRES_HDR + 3 * i + 2);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (i0 + u * NTHREADS >= nd) continue;
+      const int e = v[u] & 0xffff, l = e < E.e0 ? 0 : 1;
+      const uint8_t s = (uint8_t)(v[u] >> 16);
+      E.st[e] = s;
+      stc(E.gst[l] + (e < E.e0 ? e : e - E.e0), s);
+      stc(E.calive[l] + c0[u], (uint8_t)0);
+      stc(E.calive[l] + c1[u], (uint8_t)0);
+    }
+  }
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) E.tmp[A_TMP_WORDS - 8 + i] = h[i];
+    // features of the same result already published? (used after this point only)
+    E.tmp[A_TMP_WORDS - 3] = (unsigned)ft == (unsigned)dt && (ft >> 32) == ((dt >> 32) & 0xffffu);
   }
   __syncthreads();
-  lm = E.tmp[A_TMP_WORDS - 8];
+  const int lm = E.tmp[A_TMP_WORDS - 8];
   pr[0] = E.tmp[A_TMP_WORDS - 7];
   pr[1] = E.tmp[A_TMP_WORDS - 6];
   cc[0] = E.tmp[A_TMP_WORDS - 5];
   cc[1] = E.tmp[A_TMP_WORDS - 4];
   if (nd > 0) compact_alive<false>(E);
+  if (threadIdx.x == 0) E.hdr[1] = 0;  // written back above
+  __syncthreads();
   return lm;
 }
 
@@ -639,7 +843,7 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
   // the removals so far and the node)
   int spec_slot = -1, spec_nd = 0;
   if constexpr (!GL) {
-    if (p.n_spec > 0 && pend_n == 1 && gv.s0_done) {
+    if (p.n_spec > 0 && pend_n == 1 && gv.s0_done && ((const volatile int*)(lds_base + L_MISC))[5]) {
       const int a = pend_first >= 0 ? pend_first : __hip_atomic_load(p.pend + gi.node_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const unsigned want = spec_tag(p.launch_seq, gv.steps);
       const int ps = ((volatile int*)(lds_base + L_MISC))[60] - 1;  // the request's step
@@ -650,9 +854,12 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
       if ((int)threadIdx.x < p.n_spec) {
         // done, or taken and still running: a taken fixed point started earlier than this one
         // could, so waiting for it is never slower than computing it here
+        // tags as phase A read them beside the arg-max partials (L_PREF, free until the tile
+        // prefix), polled again only while a taken result is still running
         const g_u64* tp = (const g_u64*)(p.sres + (size_t)threadIdx.x * p.sres_stride);
-        unsigned long long v = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long st = __hip_atomic_load(tp + SRES_STARTED / 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long* pre = (const unsigned long long*)(lds_base + L_PREF) + 2 * threadIdx.x;
+        unsigned long long v = pre[0];
+        const unsigned long long st = pre[1];
         bool done = (unsigned)v == want && (int)((v >> 32) & 0xffffu) == a;
         if (!done && (unsigned)st == want && (int)(st >> 32) == a) {
           const unsigned long long t0 = wall_clock64();
@@ -746,119 +953,21 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
     }
   }
   MD_PROF_A(2);
-  // residual degrees by edge-parallel atomics
-  for (int x = threadIdx.x; x < n; x += NTHREADS) {
-    uf_store(E.deg0, x, 0);
-    uf_store(E.deg1, x, 0);
-  }
-  __syncthreads();
-  for_each_alive<GL>(E, [&](int e, int u, int v) {
-    auto d = e < e0 ? E.deg0 : E.deg1;
-    uf_add(d, u, 1);
-    uf_add(d, v, 1);
-  });
-  __syncthreads();
-  // live list (ascending ids), per-layer aggregates (U/PrepareBatchGraph.py:35-74): one
-  // fused block exchange for the scan and all reductions
-  const int chunk = (n + NTHREADS - 1) / NTHREADS;
-  const int x0 = min(n, (int)threadIdx.x * chunk), x1 = min(n, x0 + chunk);
-  int nlive = 0, dm0 = 0, dm1 = 0, sd0 = 0, sd1 = 0, bad = 0;
-  long long th0 = 0, th1 = 0;
   float* q = p.q + gi.node_off;
   int* gdeg0 = p.deg[0] + gi.node_off;
   int* gdeg1 = p.deg[1] + gi.node_off;
-  for (int x = x0; x < x1; ++x) {
-    const int d0 = uf_load(E.deg0, x), d1 = uf_load(E.deg1, x);
-    stc(gdeg0 + x, d0);
-    stc(gdeg1 + x, d1);
-    stc(q + x, NEG_INF);
-    bad |= ((d0 > 0) != (d1 > 0));
-    if (d0 > 0) {
-      nlive++;
-      dm0 = max(dm0, d0);
-      dm1 = max(dm1, d1);
-      th0 += (long long)d0 * (d0 - 1) / 2;
-      th1 += (long long)d1 * (d1 - 1) / 2;
-    }
-    sd0 += d0;
-    sd1 += d1;
+  float* lv = (float*)(p.live + 4 * (size_t)gi.node_off);
+  EnvAgg ag;
+  if (spec_slot >= 0 && E.tmp[A_TMP_WORDS - 3]) {
+    // the speculative workgroup also produced this step's degrees, live list and aggregates
+    ag = env_copy_features(p.sres + (size_t)spec_slot * p.sres_stride, n, et, gdeg0, gdeg1, lv, q);
+    if (acc != nullptr && threadIdx.x == 0) acc[59] = 1;  // diagnostics: slot 75, features copied
+  } else {
+    ag = env_features<GL>(E, n, gdeg0, gdeg1, lv, q);
   }
-  int tot = 0, base = 0;
-  {
-    const int lane = lane_id(), w = wave_id();
-    int incl = nlive;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += y;
-    }
-    int r_nl = nlive, r_m0 = dm0, r_m1 = dm1, r_s0 = sd0, r_s1 = sd1, r_bad = bad;
-    long long r_t0 = th0, r_t1 = th1;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      r_nl += __shfl_xor(r_nl, o, 64);
-      r_m0 = max(r_m0, __shfl_xor(r_m0, o, 64));
-      r_m1 = max(r_m1, __shfl_xor(r_m1, o, 64));
-      r_s0 += __shfl_xor(r_s0, o, 64);
-      r_s1 += __shfl_xor(r_s1, o, 64);
-      r_bad |= __shfl_xor(r_bad, o, 64);
-      r_t0 += __shfl_xor(r_t0, o, 64);
-      r_t1 += __shfl_xor(r_t1, o, 64);
-    }
-    __syncthreads();
-    lds_i32* t = (lds_i32*)E.tmp;  // 12 words per wave
-    if (lane == 0) {
-      t[12 * w + 0] = r_nl;
-      t[12 * w + 1] = r_m0;
-      t[12 * w + 2] = r_m1;
-      t[12 * w + 3] = r_s0;
-      t[12 * w + 4] = r_s1;
-      t[12 * w + 5] = r_bad;
-      t[12 * w + 6] = (int)(r_t0 & 0xffffffffll);
-      t[12 * w + 7] = (int)(r_t0 >> 32);
-      t[12 * w + 8] = (int)(r_t1 & 0xffffffffll);
-      t[12 * w + 9] = (int)(r_t1 >> 32);
-    }
-    __syncthreads();
-    dm0 = dm1 = sd0 = sd1 = bad = 0;
-    th0 = th1 = 0;
-    int before = 0;
-#pragma unroll
-    for (int i = 0; i < NTHREADS / 64; ++i) {
-      const int nl_i = t[12 * i];
-      if (i < w) before += nl_i;
-      tot += nl_i;
-      dm0 = max(dm0, (int)t[12 * i + 1]);
-      dm1 = max(dm1, (int)t[12 * i + 2]);
-      sd0 += t[12 * i + 3];
-      sd1 += t[12 * i + 4];
-      bad |= t[12 * i + 5];
-      th0 += (long long)(((unsigned long long)(unsigned)t[12 * i + 7] << 32) | (unsigned)t[12 * i + 6]);
-      th1 += (long long)(((unsigned long long)(unsigned)t[12 * i + 9] << 32) | (unsigned)t[12 * i + 8]);
-    }
-    base = before + incl - nlive;
-  }
-  {
-    // live list entries {node, CSR begin layer 0, layer 1, CSR extents (u16 | u16 << 16)}: a tile
-    // reads its rows and their neighbour ranges with one 16-byte load each
-    int k = base;
-    float* lv = (float*)(p.live + 4 * (size_t)gi.node_off);
-    for (int x = x0; x < x1; ++x) {
-      if (uf_load(E.deg0, x) > 0) {
-        int b0, e0_, b1, e1_;
-        if constexpr (GL) {
-          b0 = E.grp[0][x]; e0_ = E.grp[0][x + 1]; b1 = E.grp[1][x]; e1_ = E.grp[1][x + 1];
-        } else {
-          b0 = E.rp[0][x]; e0_ = E.rp[0][x + 1]; b1 = E.rp[1][x]; e1_ = E.rp[1][x + 1];
-        }
-        if (MD_BOK(k < n, 9))
-          stc4(lv, k * 16, make_float4(__int_as_float(x), __int_as_float(b0), __int_as_float(b1),
-                                       __int_as_float((e0_ - b0) | ((e1_ - b1) << 16))));
-        ++k;
-      }
-    }
-  }
-
+  const int tot = ag.nlive, dm0 = ag.dm0, dm1 = ag.dm1, sd0 = ag.sd0, sd1 = ag.sd1, bad = ag.bad;
+  const long long th0 = ag.th0, th1 = ag.th1;
+  MD_PROF_A(34);
   if (bad && !err) err = ERR_LIVE_MISMATCH;
   const int hd0 = gv.hdmax[0], hd1 = gv.hdmax[1];
   __syncthreads();

@@ -475,6 +475,7 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
   // a dedicated environment workgroup that already stepped this graph in this launch holds
   // its current GraphVar in LDS (nobody else writes it during a launch)
   if (!(staged && p.n_env > 0)) gv_load(p, g, &gv);
+  if (threadIdx.x == 0) misc[5] = 0;
   __syncthreads();
   int pend_n = 0, pend_first = -1;
   bool stop = false;
@@ -513,6 +514,13 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
         const int i2 = __shfl_xor(bi, o, 64), c2 = __shfl_xor(bc, o, 64);
         if (c2 != 0) argmax_combine(bm, bs, bi, bc, m2, s2, i2, c2);
       }
+    } else if ((int)threadIdx.x < 64 + p.n_spec) {
+      // speculative results' tags, read beside the partials (env_step matches them against
+      // the chosen node without a round trip of its own)
+      const g_u64* tp = (const g_u64*)(p.sres + (size_t)(threadIdx.x - 64) * p.sres_stride);
+      unsigned long long* pre = (unsigned long long*)(lds + L_PREF) + 2 * (threadIdx.x - 64);
+      pre[0] = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pre[1] = __hip_atomic_load(tp + SRES_STARTED / 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (threadIdx.x == 0) {
       const int t = gv.npred;
@@ -532,6 +540,7 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
       gv.argmax = bc == 1 ? bi : -1;
       misc[1] = bi;
       misc[2] = bc;
+      misc[5] = 1;  // speculative tags pre-read in L_PREF
     }
     __syncthreads();
     if (p.run_mode == RUN_PREDICT) {
@@ -2327,7 +2336,10 @@ __device__ __noinline__ void spec_loop(KParams&) {
     const int nd = E.hdr[1];
     for (int i = threadIdx.x; i < nd; i += NTHREADS) {
       const int e = E.dl[i];
-      stc(slot + SRES_HDR + i, e | ((int)E.st[e] << 16));
+      const int l = e < E.e0 ? 0 : 1, kk = e < E.e0 ? e : e - E.e0;
+      stc(slot + SRES_HDR + 3 * i, e | ((int)E.st[e] << 16));
+      stc(slot + SRES_HDR + 3 * i + 1, E.epos[l][2 * kk]);
+      stc(slot + SRES_HDR + 3 * i + 2, E.epos[l][2 * kk + 1]);
     }
     if (threadIdx.x == 0) {
       stc(slot + 2, lm);
@@ -2345,6 +2357,28 @@ __device__ __noinline__ void spec_loop(KParams&) {
     if (threadIdx.x == 0)  // {killed edges << 48 | node << 32 | request tag}, one 8-byte granule
       __hip_atomic_store((g_u64*)slot, ((unsigned long long)(unsigned)(c | (nd << 16)) << 32) | tag,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // then the features of the state after c (degrees, live list, aggregates), tagged apart:
+    // phase A takes them when they are there, computes them itself otherwise
+    const EnvAgg ag = env_features<false>(E, n, slot + sres_deg(et), slot + sres_deg(et) + n,
+                                          (float*)(slot + sres_live(et, n)), nullptr);
+    if (threadIdx.x == 0) {
+      stc(slot + 12, ag.nlive);
+      stc(slot + 13, ag.dm0);
+      stc(slot + 14, ag.dm1);
+      stc(slot + 15, ag.sd0);
+      stc(slot + 16, ag.sd1);
+      stc(slot + 17, ag.bad);
+      stc(slot + 18, (int)(ag.th0 & 0xffffffffll));
+      stc(slot + 19, (int)(ag.th0 >> 32));
+      stc(slot + 20, (int)(ag.th1 & 0xffffffffll));
+      stc(slot + 21, (int)(ag.th1 >> 32));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store((g_u64*)(slot + SRES_FEAT), ((unsigned long long)(unsigned)c << 32) | tag, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    TSTAMP(74);
   }
 }
 

@@ -8,10 +8,25 @@ W = _lib.pack_weights(dict(np.load(os.path.join(ROOT, "mdcommunity_amd/weights/u
 NAMES = ["A:mcc", "A:feat", "A:end", "barA", "p1", "bar1", "p2", "bar2", "p3", "bar3"]
 
 def prof(name, team):
-    z = np.load(os.path.join(ROOT, f"tests/golden/rollout_{name}.npz"))
+    if name == "real":  # the testReal-sized synthetic multiplex (mdcommunity_amd.synth, N = 18000)
+        from mdcommunity_amd import synth
+        layers = synth.real_like_layers(18000, 0)
+        n = 18000
+        es = []
+        for lay in layers:
+            seen, order = set(), []
+            for u, v in lay:
+                k = (min(u, v), max(u, v))
+                if u != v and k not in seen:
+                    seen.add(k)
+                    order.append(k)
+            es.append(np.array(sorted(order), np.int32))
+        z = {"edges0": es[0], "edges1": es[1], "seq": np.zeros(1)}
+    else:
+        z = np.load(os.path.join(ROOT, f"tests/golden/rollout_{name}.npz"))
+        n = int(z["n_nodes"])
     eng = _lib.Engine(W)
     eng.set_team_size(team)
-    n = int(z["n_nodes"])
     eng.load_graphs([(n, z["edges0"], z["edges1"])])
     eng.reset()
     eng.rollout()  # warm
@@ -94,7 +109,7 @@ def batch(nb, team):
 
 if __name__ == "__main__":
     for team in [int(x) for x in sys.argv[1].split(",")]:
-        prof("gmm1000_s0", team)
+        prof(os.environ.get("MD_PROF_GRAPH", "gmm1000_s0"), team)
     if len(sys.argv) > 2:
         for nb in [int(x) for x in sys.argv[2].split(",")]:
             batch(nb, 0)

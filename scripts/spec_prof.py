@@ -37,10 +37,12 @@ chk = rows[:, 69] > 0
 hit = rows[:, 70] > 0
 print(f"requests {len(rows)}; wg0 done {have.sum()}; checks {chk.sum()}; hits {hit.sum()}")
 med = lambda x: float(np.median(x)) if len(x) else float("nan")
-print("wg0 (us after request): seen %.1f  loaded %.1f  candidate %.1f  taken %.1f  done %.1f" % (
-    med(us(64, 65)[have]), med(us(64, 73)[have]), med(us(64, 66)[have]), med(us(64, 67)[have]), med(us(64, 68)[have])))
+print("wg0 (us after request): seen %.1f  loaded %.1f  candidate %.1f  taken %.1f  done %.1f  features %.1f" % (
+    med(us(64, 65)[have]), med(us(64, 73)[have]), med(us(64, 66)[have]), med(us(64, 67)[have]), med(us(64, 68)[have]),
+    med(us(64, 74)[have])))
 print("next phase A (us after request): check start %.1f  check end %.1f (wait %.1f, mean %.1f); hit result done %.1f" % (
     med(us(64, 69)[chk]), med(us(64, 71)[chk]), med(us(69, 71)[chk]), float(np.mean(us(69, 71)[chk])), med(us(64, 72)[hit])))
+print("features copied in %d of %d profiled steps" % (int((P[:, 75] > 0).sum()), len(P)))
 print("hit slots (rank + 1):", np.bincount(rows[:, 70][chk].astype(int), minlength=17).tolist())
 late = us(69, 71)[chk]
 print("waits > 5 us: %d; largest %s" % ((late > 5).sum(), np.round(np.sort(late)[-8:], 1).tolist()))
