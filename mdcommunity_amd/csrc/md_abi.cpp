@@ -113,6 +113,7 @@ struct md_ctx {
   DevBuf<int> qg;                    // queue-mode per-graph stage counters
   // speculative environment steps (single-graph rollouts): result slots, Q of the last two
   // predictions; spec_n workgroups per launch when the CUs are free (MD_SPEC, default 16, 0 = off)
+  DevBuf<unsigned> bars;  // grid-barrier counter shards
   DevBuf<int> sres;
   DevBuf<float> qspec;
   int sres_stride = 0;
@@ -154,7 +155,7 @@ struct md_ctx {
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
     tr_stat.release(); glist.release(); ctl.release(); q.release(); spart.release();
     apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); nbc.release(); qslot.release(); qg.release(); tr_q.release(); node_w.release();
-    sres.release(); qspec.release();
+    sres.release(); qspec.release(); bars.release();
     h_req.release(); h_ans.release(); h_nact.release(); h_act.release(); h_q.release(); h_chk.release();
     ng = 0;
     hinfo.clear();
@@ -223,6 +224,7 @@ Params make_params(md_ctx* c) {
   p.h0g = c->h0g.p;
   p.h0g_dm = c->h0g.p ? c->h0g_dm : 0;
   p.bar = (unsigned*)(c->ctl.p + CTL_BAR);
+  p.bars = c->bars.p;
   p.err = c->ctl.p + CTL_ERR;
   p.qctl = (unsigned*)(c->ctl.p + CTL_Q);
   p.qslot = c->qslot.p;
@@ -438,11 +440,15 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
   // speculative environment workgroups on the CUs a single-graph rollout leaves free
   // (single-node steps only: step > 1 takes several removals per prediction)
   const int n_spec = run_mode == RUN_ROLLOUT && n_env == 1 && ngl == 1 && !host_select && c->sres.p != nullptr &&
-                             spec_fits_lds_host(c->hinfo[gl[0]].n, c->hinfo[gl[0]].e[0] + c->hinfo[gl[0]].e[1])
+                             spec_fits_lds_host(c->hinfo[gl[0]].n, c->hinfo[gl[0]].e[0] + c->hinfo[gl[0]].e[1]) &&
+                             // word-aligned state arrays (the speculative staging reads 4 states per load)
+                             c->hinfo[gl[0]].eoff[0] % 4 == 0 && c->hinfo[gl[0]].eoff[1] % 4 == 0 &&
+                             c->hinfo[gl[0]].node_off % 4 == 0
                          ? std::max(0, std::min(c->spec_n, c->cus - grid))
                          : 0;
   HIPCHK(c, hipMemcpyAsync(c->glist.p, gl, sizeof(int) * ngl, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->ctl.p, 0, sizeof(int) * CTL_WORDS, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->bars.p, 0, sizeof(unsigned) * c->bars.n, c->stream));
   // graph-head hand-off granules carry the step as their tag: stale tags from earlier launches
   // must not match
   if (n_env > 0) HIPCHK(c, hipMemsetAsync(c->hbuf.p, 0, sizeof(float) * c->hbuf.n, c->stream));
@@ -780,7 +786,7 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
     HIPCHK(c, c->calive[l].alloc(std::max<size_t>(1, 2 * te[l])));
     HIPCHK(c, c->eu[l].alloc(std::max<size_t>(1, eu[l].size())));
     HIPCHK(c, c->ev[l].alloc(std::max<size_t>(1, ev[l].size())));
-    HIPCHK(c, c->estate[l].alloc(std::max<size_t>(1, te[l])));
+    HIPCHK(c, c->estate[l].alloc(te[l] + 4));  // + 4: whole-word reads of the last states
     HIPCHK(c, c->deg[l].alloc(tn));
     HIPCHK(c, c->h0tab[l].alloc(tn * EMB));
     HIPCHK(c, c->H[l][0].alloc(tn * EMB));
@@ -793,7 +799,7 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
       HIPCHK(c, hipMemcpyAsync(c->ev[l].p, ev[l].data(), sizeof(int) * ev[l].size(), hipMemcpyHostToDevice, c->stream));
     }
   }
-  HIPCHK(c, c->covered.alloc(tn));
+  HIPCHK(c, c->covered.alloc(tn + 4));
   HIPCHK(c, c->live.alloc(4 * tn));  // {node, CSR begin l0, l1, extents} per live position
   HIPCHK(c, c->gscr.alloc(4 * tn));  // global-mode environment scratch (16 B per node; always, so MD_VARIANT=64 can force that mode)
   HIPCHK(c, c->pend.alloc(tn));
@@ -804,6 +810,7 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->q.alloc(tn));
   HIPCHK(c, c->glist.alloc(n_graphs));
   HIPCHK(c, c->ctl.alloc(CTL_WORDS));
+  HIPCHK(c, c->bars.alloc(8 * 64));
   HIPCHK(c, c->spart.alloc(tt * 384));
   HIPCHK(c, c->apart.alloc(tt * 4));
   HIPCHK(c, c->ybuf.alloc((size_t)n_graphs * 128));

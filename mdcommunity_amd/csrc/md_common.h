@@ -111,7 +111,8 @@ struct Params {
   int* tr_stat;                    // per node slot x 4: n_live, m0, m1, ntie per prediction
   float* tr_q;                     // per node slot x 2: qmax, gap per prediction
   const float* node_w;             // degree cost: [2][total nodes] static features, else null
-  unsigned* bar;                   // grid barrier counter (zeroed per launch)
+  unsigned* bar;                   // error word of the grid barrier (bit 31; zeroed per launch)
+  unsigned* bars;                  // grid barrier arrival counters: 8 shards x 64 words (zeroed per launch)
   // host selection hand-shake (mapped pinned host memory; null: end the launch instead)
   unsigned* h_req;                 // per graph: request tag (device writes)
   unsigned* h_ans;                 // per graph: answer tag (host writes)

@@ -996,6 +996,19 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
     if (threadIdx.x == 0) E.hdr[1] = 0;
   }
   MD_PROF_A(14);
+  if (p.n_spec > 0 && !err && gv.alive[0] > 0 && gv.alive[1] > 0 && ((const volatile int*)(lds_base + L_MISC))[5]) {
+    // the state after this step is in HBM once every store has drained: ask the speculative
+    // workgroups for the next step's fixed point of the likely next removals (before the
+    // first-layer table, which they do not read)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int ps = ((const volatile int*)(lds_base + L_MISC))[60];
+      __hip_atomic_store((g_u64*)p.spec_req, ((unsigned long long)(unsigned)ps << 32) | spec_tag(p.launch_seq, gv.steps),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (p.prof != nullptr && ps < p.prof_cap) p.prof[(size_t)ps * PROF_SLOTS + 64] = wall_clock64();
+    }
+  }
   // First-layer embedding by degree (unit cost): X = [d/dmax, d/dmax] (net :252-261),
   // normalize(relu(X . w_n2l)) with the 2-term FMA chain of MKL's sgemm; one thread per row
   // d = 1..dmax (the row recomputed for the norm pass and the store pass; w_n2l arrives as

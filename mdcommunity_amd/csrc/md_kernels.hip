@@ -248,6 +248,7 @@ __device__ __forceinline__ void gv_store(KParams& p, int g, const GraphVar* src)
 // separate load of the error word on the critical path.  Bounded spin: a timeout raises
 // ERR_TIMEOUT the same way, so the grid drains.
 constexpr unsigned BAR_ERR = 0x80000000u;
+constexpr int BAR_SHARDS = 8, BAR_STRIDE = 64;  // grid-barrier counter shards, one 256-byte line each
 __device__ __forceinline__ void raise_err(KParams& p, int code) {
   __hip_atomic_store(p.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_fetch_or((g_u32*)p.bar, BAR_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -263,24 +264,38 @@ __device__ __forceinline__ bool md_bok(bool ok, int site) {
 #else
 #define MD_BOK(cond, site) true
 #endif
-// returns true (uniformly) when an error was raised anywhere in the grid
+// returns true (uniformly) when an error was raised anywhere in the grid.
+// The arrival counter is sharded over BAR_SHARDS words on lines of their own (workgroup b adds
+// to shard b % BAR_SHARDS): one-word fan-in serialises every arrival at the memory side
+// (~12 ns each, MI355X_MICROARCH.md fanin row), the shards take 1/8 of them each.  Wave 0
+// polls every shard and the error word in one instruction; `target` counts this workgroup's
+// barriers.  Speculative workgroups (blockIdx >= n_main) take no part.
 __device__ __forceinline__ bool grid_sync(KParams& p, unsigned& target, int* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  target += p.n_main;  // speculative workgroups (if any) are not part of the barrier
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add((g_u32*)p.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  target += 1;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    if (lane == 0)
+      __hip_atomic_fetch_add((g_u32*)(p.bars + BAR_STRIDE * (blockIdx.x % BAR_SHARDS)), 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned want = lane < BAR_SHARDS ? target * (unsigned)((p.n_main - lane + BAR_SHARDS - 1) / BAR_SHARDS) : 0u;
+    const g_u32* w = (const g_u32*)(lane < BAR_SHARDS ? p.bars + BAR_STRIDE * lane : p.bar);
     const unsigned long long t0 = wall_clock64();
-    unsigned v;
-    while ((v = __hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < target) {
+    int err = 0;
+    while (true) {
+      const unsigned v = lane <= BAR_SHARDS ? __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      const bool lag = lane < BAR_SHARDS && v < want;
+      if (__ballot(lane == BAR_SHARDS && (v & BAR_ERR))) { err = 1; break; }
+      if (!__ballot(lag)) break;
       __builtin_amdgcn_s_sleep(1);
       if (wall_clock64() - t0 > (p.h_req != nullptr ? HOST_TIMEOUT_TICKS : BARRIER_TIMEOUT_TICKS)) {
-        raise_err(p, ERR_TIMEOUT);
-        v = BAR_ERR;
+        if (lane == 0) raise_err(p, ERR_TIMEOUT);
+        err = 1;
         break;
       }
     }
-    *flag = (v & BAR_ERR) != 0;
+    if (lane == 0) *flag = err;
   }
   __syncthreads();
   return *flag != 0;
@@ -620,18 +635,6 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
   __syncthreads();
   gv_store(p, g, &gv);
   __syncthreads();
-  if (p.n_spec > 0 && have_q && gv.status == ST_RUN) {
-    // the state after this step is in HBM (every store drained): ask the speculative
-    // workgroups for the next step's fixed point of the likely next removals
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __hip_atomic_store((g_u64*)p.spec_req,
-                         ((unsigned long long)(unsigned)misc[60] << 32) | spec_tag(p.launch_seq, gv.steps),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (p.prof != nullptr && misc[60] < p.prof_cap) p.prof[(size_t)misc[60] * PROF_SLOTS + 64] = wall_clock64();
-    }
-  }
   return staged;
 }
 
@@ -1814,6 +1817,15 @@ __device__ __forceinline__ int q_tiles_per_item(KParams& p) {
   const int f = (p.variant >> 9) & 3;
   return f == 0 ? 2 : f;
 }
+// In the launch's tail (every graph admitted and at most q_tail(p) still running) a step's
+// tiles go one per item: fewer graphs share the chip, so each stage's items are spread over
+// more workgroups (per graph and step the tiles per item are fixed: qg word bits 28-29).
+// MD_VARIANT bits 12-14 = k set the tail at 16 k running graphs (7: never), default 1/8 of
+// the workgroups.
+__device__ __forceinline__ int q_tail(KParams& p) {
+  const int v = (p.variant >> 12) & 7;
+  return v == 0 ? (int)gridDim.x / 8 : (v == 7 ? -1 : 16 * v);
+}
 // Pushes n items f(0..n-1); every thread of the workgroup calls it.
 template <class F>
 __device__ __forceinline__ void q_push(KParams& p, int n, F&& f, int* bc) {
@@ -2105,8 +2117,15 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
         break;
       }
       if (st == ST_RUN) {
-        const int nt = (nl + TILE - 1) / TILE, tpi = q_tiles_per_item(p), ni = (nt + tpi - 1) / tpi;
-        if (threadIdx.x == 0) stc(p.qg + 2 * gl + 1, ni | (nt << 16));
+        if (threadIdx.x == 0) {  // one decision for the workgroup
+          int t = q_tiles_per_item(p);
+          if (t > 1 && ldc((const int*)(p.qctl + QC_ADMIT)) >= ng && ldc((const int*)(p.qctl + QC_REM)) <= q_tail(p)) t = 1;
+          bc[5] = t;
+        }
+        __syncthreads();
+        const int tpi = bc[5];
+        const int nt = (nl + TILE - 1) / TILE, ni = (nt + tpi - 1) / tpi;
+        if (threadIdx.x == 0) stc(p.qg + 2 * gl + 1, ni | (nt << 16) | (tpi << 28));
         q_push(p, ni, [&](int i) { return q_item_tile(1, gl, i, nt, tpi); }, bc);
       } else if (st == ST_WAIT_HOST) {
         q_push(p, 1, [&](int) { return q_item(QK_ENV, 1, gl, 0); }, bc);  // poll again later
@@ -2165,7 +2184,7 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
       next = 4;
     }
     if (next != 0) {
-      const int sz = ldc(p.qg + 2 * gl + 1), ni = sz & 0xffff, nt = sz >> 16, tpi = q_tiles_per_item(p);
+      const int sz = ldc(p.qg + 2 * gl + 1), ni = sz & 0xffff, nt = (sz >> 16) & 0xfff, tpi = (sz >> 28) & 3;
       if (next == 1) {
         q_push(p, ni + 1, [&](int i) { return i < ni ? q_item_tile(2, gl, i, nt, tpi) : q_item(QK_VN, 1, gl, 0); }, bc);
       } else if (next == 2) {
@@ -2247,28 +2266,39 @@ __device__ __noinline__ void spec_loop(KParams&) {
     // step t's state and the previous prediction Q(t-1), loads batched; nodes live now were
     // live then, so their entries are that prediction's
     {
-      const int e0 = E.e0, span = max(et, n);
-      for (int b = 0; b < span; b += 8 * NTHREADS) {
-        int ss[8], cv[8], dd[8];
-        float qq[8];
+      // edge states and covered flags as whole words (4 per load; the single graph's arrays
+      // start word-aligned and have 4 bytes of slack at the end)
+      const int e0 = E.e0, e1 = et - e0, w0 = (e0 + 3) >> 2, w1 = (e1 + 3) >> 2, wn = (n + 3) >> 2;
+      const int span = max(max(w0 + w1, wn), n);
+      for (int b = 0; b < span; b += 4 * NTHREADS) {
+        unsigned sw[4], cw[4];
+        int dd[4];
+        float qq[4];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < 4; ++u) {
           const int i = b + u * NTHREADS + threadIdx.x;
-          if (i < et) ss[u] = ldc(E.gst[i < e0 ? 0 : 1] + (i < e0 ? i : i - e0));
+          if (i < w0 + w1) sw[u] = ldc((const int*)(i < w0 ? E.gst[0] + 4 * i : E.gst[1] + 4 * (i - w0)));
+          if (i < wn) cw[u] = ldc((const int*)(E.gcov + 4 * i));
           if (i < n) {
-            cv[u] = ldc(E.gcov + i);
             dd[u] = ldc(p.deg[0] + gi.node_off + i);
             qq[u] = ldc(p.qspec + (size_t)qb * p.qspec_n + gi.node_off + i);
           }
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < 4; ++u) {
           const int i = b + u * NTHREADS + threadIdx.x;
-          if (i < et) E.st[i] = (uint8_t)ss[u];
-          if (i < n) {
-            E.cov8[i] = (uint8_t)cv[u];
-            qv[i] = dd[u] > 0 ? qq[u] : NEG_INF;
+          if (i < w0 + w1) {
+            const int base = i < w0 ? 4 * i : e0 + 4 * (i - w0), lim = i < w0 ? e0 : et;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (base + k < lim) E.st[base + k] = (uint8_t)(sw[u] >> (8 * k));
           }
+          if (i < wn) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (4 * i + k < n) E.cov8[4 * i + k] = (uint8_t)(cw[u] >> (8 * k));
+          }
+          if (i < n) qv[i] = dd[u] > 0 ? qq[u] : NEG_INF;
         }
       }
     }
