@@ -361,6 +361,26 @@ __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* tot) {
 
 #include "md_env.h"
 
+// Sum of one column of a transposed tile (a[row], rows 0..15) over its first nv rows (the valid
+// rows are a prefix), added in row order; every LDS read is issued before the first add (a
+// break-at-the-first-invalid-row loop is a chain of dependent LDS round trips).
+__device__ __forceinline__ float col_sum16(const float* a, int nv) {
+  float v[TILE];
+#pragma unroll
+  for (int r = 0; r < TILE; ++r) v[r] = a[r];
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < TILE; ++r)
+    if (r < nv) s = s + v[r];
+  return s;
+}
+__device__ __forceinline__ int tile_rows_valid(const int* rows) {
+  int nv = 0;
+#pragma unroll
+  for (int r = 0; r < TILE; ++r) nv += rows[r] >= 0;
+  return nv;
+}
+
 // Merge arg-max partial (m2, s2, i2, c2) into (bm, bs, bi, bc); c = 0 marks an empty partial.
 __device__ __forceinline__ void argmax_combine(float& bm, float& bs, int& bi, int& bc, float m2, float s2,
                                                int i2, int c2) {
@@ -1974,12 +1994,8 @@ __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int
     const int l = threadIdx.x >> 6, c = threadIdx.x & 63;
     const float* ate = scr + S_E + l * 64 * LDT + c * LDT;
     const float* atx = scr + S_X + l * 64 * LDT + c * LDT;
-    float s_new = 0.f, s_old = 0.f;
-    for (int r = 0; r < TILE; ++r) {
-      if (rows[r] < 0) break;
-      s_new = s_new + ate[r];
-      s_old = s_old + atx[r];
-    }
+    const int nv = tile_rows_valid(rows);
+    const float s_new = col_sum16(ate, nv), s_old = it == 1 ? col_sum16(atx, nv) : 0.f;
     float* sp = p.spart + (size_t)(gi.tile_off + j) * 384;
     if (it == 1) {
       stc(sp + l * 64 + c, s_old);        // S0 (first-layer input)
@@ -2659,12 +2675,8 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
           const int l = sit ? L : (int)threadIdx.x >> 6, c = threadIdx.x & 63;
           const float* ate = scr + S_E + l * 64 * LDT + c * LDT;
           const float* atx = scr + S_X + l * 64 * LDT + c * LDT;
-          float s_new = 0.f, s_old = 0.f;
-          for (int r = 0; r < TILE; ++r) {
-            if (rows[r] < 0) break;
-            s_new = s_new + ate[r];
-            s_old = s_old + atx[r];
-          }
+          const int nv = tile_rows_valid(rows);
+          const float s_new = col_sum16(ate, nv), s_old = it == 1 ? col_sum16(atx, nv) : 0.f;
           float* sp = p.spart + (size_t)(gi.tile_off + j) * 384;
           if (it == 1) {
             stc(sp + l * 64 + c, s_old);        // S0 (first-layer input)
