@@ -179,6 +179,10 @@ const char* md_version(void);
  *                       256   push single-item stages instead of running them inline (queue mode)
  *                       512..1536 (bits 9-10 = 1..3)  tiles per queue work item (default 2)
  *                       2048  K2 end-game shortcut off (one forward pass per removal step)
+ *                       4096  queue mode: iteration-1 tiles build their own neighbour lists
+ *                             instead of loading the ones the environment item wrote
+ *                       bits 13-15 = k  queue-mode tail threshold at 16 k running graphs
+ *                             (7: never; default 1/8 of the admission limit)
  *                       bits 16+  queue-mode admission limit (graphs running at once)
  *   MD_ENV_MODE       0: no dedicated environment workgroups for small batches (shared
  *                     mode); default 1

@@ -849,7 +849,7 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, hipStreamSynchronize(c->stream));
   // queue-mode buffers last (allocation order moves the other buffers' addresses)
   HIPCHK(c, c->qslot.alloc(Q_CAP));
-  HIPCHK(c, c->qg.alloc(2 * G_CAP));
+  HIPCHK(c, c->qg.alloc(3 * G_CAP));  // stage counter, stage size per graph slot; lists-built flag
   {
     // speculative-step slots: killed-edge lists of one graph (LDS-mode graphs only)
     int maxw = 0;

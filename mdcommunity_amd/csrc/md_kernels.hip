@@ -1639,17 +1639,36 @@ __device__ __noinline__ void attention_q_tile(KParams&, float*, float*, const Gr
   }
   __syncthreads();
   TSTAMP(33);
+  TSTAMP(35);
+  // mix E_l = F_l + gate * F_other (mul then add, as the reference) fused into the first pass
+  // of the row normalisation (each element is read there by exactly one thread)
   {
-    const float* oth = scr + S_F + (1 - l) * 64 * LDT;
+    float* red = scr + S_RED;
+    const int t = threadIdx.x;
+    if (t < 256) {
+      const int ll = t >> 7, row = (t >> 3) & 15, j = t & 7;
+      const float* f = scr + S_F + ll * 64 * LDT;
+      const float* o = scr + S_F + (1 - ll) * 64 * LDT;
+      float* e = scr + S_E + ll * 64 * LDT;
+      const float gt = gate[ll * 16 + row];
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int c = 8 * i + j;
+        const float v = f[c * LDT + row] + gt * o[c * LDT + row];
+        e[c * LDT + row] = v;
+        acc = fmaf(v, v, acc);
+      }
+      red[(ll * 16 + row) * 8 + j] = acc;
+    }
+    __syncthreads();
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 4 * ak + r;
-      ate[col * LDT + row] = atf[col * LDT + row] + gate[l * 16 + row] * oth[col * LDT + row];
+      const float den = fmaxf(sqrtf(sumsq8_finish(red + (l * 16 + row) * 8)), 1e-12f);
+      ate[col * LDT + row] = ate[col * LDT + row] / den;
     }
   }
-  __syncthreads();
-  TSTAMP(35);
-  normalize_tile(scr + S_E, scr);
   __syncthreads();
   TSTAMP(39);
   if (htag != 0ull) head_receive(p, lds, g, htag);
@@ -1660,31 +1679,34 @@ __device__ __noinline__ void attention_q_tile(KParams&, float*, float*, const Gr
     // runs four independent chains of one layer (256 threads per layer).
     const int ll = threadIdx.x >> 8, t = threadIdx.x & 255;
     const float* at = scr + S_E + ll * 64 * LDT;
-    float h[4], acc[4];
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    f2v h[2], acc[2];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int idx = t + 256 * k, row = idx >> 6, a = idx & 63;
-      h[k] = at[a * LDT + row];
-      acc[k] = 0.f;
+      h[k >> 1][k & 1] = at[a * LDT + row];
+      acc[k >> 1][k & 1] = 0.f;
     }
     const float4* y4 = (const float4*)(lds + L_YS + ll * 64);
     const float4* c4 = (const float4*)(wi + W_ICP);
+    // chains k = 0..3 in pairs: packed multiply then packed FMA per b (each component rounds
+    // exactly as h * y then fmaf(., cp, acc))
 #pragma unroll 4
     for (int b4 = 0; b4 < 16; ++b4) {
       const float4 yv = y4[b4], cv = c4[b4];
+      const float ys[4] = {yv.x, yv.y, yv.z, yv.w}, cs[4] = {cv.x, cv.y, cv.z, cv.w};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        acc[k] = fmaf(h[k] * yv.x, cv.x, acc[k]);
-        acc[k] = fmaf(h[k] * yv.y, cv.y, acc[k]);
-        acc[k] = fmaf(h[k] * yv.z, cv.z, acc[k]);
-        acc[k] = fmaf(h[k] * yv.w, cv.w, acc[k]);
+      for (int q = 0; q < 4; ++q) {
+        const f2v yy = {ys[q], ys[q]}, cc = {cs[q], cs[q]};
+#pragma unroll
+        for (int k2 = 0; k2 < 2; ++k2) acc[k2] = __builtin_elementwise_fma(h[k2] * yy, cc, acc[k2]);
       }
     }
     float* af = scr + S_F + ll * 64 * LDT;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int idx = t + 256 * k, row = idx >> 6, a = idx & 63;
-      af[a * LDT + row] = acc[k];
+      af[a * LDT + row] = acc[k >> 1][k & 1];
     }
   }
   __syncthreads();
@@ -1715,7 +1737,10 @@ __device__ __noinline__ void attention_q_tile(KParams&, float*, float*, const Gr
     for (int k = 0; k < 4; ++k) a = fmaf(gs[4 + ll * 4 + k], wi[W_IW2 + 32 + k], a);
     ql[ll * 16 + row] = a;
   }
-  __syncthreads();
+  // the arg-max partial below runs on the same wave: its LDS writes are visible to itself
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   TSTAMP(42);
   if (threadIdx.x < 64) {
     // q = w0 * Q0 + w1 * Q1 per row, and the tile's arg-max partial by a 16-lane butterfly
@@ -1840,10 +1865,10 @@ __device__ __forceinline__ int q_tiles_per_item(KParams& p) {
 // In the launch's tail (every graph admitted and at most q_tail(p) still running) a step's
 // tiles go one per item: fewer graphs share the chip, so each stage's items are spread over
 // more workgroups (per graph and step the tiles per item are fixed: qg word bits 28-29).
-// MD_VARIANT bits 12-14 = k set the tail at 16 k running graphs (7: never), default 1/8 of
+// MD_VARIANT bits 13-15 = k set the tail at 16 k running graphs (7: never), default 1/8 of
 // the workgroups.
 __device__ __forceinline__ int q_tail(KParams& p) {
-  const int v = (p.variant >> 12) & 7;
+  const int v = (p.variant >> 13) & 7;
   return v == 0 ? (int)gridDim.x / 8 : (v == 7 ? -1 : 16 * v);
 }
 // Pushes n items f(0..n-1); every thread of the workgroup calls it.
@@ -1908,6 +1933,159 @@ __device__ __forceinline__ unsigned q_wait(KParams& p, unsigned tk, int* bc, uns
   return item;
 }
 
+// Queue mode, after phase A of graph slot gl in LDS mode: the alive neighbour lists of every
+// tile of the step, both layers, written to the tiles' neighbour-list cache slots in
+// nbc_store's format, so the iteration-1 tiles reload them like iterations 2-3 instead of each
+// building its own (one pass over the live rows' CSR entries on one workgroup instead of one
+// flag round trip, scan and compaction per tile).  The same lists: live rows in ascending id
+// order, 16 per tile, each row's alive CSR entries in CSR order (the reference's in_edges
+// order); a tile whose layer has more than NB_CAP entries gets ok = 0 (the per-row gather).
+// Returns false (the tiles build their lists) when the scratch does not fit.
+__device__ __noinline__ bool env_build_lists(KParams&, const GraphInfo gi, int gl) {
+  KParams& p = kp();
+  float* const lds = lds_base();
+  int* ia = (int*)(lds + L_W);
+  const int n = gi.n, et = gi.e[0] + gi.e[1];
+  const EnvLayout Lo = env_layout(n, et);
+  const EnvView<false> E = env_view<false>(p, gi, ia);
+  const int nl = ((const GraphVar*)(lds + L_GV))->n_live, nt = (nl + TILE - 1) / TILE;
+  if (Lo.total + 3 * nl + 2 * nt + 8 > A_WORDS || gl * p.nbc_gstride + nt > p.nbc_slots || nl <= 0) return false;
+  // scratch after the environment: node of each live position, per-position prefixes of the
+  // CSR extent and of the alive count (nl + 1 each), per-tile alive totals of both layers
+  int* pn = ia + Lo.total;
+  int* px = pn + nl;
+  int* pd = px + nl + 1;
+  int* tt = pd + nl + 1;
+  int* tmp = E.tmp;
+  int* base_slot = p.nbc + (size_t)gl * p.nbc_gstride * NBC_INTS;
+  {
+    // live positions (ascending ids, as the live list)
+    const int chunk = (n + NTHREADS - 1) / NTHREADS;
+    const int x0 = min(n, (int)threadIdx.x * chunk), x1 = min(n, x0 + chunk);
+    int c = 0;
+    for (int x = x0; x < x1; ++x) c += uf_load(E.deg0, x) > 0;
+    int tot = 0;
+    int k = block_excl_scan(c, tmp, &tot);
+    for (int x = x0; x < x1; ++x)
+      if (uf_load(E.deg0, x) > 0) pn[k++] = x;
+  }
+  __syncthreads();
+  for (int l = 0; l < 2; ++l) {
+    const lds_i32* rp = E.rp[l];
+    const auto dg = l ? E.deg1 : E.deg0;
+    const int* adj = p.adj[l] + gi.coff[l];
+    const uint8_t* ca = p.calive[l] + gi.coff[l];
+    // prefixes over live positions of the CSR extent and of the alive count
+    const int chunk = (nl + NTHREADS - 1) / NTHREADS;
+    const int i0 = min(nl, (int)threadIdx.x * chunk), i1 = min(nl, i0 + chunk);
+    int se = 0, sd = 0;
+    for (int i = i0; i < i1; ++i) {
+      const int x = pn[i];
+      se += rp[x + 1] - rp[x];
+      sd += uf_load(dg, x);
+    }
+    int te = 0, td = 0;
+    int oe = block_excl_scan(se, tmp, &te);
+    int od = block_excl_scan(sd, tmp, &td);
+    for (int i = i0; i < i1; ++i) {
+      const int x = pn[i];
+      px[i] = oe;
+      pd[i] = od;
+      oe += rp[x + 1] - rp[x];
+      od += uf_load(dg, x);
+    }
+    if (threadIdx.x == 0) {
+      px[nl] = te;
+      pd[nl] = td;
+    }
+    __syncthreads();
+    // the CSR entries of the live rows in order, a contiguous run per thread: alive flags,
+    // then each alive entry's place in its tile's list (an entry's index among the layer's
+    // alive entries, minus that of the tile's first row)
+    const int ce = (te + NTHREADS - 1) / NTHREADS;
+    const int e0 = min(te, (int)threadIdx.x * ce), e1 = min(te, e0 + ce);
+    int i = 0;
+    {
+      int lo = 0, hi = nl - 1;  // last position with px[i] <= e0
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (px[mid] <= e0) lo = mid; else hi = mid - 1;
+      }
+      i = lo;
+    }
+    const int ist = i;
+    // flag loads eight at a time (all in flight before the first is used)
+    constexpr int B = 8;
+    int keep = 0;
+    for (int b = e0; b < e1; b += B) {
+      int cp[B], f[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int e = b + u;
+        cp[u] = -1;
+        if (e < e1) {
+          while (px[i + 1] <= e) ++i;
+          cp[u] = rp[pn[i]] + (e - px[i]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) f[u] = cp[u] >= 0 ? ldc(ca + cp[u]) : 0;
+#pragma unroll
+      for (int u = 0; u < B; ++u) keep += f[u] != 0;
+    }
+    int tk = 0;
+    int o = block_excl_scan(keep, tmp, &tk);
+    i = ist;
+    for (int b = e0; b < e1; b += B) {
+      int cp[B], ps[B], f[B], nb[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int e = b + u;
+        cp[u] = -1;
+        ps[u] = 0;
+        if (e < e1) {
+          while (px[i + 1] <= e) ++i;
+          cp[u] = rp[pn[i]] + (e - px[i]);
+          ps[u] = i;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        f[u] = cp[u] >= 0 ? ldc(ca + cp[u]) : 0;
+        nb[u] = cp[u] >= 0 ? adj[cp[u]] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        if (!f[u]) continue;
+        const int j = ps[u] >> 4, w = o - pd[j << 4];
+        if (w < NB_CAP) {
+          uint16_t* ent = (uint16_t*)(base_slot + (size_t)j * NBC_INTS + NBC_HDR + l * NBC_LWORDS);
+          __hip_atomic_store((__attribute__((address_space(1))) uint16_t*)(ent + w), (uint16_t)nb[u],
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        ++o;
+      }
+    }
+    // headers: per row its offset and count in the tile's list, per tile the total
+    for (int q = threadIdx.x; q < nt * TILE; q += NTHREADS) {
+      const int j = q >> 4, r = q & 15, at = (j << 4) + r, end = min(nl, (j + 1) << 4);
+      int* hd = base_slot + (size_t)j * NBC_INTS;
+      const int tot = pd[end] - pd[j << 4];
+      stc(hd + l * 16 + r, at < nl ? pd[at] - pd[j << 4] : tot);
+      stc(hd + 32 + l * 16 + r, at < nl ? pd[at + 1] - pd[at] : 0);
+      if (r == 0) {
+        stc(hd + 64 + l, tot);
+        tt[l * nt + j] = tot;
+      }
+    }
+    __syncthreads();
+  }
+  for (int j = threadIdx.x; j < nt; j += NTHREADS)
+    stc(base_slot + (size_t)j * NBC_INTS + 66, (tt[j] <= NB_CAP && tt[nt + j] <= NB_CAP) ? 1 : 0);
+  __syncthreads();
+  return true;
+}
+
 // One tile of one graph for iteration `it` (queue mode; the same pieces and order as the
 // lock-step tile loop).  Neighbour lists: built and cached at iteration 1, reloaded at 2-3.
 __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int it, int j) {
@@ -1935,12 +2113,15 @@ __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int
   } while (0)
   const int slot = gl * p.nbc_gstride + j;
   const bool cacheable = slot < p.nbc_slots && !(p.variant & 16);
-  const bool cached = cacheable && it > 1;
-  int cw = 0, ch = 0;
-  if (cached) {
+  // iteration 1: the environment item built this step's lists when its flag says so (read in
+  // the same round trip as the speculative reload)
+  const bool want = cacheable && (it > 1 || !(p.variant & 4096));
+  int cw = 0, ch = 0, built = 0;
+  if (want) {
     const int* src = p.nbc + (size_t)slot * NBC_INTS;
     cw = ldc(src + NBC_HDR + (threadIdx.x >> 8) * NBC_LWORDS + (threadIdx.x & 255));
     if (threadIdx.x < 67) ch = ldc(src + threadIdx.x);
+    if (it == 1 && threadIdx.x == 67) built = ldc(p.qg + 2 * G_CAP + gl);
   }
   if (threadIdx.x < TILE) {
     const int r = j * TILE + threadIdx.x;
@@ -1955,6 +2136,9 @@ __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int
     hdr[96 + 16 + threadIdx.x] = ok ? (int)(c >> 16) : 0;
   }
   int* misc = (int*)(lds + L_MISC);
+  if (threadIdx.x == 67) misc[58] = it > 1 || built;
+  __syncthreads();
+  const bool cached = want && misc[58] != 0;
   if (cached) {
     ((lds_i32*)(int*)(scr + S_NBL))[(threadIdx.x >> 8) * NBC_LWORDS + (threadIdx.x & 255)] = cw;
     if (threadIdx.x < 64) hdr[threadIdx.x] = ch;
@@ -2121,7 +2305,7 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
     const int it = (int)((item >> 3) & 3u), gl = (int)((item >> 5) & 1023u), j = q_item_j(item);
     const int g = p.glist[gl];
     if (kind == QK_ENV) {
-      phase_a(p, g, it != 0, lds, false);
+      const bool lds_env = phase_a(p, g, it != 0, lds, false);
       pre = q_peek(p, tk);
       wdirty = true;
       const GraphVar& gv = *(const GraphVar*)(lds + L_GV);
@@ -2141,7 +2325,12 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
         __syncthreads();
         const int tpi = bc[5];
         const int nt = (nl + TILE - 1) / TILE, ni = (nt + tpi - 1) / tpi;
-        if (threadIdx.x == 0) stc(p.qg + 2 * gl + 1, ni | (nt << 16) | (tpi << 28));
+        // this step's neighbour lists for the iteration-1 tiles (MD_VARIANT bit 12: off)
+        const bool built = lds_env && !(p.variant & (4096 | 16)) && env_build_lists(p, p.ginfo[g], gl);
+        if (threadIdx.x == 0) {
+          stc(p.qg + 2 * gl + 1, ni | (nt << 16) | (tpi << 28));
+          stc(p.qg + 2 * G_CAP + gl, built ? 1 : 0);
+        }
         q_push(p, ni, [&](int i) { return q_item_tile(1, gl, i, nt, tpi); }, bc);
       } else if (st == ST_WAIT_HOST) {
         q_push(p, 1, [&](int) { return q_item(QK_ENV, 1, gl, 0); }, bc);  // poll again later
