@@ -41,6 +41,23 @@ enum { PA_ROUNDS = 0, PA_UNITE = 1, PA_LABEL = 2, PA_PRUNE = 3, PA_COUNT = 4, PA
 // Global-mode arrays are plain (flat) int pointers with agent-scope atomics; LDS-mode arrays
 // are address-space-3 pointers (ds_* instructions, no aperture conversion, and no aliasing
 // with the private stack, so view fields stay in registers).
+// Queue-mode environment-item piece profile (builds with -DMD_QPROF, MD_VARIANT bit 8): device
+// ticks per piece summed over items in md_profile slots 80.. (scripts/batch_prof.py)
+#ifdef MD_QPROF
+#define QENV_INIT() unsigned long long tqe_ = wall_clock64()
+#define QENV(k)                                                                        \
+  do {                                                                                 \
+    if (p.prof != nullptr && p.qmode && (p.variant & 8) && threadIdx.x == 0) {         \
+      const unsigned long long now_ = wall_clock64();                                  \
+      atomicAdd(p.prof + 80 + (k), now_ - tqe_);                                       \
+      tqe_ = now_;                                                                     \
+    }                                                                                  \
+  } while (0)
+#else
+#define QENV_INIT() do {} while (0)
+#define QENV(k) do {} while (0)
+#endif
+
 __device__ __forceinline__ int uf_load(int* a, int i) {
   return __hip_atomic_load(a + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -833,11 +850,13 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
   const int n = gi.n, e0 = gi.e[0], et = e0 + gi.e[1];
   (void)et;  // bounds checks only
   int* ia = (int*)area;
+  QENV_INIT();
   const EnvView<GL> E = env_view<GL>(p, gi, ia);
   if constexpr (!GL) {
     if (!staged) env_stage_lds(E, n);
     __syncthreads();
   }
+  QENV(0);
   // a speculative workgroup may already have run this step's fixed point for the chosen node
   // (single-node steps picked by the device or the host; results are tagged with the launch,
   // the removals so far and the node)
@@ -953,6 +972,7 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
     }
   }
   MD_PROF_A(2);
+  QENV(1);
   float* q = p.q + gi.node_off;
   int* gdeg0 = p.deg[0] + gi.node_off;
   int* gdeg1 = p.deg[1] + gi.node_off;
@@ -968,6 +988,7 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
   const int tot = ag.nlive, dm0 = ag.dm0, dm1 = ag.dm1, sd0 = ag.sd0, sd1 = ag.sd1, bad = ag.bad;
   const long long th0 = ag.th0, th1 = ag.th1;
   MD_PROF_A(34);
+  QENV(2);
   if (bad && !err) err = ERR_LIVE_MISMATCH;
   const int hd0 = gv.hdmax[0], hd1 = gv.hdmax[1];
   __syncthreads();
@@ -996,6 +1017,7 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
     if (threadIdx.x == 0) E.hdr[1] = 0;
   }
   MD_PROF_A(14);
+  QENV(3);
   if (p.n_spec > 0 && !err && gv.alive[0] > 0 && gv.alive[1] > 0 && ((const volatile int*)(lds_base + L_MISC))[5]) {
     // the state after this step is in HBM once every store has drained: ask the speculative
     // workgroups for the next step's fixed point of the likely next removals (before the
@@ -1065,5 +1087,6 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
   }
   __syncthreads();
   MD_PROF_A(15);
+  QENV(4);
   return err;
 }

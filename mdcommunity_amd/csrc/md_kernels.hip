@@ -2305,7 +2305,13 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
     const int it = (int)((item >> 3) & 3u), gl = (int)((item >> 5) & 1023u), j = q_item_j(item);
     const int g = p.glist[gl];
     if (kind == QK_ENV) {
+#ifdef MD_QPROF
+      const unsigned long long tqa = wall_clock64();
+#endif
       const bool lds_env = phase_a(p, g, it != 0, lds, false);
+#ifdef MD_QPROF
+      if (qp != nullptr && (p.variant & 8) && threadIdx.x == 0) atomicAdd(qp + 85, wall_clock64() - tqa);
+#endif
       pre = q_peek(p, tk);
       wdirty = true;
       const GraphVar& gv = *(const GraphVar*)(lds + L_GV);
@@ -2326,7 +2332,13 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
         const int tpi = bc[5];
         const int nt = (nl + TILE - 1) / TILE, ni = (nt + tpi - 1) / tpi;
         // this step's neighbour lists for the iteration-1 tiles (MD_VARIANT bit 12: off)
+#ifdef MD_QPROF
+        const unsigned long long tqb = wall_clock64();
+#endif
         const bool built = lds_env && !(p.variant & (4096 | 16)) && env_build_lists(p, p.ginfo[g], gl);
+#ifdef MD_QPROF
+        if (qp != nullptr && (p.variant & 8) && threadIdx.x == 0) atomicAdd(qp + 86, wall_clock64() - tqb);
+#endif
         if (threadIdx.x == 0) {
           stc(p.qg + 2 * gl + 1, ni | (nt << 16) | (tpi << 28));
           stc(p.qg + 2 * G_CAP + gl, built ? 1 : 0);

@@ -50,6 +50,9 @@ if len(P) and P[0, 0] == 1 and P[0, 9] > 0:
             row = P[0, 20 + 8 * it: 27 + 8 * it] / 1e5
             cnt = max(1, {0: 1, 1: 1, 2: 1}[it])
             print("  TILE it%d pieces (WG-ms): " % (it + 1) + "  ".join("%s %.1f" % (nm, v) for nm, v in zip(names_t, row)))
+        env_n = ["stage", "fixed point", "features", "write-back", "h0 table"]
+        print("  ENV pieces (WG-ms): " + "  ".join("%s %.1f" % (nm, v) for nm, v in zip(env_n, P[0, 80:85] / 1e5)) +
+              " | phase A total %.1f  neighbour lists %.1f" % (P[0, 85] / 1e5, P[0, 86] / 1e5))
         sys.exit(0)
     wb = P[0, 20:64] / 1e5
     nb_ = int(np.max(np.nonzero(wb)[0])) + 1 if np.any(wb) else 0
