@@ -105,6 +105,7 @@ struct md_ctx {
   DevBuf<int> rowptr[2], adj[2], epos[2], eu[2], ev[2];
   DevBuf<uint8_t> estate[2], calive[2], covered;
   DevBuf<int> deg[2], live, gscr, pend, tr_action, tr_rank, tr_stat, glist, ctl;
+  DevBuf<long long> tpart;  // grid-wide environment step: per-workgroup partials [2][TEAM_MAX_WG][16]
   DevBuf<float> H[2][2], h0tab[2], q, spart, apart, ybuf, hbuf, tr_q, node_w;
   DevBuf<unsigned long long> xbuf;
   DevBuf<int> nbc;  // neighbour-list cache slots (tiles of the largest launch)
@@ -153,7 +154,7 @@ struct md_ctx {
       H[l][0].release(); H[l][1].release();
     }
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
-    tr_stat.release(); glist.release(); ctl.release(); q.release(); spart.release();
+    tr_stat.release(); glist.release(); ctl.release(); tpart.release(); q.release(); spart.release();
     apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); nbc.release(); qslot.release(); qg.release(); tr_q.release(); node_w.release();
     sres.release(); qspec.release(); bars.release();
     h_req.release(); h_ans.release(); h_nact.release(); h_act.release(); h_q.release(); h_chk.release();
@@ -183,7 +184,7 @@ md_status fail(md_ctx* c, md_status s, const char* fmt, ...) {
   } while (0)
 
 // Control block layout (ints): [0] barrier counter, [1] error word (zeroed before each launch).
-constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_Q = 2, CTL_SPEC = 8, CTL_WORDS = 12;
+constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_Q = 2, CTL_SPEC = 8, CTL_TEAM = 12, CTL_WORDS = 16;
 constexpr int SPEC_MAX = 32;  // speculative workgroups per launch at most  // CTL_SPEC: u64 request word
 
 Params make_params(md_ctx* c) {
@@ -208,6 +209,8 @@ Params make_params(md_ctx* c) {
   p.live = c->live.p;
   p.q = c->q.p;
   p.gscr = c->gscr.p;
+  p.tpart = c->tpart.p;
+  p.tctl = c->ctl.p + CTL_TEAM;
   p.spart = c->spart.p;
   p.apart = c->apart.p;
   p.ybuf = c->ybuf.p;
@@ -435,7 +438,12 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
   const int n_env = env_workgroups(c, v);
   // batches of whole rollouts run through the device work queue (MD_VARIANT bit 32: the
   // lock-step shared mode instead), one workgroup per CU
-  const bool qmode = run_mode == RUN_ROLLOUT && n_env == 0 && !(c->variant & 32);
+  // (one graph too large for LDS: the lock-step kernel, whose environment step runs on every
+  // workgroup of the launch -- team_env_step -- unless MD_VARIANT bit 2 turns that off)
+  const bool team_env = ngl == 1 && !(c->variant & 2) &&
+                        (!phase_a_fits_lds_host(c->hinfo[gl[0]].n, c->hinfo[gl[0]].e[0] + c->hinfo[gl[0]].e[1]) ||
+                         (c->variant & 64));
+  const bool qmode = run_mode == RUN_ROLLOUT && n_env == 0 && !(c->variant & 32) && !team_env;
   const int grid = qmode ? c->cus : grid_size(c, v, n_env);
   // speculative environment workgroups on the CUs a single-graph rollout leaves free
   // (single-node steps only: step > 1 takes several removals per prediction)
@@ -801,7 +809,7 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   }
   HIPCHK(c, c->covered.alloc(tn + 4));
   HIPCHK(c, c->live.alloc(4 * tn));  // {node, CSR begin l0, l1, extents} per live position
-  HIPCHK(c, c->gscr.alloc(4 * tn));  // global-mode environment scratch (16 B per node; always, so MD_VARIANT=64 can force that mode)
+  HIPCHK(c, c->gscr.alloc(5 * tn));  // global-mode environment scratch (20 B per node; always, so MD_VARIANT=64 can force that mode)
   HIPCHK(c, c->pend.alloc(tn));
   HIPCHK(c, c->tr_action.alloc(tn));
   HIPCHK(c, c->tr_rank.alloc(tn));
@@ -810,6 +818,7 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->q.alloc(tn));
   HIPCHK(c, c->glist.alloc(n_graphs));
   HIPCHK(c, c->ctl.alloc(CTL_WORDS));
+  if (c->tpart.p == nullptr) HIPCHK(c, c->tpart.alloc(2 * (size_t)TEAM_MAX_WG * 16));
   HIPCHK(c, c->bars.alloc(8 * 64));
   HIPCHK(c, c->spart.alloc(tt * 384));
   HIPCHK(c, c->apart.alloc(tt * 4));

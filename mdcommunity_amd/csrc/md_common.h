@@ -22,6 +22,7 @@ constexpr int NB_CAP_ENTRIES = 2052;   // alive neighbour entries per layer kept
 constexpr int NBC_HDR = 80, NBC_LWORDS = NB_CAP_ENTRIES / 2, NBC_INTS = 2176;
 static_assert(NBC_HDR + 2 * NBC_LWORDS <= NBC_INTS, "cache slot");
 constexpr int XB_SLOTS = 256;
+constexpr int TEAM_MAX_WG = 1024;  // workgroups of a launch the grid-wide environment step supports
 constexpr int Q_CAP = 1 << 18;   // queue-mode ring slots (items in flight << Q_CAP)
 
 // Offsets (floats) of each tensor in the packed weight blob (see include/mdroll.h).
@@ -96,7 +97,9 @@ struct Params {
   float* H[2][2];                  // [layer][buffer] node embeddings, node-major x 64
   float* h0tab[2];                 // [layer] first-layer embedding: by degree (unit) / by node (degree cost)
   float* q;                        // per node (-inf = masked)
-  int* gscr;                       // phase-A scratch in global memory for graphs too big for LDS: 4 per node
+  int* gscr;                       // phase-A scratch in global memory for graphs too big for LDS: 5 per node
+  long long* tpart;                // grid-wide environment step: per-workgroup partials [2][TEAM_MAX_WG][16]
+  int* tctl;                       // grid-wide environment step: {actions (-1: none), first action}
   float* spart;                    // per tile: [3 sums][2 layers][64] virtual-node partial sums
   float* apart;                    // per tile: arg-max partial {max, second, idx, count}
   float* ybuf;                     // per graph: [2][64] virtual-node embedding after iteration 2

@@ -691,7 +691,7 @@ __device__ __forceinline__ EnvView<GL> env_view(KParams& p, const GraphInfo& gi,
   }
   E.gcov = p.covered + gi.node_off;
   if constexpr (GL) {
-    int* gs = p.gscr + 4 * (size_t)gi.node_off;
+    int* gs = p.gscr + 5 * (size_t)gi.node_off;  // par0, par1, deg0, deg1, LMCC counts (team step)
     E.par0 = gs;
     E.par1 = gs + n;
     E.deg0 = gs + 2 * n;
@@ -839,6 +839,63 @@ __device__ __forceinline__ int env_apply_spec(const EnvView<false>& E, const int
 // the unit-cost first-layer table.  Returns 0 or an ERR_* code.
 // Not inlined: the environment step has its own register allocation (inlined, it raised the
 // register pressure of the whole rollout loop -- spills in the tile phases).
+// First-layer embedding by degree (unit cost): X = [d/dmax, d/dmax] (net :252-261),
+// normalize(relu(X . w_n2l)) with the 2-term FMA chain of MKL's sgemm; one thread per row
+// d = 1..dmax (the row recomputed for the norm pass and the store pass; w_n2l arrives as
+// scalar loads), the norm in torch's order (wave_norm64's).  The table depends on dmax
+// only, so it is rebuilt only when dmax changed (hd0, hd1: the dmax of the current tables).
+__device__ __forceinline__ void h0_update(KParams& p, const GraphInfo& gi, GraphVar& gv, int dm0, int dm1, int hd0, int hd1) {
+  if (p.node_w == nullptr) {
+    const float* wn = p.w + W_N2L;
+    for (int l = 0; l < 2; ++l) {
+      const int dm = l ? dm1 : dm0;
+      if (dm == (l ? hd1 : hd0)) continue;
+      float* tab = p.h0tab[l] + (size_t)gi.node_off * EMB;  // degrees <= n-1 fit the graph's rows
+      if (dm <= p.h0g_dm) {
+        // the table of this dmax is precomputed (md_h0_kernel at load): a 16-byte copy
+        const float* src = p.h0g + h0g_row(dm, 1) * EMB;
+        const int nq = 16 * dm;
+        for (int i0 = threadIdx.x; i0 < nq; i0 += 4 * NTHREADS) {
+          float4 x[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (i0 + k * NTHREADS < nq) x[k] = ldc4(src, (i0 + k * NTHREADS) * 16);
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (i0 + k * NTHREADS < nq) stc4(tab, EMB * 4 + (i0 + k * NTHREADS) * 16, x[k]);
+        }
+        continue;
+      }
+      for (int d = 1 + (int)threadIdx.x; d <= dm; d += NTHREADS) {
+        const float f = (float)d / (float)dm;
+        float acc[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+        for (int c = 0; c < 64; ++c) {
+          const float x = fmaxf(fmaf(f, wn[64 + c], fmaf(f, wn[c], 0.f)), 0.f);
+          acc[c & 7] = fmaf(x, x, acc[c & 7]);
+        }
+        const float den = fmaxf(sqrtf(sumsq8_finish(acc)), 1e-12f);
+#pragma unroll
+        for (int c4 = 0; c4 < 16; ++c4) {
+          float o[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int c = 4 * c4 + k;
+            o[k] = fmaxf(fmaf(f, wn[64 + c], fmaf(f, wn[c], 0.f)), 0.f) / den;
+          }
+          stc4(tab, d * 256 + c4 * 16, make_float4(o[0], o[1], o[2], o[3]));
+        }
+      }
+    }
+    if (threadIdx.x == 0) {
+      gv.hdmax[0] = dm0;
+      gv.hdmax[1] = dm1;
+    }
+  }
+}
+
 template <bool GL>
 __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, float*, int pend_n,
                         int pend_first, const float*, bool staged) {
@@ -1031,62 +1088,374 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
       if (p.prof != nullptr && ps < p.prof_cap) p.prof[(size_t)ps * PROF_SLOTS + 64] = wall_clock64();
     }
   }
-  // First-layer embedding by degree (unit cost): X = [d/dmax, d/dmax] (net :252-261),
-  // normalize(relu(X . w_n2l)) with the 2-term FMA chain of MKL's sgemm; one thread per row
-  // d = 1..dmax (the row recomputed for the norm pass and the store pass; w_n2l arrives as
-  // scalar loads), the norm in torch's order (wave_norm64's).  The table depends on dmax
-  // only, so it is rebuilt only when dmax changed.
-  if (p.node_w == nullptr) {
-    const float* wn = p.w + W_N2L;
-    for (int l = 0; l < 2; ++l) {
-      const int dm = l ? dm1 : dm0;
-      if (dm == (l ? hd1 : hd0)) continue;
-      float* tab = p.h0tab[l] + (size_t)gi.node_off * EMB;  // degrees <= n-1 fit the graph's rows
-      if (dm <= p.h0g_dm) {
-        // the table of this dmax is precomputed (md_h0_kernel at load): a 16-byte copy
-        const float* src = p.h0g + h0g_row(dm, 1) * EMB;
-        const int nq = 16 * dm;
-        for (int i0 = threadIdx.x; i0 < nq; i0 += 4 * NTHREADS) {
-          float4 x[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if (i0 + k * NTHREADS < nq) x[k] = ldc4(src, (i0 + k * NTHREADS) * 16);
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if (i0 + k * NTHREADS < nq) stc4(tab, EMB * 4 + (i0 + k * NTHREADS) * 16, x[k]);
-        }
-        continue;
-      }
-      for (int d = 1 + (int)threadIdx.x; d <= dm; d += NTHREADS) {
-        const float f = (float)d / (float)dm;
-        float acc[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-#pragma unroll
-        for (int c = 0; c < 64; ++c) {
-          const float x = fmaxf(fmaf(f, wn[64 + c], fmaf(f, wn[c], 0.f)), 0.f);
-          acc[c & 7] = fmaf(x, x, acc[c & 7]);
-        }
-        const float den = fmaxf(sqrtf(sumsq8_finish(acc)), 1e-12f);
-#pragma unroll
-        for (int c4 = 0; c4 < 16; ++c4) {
-          float o[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int c = 4 * c4 + k;
-            o[k] = fmaxf(fmaf(f, wn[64 + c], fmaf(f, wn[c], 0.f)), 0.f) / den;
-          }
-          stc4(tab, d * 256 + c4 * 16, make_float4(o[0], o[1], o[2], o[3]));
-        }
-      }
-    }
-    if (threadIdx.x == 0) {
-      gv.hdmax[0] = dm0;
-      gv.hdmax[1] = dm1;
-    }
-  }
+  h0_update(p, gi, gv, dm0, dm1, hd0, hd1);
   __syncthreads();
   MD_PROF_A(15);
   QENV(4);
   return err;
+}
+
+// ------------------------------------------------------------------ grid-wide environment step
+// A graph too large for one workgroup's LDS (global mode: testReal sizes, N ~ 10^4 - 10^5)
+// running alone in a launch: instead of one workgroup scanning every edge of the graph in HBM
+// while the others wait at the barrier, every workgroup of the launch takes part -- edges and
+// nodes grid-strided, the union-find forests in HBM with agent-scope atomics, a grid barrier
+// between passes.  The passes are the one-workgroup code's (mcc_fixed_point, env_features):
+// the same Jacobi rounds reach the same unique fixed point and pruned-edge set, the same LMCC
+// count, degrees, ascending live list and aggregates.  Cross-workgroup sums go through
+// per-workgroup partials (two alternating slots: a slot is rewritten two reductions later, after
+// every workgroup has passed the barrier that follows its reads).
+struct Team {
+  int gt, gs;      // this thread's index in the grid, grid stride (threads)
+  int use;         // reductions so far (partial slot = use & 1)
+  unsigned* target;
+  int* flag;
+  int* tmp;        // LDS, >= 8 * 16 + 16 words
+  unsigned long long* acc;  // diagnostics (md_profile): per-step piece ticks of workgroup 0, else null
+  unsigned long long t;
+};
+// Team-step piece profile (md_profile, workgroup 0): slots 80.. of the step's record:
+// 80 rounds, 81 union passes, 82 label passes + reduction, 83 prune passes + reduction,
+// 84 LMCC count, 85 features, 86 fixed-point inits
+#define TEAM_ACC(T, k)                                                    \
+  do {                                                                    \
+    if ((T).acc != nullptr && threadIdx.x == 0) {                         \
+      const unsigned long long now_ = wall_clock64();                     \
+      (T).acc[k] += now_ - (T).t;                                         \
+      (T).t = now_;                                                       \
+    }                                                                     \
+  } while (0)
+
+// arr[idx] += 1 for every lane with `on`; lanes of the wave that share an index (the first two
+// distinct indices) are combined into one atomic -- a hub's edges and a giant component's
+// nodes would otherwise serialise thousands of atomics on one word.  Every lane of the wave
+// calls it (wave-uniform loops).
+template <class P>
+__device__ __forceinline__ void agg_add1(P arr, int idx, bool on) {
+  unsigned long long m = __ballot(on);
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    if (m == 0ull) break;
+    const int leader = __ffsll((long long)m) - 1;
+    const int key = __shfl(idx, leader, 64);
+    const unsigned long long same = __ballot(on && idx == key);
+    if (lane_id() == leader) uf_add(arr, key, (int)__popcll(same));
+    if (idx == key) on = false;
+    m &= ~same;
+  }
+  if (on) uf_add(arr, idx, 1);
+}
+
+// Reduces K 64-bit values over the grid (bit k of maxmask: max, else sum; every value >= 0 for
+// a max) into tot[k]; `before`, when given, receives the sum of value 0 over the lower
+// workgroups (the base of an ascending scan).  Returns true on a grid error.
+template <int K>
+__device__ bool team_reduce(KParams& p, Team& T, const long long (&v)[K], unsigned maxmask, long long (&tot)[K],
+                            long long* before) {
+  static_assert(K <= 16, "16 partials per workgroup");
+  const int lane = lane_id(), w = wave_id();
+  long long r[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    r[k] = v[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const long long y = __shfl_xor(r[k], o, 64);
+      r[k] = (maxmask >> k & 1u) ? (r[k] > y ? r[k] : y) : r[k] + y;
+    }
+  }
+  long long* lt = (long long*)T.tmp;  // [8 waves][K], then [K + 1] totals
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) lt[w * K + k] = r[k];
+  }
+  __syncthreads();
+  const int slot = T.use & 1;
+  if (threadIdx.x < K) {
+    const int k = threadIdx.x;
+    long long a = 0;
+    for (int i = 0; i < NTHREADS / 64; ++i) {
+      const long long y = lt[i * K + k];
+      a = (maxmask >> k & 1u) ? (a > y ? a : y) : a + y;
+    }
+    __hip_atomic_store((g_u64*)(p.tpart + ((size_t)slot * TEAM_MAX_WG + blockIdx.x) * 16 + k), (unsigned long long)a,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  T.use++;
+  if (grid_sync(p, *T.target, T.flag)) return true;
+  if (w == 0) {
+    long long a[K];
+    long long pre = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] = 0;
+    for (int b = lane; b < p.n_main; b += 64) {
+      const g_u64* src = (const g_u64*)(p.tpart + ((size_t)slot * TEAM_MAX_WG + b) * 16);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const long long y = (long long)__hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a[k] = (maxmask >> k & 1u) ? (a[k] > y ? a[k] : y) : a[k] + y;
+        if (k == 0 && b < (int)blockIdx.x) pre += y;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const long long y = __shfl_xor(a[k], o, 64);
+        a[k] = (maxmask >> k & 1u) ? (a[k] > y ? a[k] : y) : a[k] + y;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) lt[8 * 16 + k] = a[k];
+      lt[8 * 16 + K] = pre;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) tot[k] = lt[8 * 16 + k];
+  if (before != nullptr) *before = lt[8 * 16 + K];
+  __syncthreads();
+  return false;
+}
+
+// Mutual-LMCC fixed point of mcc_fixed_point on the whole grid (cover >= 0: cover that node in
+// the first union pass; its covered edge counts per layer in cc).  LMCC size in lm, pruned edge
+// counts in pr.  Labels (component roots) end in E.deg0 / E.deg1 as there.
+__device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, int* cnt, int cover, bool set_cover, int& lm,
+                                 int* pr, int* cc) {
+  const int n = E.gi->n, et = E.et, e0 = E.e0;
+  if (T.acc != nullptr && threadIdx.x == 0) T.t = wall_clock64();
+  for (int x = T.gt; x < n; x += T.gs) {
+    uf_store(E.par0, x, x);
+    uf_store(E.par1, x, x);
+  }
+  if (grid_sync(p, *T.target, T.flag)) return true;
+  TEAM_ACC(T, 6);
+  if (set_cover && cover >= 0 && threadIdx.x == 0) stc(E.gcov + cover, (uint8_t)1);  // read by the count pass
+  bool first = true;
+  pr[0] = pr[1] = 0;
+  while (true) {
+    long long k0 = 0, k1 = 0;
+    for (int e = T.gt; e < et; e += T.gs) {
+      if (E.state(e) != E_ALIVE) continue;
+      const int u = E.u(e), v = E.v(e);
+      if (first && cover >= 0 && (u == cover || v == cover)) {
+        E.kill(e, E_COVERED);
+        if (e < e0) k0++; else k1++;
+      } else {
+        uf_unite(e < e0 ? E.par0 : E.par1, u, v);
+      }
+    }
+    if (first)  // LMCC counters, used after the last round
+      for (int x = T.gt; x < n; x += T.gs) uf_store(cnt, x, 0);
+    if (grid_sync(p, *T.target, T.flag)) return true;
+    TEAM_ACC(T, 1);
+    if (T.acc != nullptr && threadIdx.x == 0) T.acc[0] += 1;
+    long long diff = 0;
+    for (int x = T.gt; x < n; x += T.gs) {
+      const int r0 = uf_find(E.par0, x), r1 = uf_find(E.par1, x);
+      uf_store(E.deg0, x, r0);
+      uf_store(E.deg1, x, r1);
+      diff += r0 != r1;
+    }
+    const long long v3[3] = {diff, k0, k1};
+    long long t3[3];
+    if (team_reduce<3>(p, T, v3, 0u, t3, nullptr)) return true;
+    TEAM_ACC(T, 2);
+    if (first && cover >= 0) {
+      cc[0] = (int)t3[1];
+      cc[1] = (int)t3[2];
+    }
+    first = false;
+    if (t3[0] == 0) break;
+    // prune every alive edge whose endpoints the other layer separates; the next round's forests
+    // start over (the parents are not read by this pass)
+    long long c0 = 0, c1 = 0;
+    for (int e = T.gt; e < et; e += T.gs) {
+      if (E.state(e) != E_ALIVE) continue;
+      const int u = E.u(e), v = E.v(e);
+      auto other = e < e0 ? E.deg1 : E.deg0;
+      if (uf_load(other, u) != uf_load(other, v)) {
+        E.kill(e, E_PRUNED);
+        if (e < e0) c0++; else c1++;
+      }
+    }
+    for (int x = T.gt; x < n; x += T.gs) {
+      uf_store(E.par0, x, x);
+      uf_store(E.par1, x, x);
+    }
+    const long long v2[2] = {c0, c1};
+    long long t2[2];
+    if (team_reduce<2>(p, T, v2, 0u, t2, nullptr)) return true;
+    TEAM_ACC(T, 3);
+    pr[0] += (int)t2[0];
+    pr[1] += (int)t2[1];
+  }
+  // the LMCC: non-covered nodes per component (layer-0 label = layer-1 label at the fixed point)
+  for (int xb = T.gt - lane_id(); xb < n; xb += T.gs) {
+    const int x = xb + lane_id();
+    const bool on = x < n && !E.covered(x);
+    agg_add1(cnt, on ? uf_load(E.deg0, x) : 0, on);
+  }
+  if (grid_sync(p, *T.target, T.flag)) return true;
+  long long best = 0;
+  for (int x = T.gt; x < n; x += T.gs) best = max(best, (long long)uf_load(cnt, x));
+  const long long vb[1] = {best};
+  long long tb[1];
+  if (team_reduce<1>(p, T, vb, 1u, tb, nullptr)) return true;
+  TEAM_ACC(T, 4);
+  lm = (int)tb[0];
+  return false;
+}
+
+// env_features on the whole grid: residual degrees by edge-parallel atomics, then per workgroup a
+// contiguous node range (workgroup order = ascending ids) for the live list, its base from the
+// live counts of the lower workgroups.
+__device__ bool team_features(KParams& p, Team& T, const EnvView<true>& E, int n, int* gdeg0, int* gdeg1, float* lv,
+                              float* q, EnvAgg& ag) {
+  const int e0 = E.e0;
+  if (T.acc != nullptr && threadIdx.x == 0) T.t = wall_clock64();
+  for (int x = T.gt; x < n; x += T.gs) {
+    uf_store(E.par0, x, 0);
+    uf_store(E.par1, x, 0);
+  }
+  if (grid_sync(p, *T.target, T.flag)) return true;
+  // (par1 follows par0: one index space l * n + node for the combined atomics)
+  for (int eb = T.gt - lane_id(); eb < E.et; eb += T.gs) {
+    const int e = eb + lane_id();
+    const bool on = e < E.et && E.state(e) == E_ALIVE;
+    const int base = e < e0 ? 0 : n;
+    agg_add1(E.par0, on ? base + E.u(e) : 0, on);
+    agg_add1(E.par0, on ? base + E.v(e) : 0, on);
+  }
+  if (grid_sync(p, *T.target, T.flag)) return true;
+  const int cw = (n + p.n_main - 1) / p.n_main;
+  const int w0 = min(n, (int)blockIdx.x * cw), w1 = min(n, w0 + cw);
+  const int ct = (w1 - w0 + NTHREADS - 1) / NTHREADS;
+  const int x0 = min(w1, w0 + (int)threadIdx.x * ct), x1 = min(w1, x0 + ct);
+  long long nlive = 0, dm0 = 0, dm1 = 0, sd0 = 0, sd1 = 0, bad = 0, th0 = 0, th1 = 0;
+  for (int x = x0; x < x1; ++x) {
+    const int d0 = uf_load(E.par0, x), d1 = uf_load(E.par1, x);
+    stc(gdeg0 + x, d0);
+    stc(gdeg1 + x, d1);
+    stc(q + x, NEG_INF);
+    bad |= ((d0 > 0) != (d1 > 0));
+    if (d0 > 0) {
+      nlive++;
+      dm0 = max(dm0, (long long)d0);
+      dm1 = max(dm1, (long long)d1);
+      th0 += (long long)d0 * (d0 - 1) / 2;
+      th1 += (long long)d1 * (d1 - 1) / 2;
+    }
+    sd0 += d0;
+    sd1 += d1;
+  }
+  int wtot = 0;
+  const int off = block_excl_scan((int)nlive, T.tmp, &wtot);
+  const long long v8[8] = {nlive, sd0, sd1, bad, th0, th1, dm0, dm1};
+  long long t8[8], before = 0;
+  if (team_reduce<8>(p, T, v8, 0xc0u, t8, &before)) return true;
+  int k = (int)before + off;
+  for (int x = x0; x < x1; ++x) {
+    if (uf_load(E.par0, x) > 0) {
+      const int b0 = E.grp[0][x], b1 = E.grp[1][x];
+      const int x0e = E.grp[0][x + 1], x1e = E.grp[1][x + 1];
+      if (MD_BOK(k < n, 9))
+        stc4(lv, k * 16, make_float4(__int_as_float(x), __int_as_float(b0), __int_as_float(b1),
+                                     __int_as_float((x0e - b0) | ((x1e - b1) << 16))));
+      ++k;
+    }
+  }
+  TEAM_ACC(T, 5);
+  ag.nlive = (int)t8[0];
+  ag.sd0 = (int)t8[1];
+  ag.sd1 = (int)t8[2];
+  ag.bad = t8[3] != 0;
+  ag.th0 = t8[4];
+  ag.th1 = t8[5];
+  ag.dm0 = (int)t8[6];
+  ag.dm1 = (int)t8[7];
+  return false;
+}
+
+// The environment step of graph g on every workgroup of the launch (env_step's work once the
+// actions are known): workgroup 0 holds the graph's GraphVar in LDS and keeps its books (the
+// others read the counts they need from the partials); pend_n actions, the first pend_first
+// (or p.pend[0] when < 0).  Returns an ERR_* code (0: ok) in *err; true on a grid error.
+__device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_first, int* err) {
+  const GraphInfo gi = p.ginfo[g];
+  const int n = gi.n;
+  GraphVar& gv = *(GraphVar*)(lds_base() + L_GV);
+  const bool books = blockIdx.x == 0;
+  const EnvView<true> E = env_view<true>(p, gi, (int*)(lds_base() + L_SCR));
+  int* cnt = p.gscr + 5 * (size_t)gi.node_off + 4 * n;
+  // every workgroup follows the same control flow: alive counts and s0 from the graph's
+  // GraphVar as the last phase A stored it
+  int alive0 = ldc(&p.gvar[g].alive[0]), alive1 = ldc(&p.gvar[g].alive[1]);
+  const int s0_done = ldc(&p.gvar[g].s0_done);
+  *err = 0;
+  for (int k = 0; k < pend_n; ++k) {
+    if (alive0 == 0 || alive1 == 0) break;  // terminal between queued actions
+    const int a = k == 0 && pend_first >= 0 ? pend_first
+                                            : __hip_atomic_load(p.pend + gi.node_off + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a < 0 || a >= n) { *err = ERR_BADNODE; break; }
+    if (E.covered(a)) { *err = ERR_COVERED; break; }
+    int pr[2], c[2], lm = 0;
+    // (workgroup 0 sets covered(a) after the fixed point's first barrier: every workgroup has
+    // read it by then)
+    if (team_fixed_point(p, T, E, cnt, a, books, lm, pr, c)) return true;
+    alive0 -= c[0] + pr[0];
+    alive1 -= c[1] + pr[1];
+    if (books && threadIdx.x == 0) {
+      gv.counter[0] += c[0];
+      gv.counter[1] += c[1];
+      gv.removed[0] += pr[0];
+      gv.removed[1] += pr[1];
+      gv.alive[0] -= c[0] + pr[0];
+      gv.alive[1] -= c[1] + pr[1];
+      gv.n_cov += 1;
+      gv.lmcc = lm;
+      if (MD_BOK(gv.steps < gi.n, 8)) {
+        p.tr_action[gi.node_off + gv.steps] = a;
+        p.tr_rank[gi.node_off + gv.steps] = lm;
+      }
+      gv.steps += 1;
+    }
+  }
+  if (!s0_done && *err == 0) {
+    int pr[2], lm = 0;
+    if (team_fixed_point(p, T, E, cnt, -1, false, lm, pr, nullptr)) return true;
+    if (books && threadIdx.x == 0) {
+      gv.removed[0] += pr[0];
+      gv.removed[1] += pr[1];
+      gv.max_rank = lm;
+      gv.lmcc = lm;
+      gv.s0_done = 1;
+    }
+  }
+  EnvAgg ag;
+  if (team_features(p, T, E, n, p.deg[0] + gi.node_off, p.deg[1] + gi.node_off, (float*)(p.live + 4 * (size_t)gi.node_off),
+                    p.q + gi.node_off, ag))
+    return true;
+  if (books) {
+    if (ag.bad && *err == 0) *err = ERR_LIVE_MISMATCH;
+    const int hd0 = gv.hdmax[0], hd1 = gv.hdmax[1];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      gv.n_live = ag.nlive;
+      gv.dmax[0] = ag.dm0;
+      gv.dmax[1] = ag.dm1;
+      gv.alive[0] = ag.sd0 / 2;
+      gv.alive[1] = ag.sd1 / 2;
+      gv.twohop[0] = ag.th0;
+      gv.twohop[1] = ag.th1;
+    }
+    h0_update(p, gi, gv, ag.dm0, ag.dm1, hd0, hd1);
+    __syncthreads();
+  }
+  return false;
 }

@@ -502,7 +502,10 @@ __device__ __noinline__ int host_handshake(KParams&, const GraphInfo gi, int g, 
 }
 
 // Phase A of one graph: reduce the previous prediction, then apply / MCC / features.
-__device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds, bool staged) {
+// team_out (grid-wide environment step): when the step would run in global mode, phase A stops
+// once the actions are known: {pend_n, pend_first, 1} in team_out, the GraphVar left in LDS for
+// the caller to finish (team_env_step); team_out[2] = 0 otherwise.
+__device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds, bool staged, int* team_out = nullptr) {
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   GraphVar& gv = *(GraphVar*)(lds + L_GV);
   int* misc = (int*)(lds + L_MISC);
@@ -510,7 +513,10 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
   // a dedicated environment workgroup that already stepped this graph in this launch holds
   // its current GraphVar in LDS (nobody else writes it during a launch)
   if (!(staged && p.n_env > 0)) gv_load(p, g, &gv);
-  if (threadIdx.x == 0) misc[5] = 0;
+  if (threadIdx.x == 0) {
+    misc[5] = 0;
+    if (team_out != nullptr) team_out[2] = 0;
+  }
   __syncthreads();
   int pend_n = 0, pend_first = -1;
   bool stop = false;
@@ -615,6 +621,15 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
   if (!stop) {
     const int et = gi.e[0] + gi.e[1];
     const bool fits = phase_a_fits_lds(gi.n, et) && !(p.variant & 64);  // 64: force global mode (tests)
+    if (team_out != nullptr && !fits) {
+      if (threadIdx.x == 0) {
+        team_out[0] = pend_n;
+        team_out[1] = pend_first;
+        team_out[2] = 1;
+      }
+      __syncthreads();
+      return staged;
+    }
     float* area = lds + L_W;
     const bool was_staged = staged && fits;
     staged = fits;
@@ -2650,6 +2665,11 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
     return;
   }
   const bool ded = p.n_env > 0;
+  // grid-wide environment step: one graph too large for LDS (global mode) in shared mode
+  // (MD_VARIANT bit 2: off, the one-workgroup step)
+  const bool team = !ded && p.nglist == 1 && p.tctl != nullptr && !(p.variant & 2) && p.n_main <= TEAM_MAX_WG &&
+                    (!phase_a_fits_lds(p.ginfo[p.glist[0]].n, p.ginfo[p.glist[0]].e[0] + p.ginfo[p.glist[0]].e[1]) ||
+                     (p.variant & 64));
   const bool is_env = ded && (int)blockIdx.x < p.n_env;
   const bool is_head = ded && !is_env && (int)blockIdx.x < 2 * p.n_env;
   const int twg0 = ded ? 2 * p.n_env : 0;
@@ -2682,6 +2702,56 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
     __syncthreads();
     if (ded) {
       if (is_env) staged = phase_a(p, p.glist[blockIdx.x], have_q, lds, staged);
+    } else if (team) {
+      // one global-mode graph: workgroup 0 decides the actions, then every workgroup runs the
+      // environment step (team_env_step) and workgroup 0 finishes phase A
+      int* tq = (int*)(lds + L_MISC) + 54;
+      if (blockIdx.x == 0) {
+        phase_a(p, p.glist[0], have_q, lds, false, tq);
+        if (threadIdx.x == 0) {
+          stc(p.tctl, tq[2] ? tq[0] : -1);
+          stc(p.tctl + 1, tq[1]);
+        }
+      }
+      if (grid_sync(p, target, bflag)) break;
+      if (threadIdx.x == 0) {
+        tq[0] = ldc(p.tctl);
+        tq[1] = ldc(p.tctl + 1);
+      }
+      __syncthreads();
+      const int pn = tq[0], pf = tq[1];
+      __syncthreads();
+      if (pn >= 0) {
+        Team T;
+        T.gt = (int)blockIdx.x * NTHREADS + (int)threadIdx.x;
+        T.gs = p.n_main * NTHREADS;
+        T.use = 0;
+        T.target = &target;
+        T.flag = bflag;
+        T.tmp = (int*)(scr + S_M);
+        T.acc = nullptr;
+        T.t = 0;
+        if (p.prof != nullptr && blockIdx.x == 0 && pstep < p.prof_cap) {
+          T.acc = p.prof + (size_t)pstep * PROF_SLOTS + 80;
+          if (threadIdx.x == 0) p.prof[(size_t)pstep * PROF_SLOTS + 87] = wall_clock64();
+        }
+        int terr = 0;
+        if (team_env_step(p, T, p.glist[0], pn, pf, &terr)) break;
+        if (T.acc != nullptr && threadIdx.x == 0) T.acc[7] = wall_clock64() - T.acc[7];  // slot 87: step total
+        if (blockIdx.x == 0) {
+          GraphVar& gv = *(GraphVar*)(lds + L_GV);
+          if (threadIdx.x == 0) {
+            gv.npend = 0;
+            if (terr) raise_err(p, terr);
+            if (gv.alive[0] == 0 || gv.alive[1] == 0) gv.status = ST_TERMINAL;
+            else if (p.run_mode == RUN_STEP) gv.status = ST_PAUSED;
+            else gv.status = ST_RUN;
+          }
+          __syncthreads();
+          gv_store(p, p.glist[0], &gv);
+          __syncthreads();
+        }
+      }
     } else {
       bool wdirty = false;
       for (int gi = blockIdx.x; gi < ng; gi += p.n_main) {

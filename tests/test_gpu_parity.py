@@ -346,3 +346,36 @@ def test_speculative_steps_match_plain(monkeypatch, name):
                 assert hits == 0
             else:
                 assert hits >= len(seq) // 2, (key, hits, len(seq))
+
+
+def test_grid_wide_environment_step(monkeypatch):
+    """One global-mode graph per launch runs its environment step on every workgroup
+    (team_env_step: grid-strided union-find in HBM, grid barriers between the passes).
+    MD_ENV_MODE=0 + MD_VARIANT=64 force it on small graphs; MD_VARIANT bit 2 restores the
+    one-workgroup step.  Both give the certified sequences and AUDC, the same Q at s0, the same
+    single-action steps (md_step) and the same multi-action rollouts (step > 1, host picks)."""
+    monkeypatch.setenv("MD_ENV_MODE", "0")
+    out = {}
+    for variant in ("64", "66"):
+        monkeypatch.setenv("MD_VARIANT", variant)
+        e = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
+        try:
+            for name in ("er100", "gmm200_s7", "er300_dense", "gmm1000_s0"):
+                z = load_golden(name)
+                n = int(z["n_nodes"])
+                e.load_graphs([(n, z["edges0"], z["edges1"])])
+                assert int(e.reset()[0]) == int(z["max_rank"]), (variant, name)
+                q, _, _, _ = e.predict()
+                seq, ranks = e.rollout()[0]
+                assert seq.tolist() == load_cert(name)["gpu_seq"].tolist(), (variant, name)
+                assert audc(ranks, int(z["max_rank"]), n) == float(z["score"]), (variant, name)
+                e.reset()
+                steps = [int(e.step(np.array([a], np.int32))[0][0]) for a in seq[:5].tolist()]
+                assert steps == ranks[:5].tolist(), (variant, name)
+                e.reset()
+                s3, r3 = e.rollout(step=3)[0]
+                out[(variant, name)] = (q.tobytes(), s3.tolist(), r3.tolist())
+        finally:
+            e.close()
+    for name in ("er100", "gmm200_s7", "er300_dense", "gmm1000_s0"):
+        assert out[("64", name)] == out[("66", name)], name
