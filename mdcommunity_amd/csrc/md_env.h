@@ -132,6 +132,36 @@ __device__ __forceinline__ void uf_unite2(P par, int a, int b) {
   }
 }
 
+// Union-find for the grid-wide step: roots linked by a random priority (a bijective hash of the
+// node id) instead of the id -- concurrent min-id linking of a large component builds deep
+// chains (one edge's union took ~30 us over HBM at N = 18000); random linking keeps the trees
+// shallow in expectation.  A component's root is its node of least priority: still one
+// canonical label per node set, so the layers' partitions compare root for root.
+__device__ __forceinline__ unsigned uf_pri(int x) { return (unsigned)x * 2654435761u; }
+template <class P>
+__device__ __forceinline__ int uf_find_h(P par, int v) {
+  int cur = uf_load(par, v);
+  if (cur != v) {
+    int prev = v, next;
+    while (cur != (next = uf_load(par, cur))) {
+      uf_store(par, prev, next);  // path halving; any ancestor is a valid parent
+      prev = cur;
+      cur = next;
+    }
+  }
+  return cur;
+}
+template <class P>
+__device__ __forceinline__ void uf_unite_h(P par, int a, int b) {
+  while (true) {
+    a = uf_find_h(par, a);
+    b = uf_find_h(par, b);
+    if (a == b) return;
+    if (uf_pri(a) > uf_pri(b)) { const int t = a; a = b; b = t; }
+    if (uf_cas(par, b, b, a) == b) return;
+  }
+}
+
 // ------------------------------------------------------------------ layout and view
 // LDS layout of a graph's environment (words from the start of the phase-A area): the edge
 // region first (u16 endpoints, state, state at the last write-back, covered flags) so a
@@ -1113,6 +1143,8 @@ struct Team {
   int* tmp;        // LDS, >= 8 * 16 + 16 words
   unsigned long long* acc;  // diagnostics (md_profile): per-step piece ticks of workgroup 0, else null
   unsigned long long t;
+  unsigned long long* prof_any;  // diagnostics: the step's record (every workgroup), else null
+  unsigned long long t0any;
 };
 // Team-step piece profile (md_profile, workgroup 0): slots 80.. of the step's record:
 // 80 rounds, 81 union passes, 82 label passes + reduction, 83 prune passes + reduction,
@@ -1126,16 +1158,14 @@ struct Team {
     }                                                                     \
   } while (0)
 
-// arr[idx] += 1 for every lane with `on`; lanes of the wave that share an index (the first two
-// distinct indices) are combined into one atomic -- a hub's edges and a giant component's
-// nodes would otherwise serialise thousands of atomics on one word.  Every lane of the wave
-// calls it (wave-uniform loops).
+// arr[idx] += 1 for every lane with `on`; lanes of the wave that share an index are combined
+// into one atomic -- a hub's edges and a giant component's nodes would otherwise serialise
+// thousands of returning atomics on one word.  Every lane of the wave calls it (wave-uniform
+// loops).
 template <class P>
 __device__ __forceinline__ void agg_add1(P arr, int idx, bool on) {
   unsigned long long m = __ballot(on);
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    if (m == 0ull) break;
+  while (m != 0ull) {  // one atomic per distinct index of the wave
     const int leader = __ffsll((long long)m) - 1;
     const int key = __shfl(idx, leader, 64);
     const unsigned long long same = __ballot(on && idx == key);
@@ -1143,7 +1173,25 @@ __device__ __forceinline__ void agg_add1(P arr, int idx, bool on) {
     if (idx == key) on = false;
     m &= ~same;
   }
-  if (on) uf_add(arr, idx, 1);
+}
+
+// agg_add1 on an HBM array, returning the largest count any of this lane's adds produced (the
+// lane that makes a word's last add sees the word's final count).
+__device__ __forceinline__ int agg_add1_max(int* arr, int idx, bool on) {
+  unsigned long long m = __ballot(on);
+  int best = 0;
+  while (m != 0ull) {  // one atomic per distinct index of the wave
+    const int leader = __ffsll((long long)m) - 1;
+    const int key = __shfl(idx, leader, 64);
+    const unsigned long long same = __ballot(on && idx == key);
+    if (lane_id() == leader) {
+      const int k = (int)__popcll(same);
+      best = max(best, __hip_atomic_fetch_add(arr + key, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + k);
+    }
+    if (idx == key) on = false;
+    m &= ~same;
+  }
+  return best;
 }
 
 // Reduces K 64-bit values over the grid (bit k of maxmask: max, else sum; every value >= 0 for
@@ -1240,6 +1288,7 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
   pr[0] = pr[1] = 0;
   while (true) {
     long long k0 = 0, k1 = 0;
+    if (T.prof_any != nullptr) T.t0any = wall_clock64();
     for (int e = T.gt; e < et; e += T.gs) {
       if (E.state(e) != E_ALIVE) continue;
       const int u = E.u(e), v = E.v(e);
@@ -1247,17 +1296,27 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
         E.kill(e, E_COVERED);
         if (e < e0) k0++; else k1++;
       } else {
-        uf_unite(e < e0 ? E.par0 : E.par1, u, v);
+        uf_unite_h(e < e0 ? E.par0 : E.par1, u, v);
       }
     }
     if (first)  // LMCC counters, used after the last round
       for (int x = T.gt; x < n; x += T.gs) uf_store(cnt, x, 0);
+    if (T.acc != nullptr) {  // diagnostics: workgroup 0's own union work (slot 88), before the barrier
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) T.acc[8] += wall_clock64() - T.t;
+    }
+    if (T.prof_any != nullptr) {  // slowest workgroup's union work (slot 89)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_fetch_max(T.prof_any + 9, wall_clock64() - T.t0any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (grid_sync(p, *T.target, T.flag)) return true;
     TEAM_ACC(T, 1);
     if (T.acc != nullptr && threadIdx.x == 0) T.acc[0] += 1;
     long long diff = 0;
     for (int x = T.gt; x < n; x += T.gs) {
-      const int r0 = uf_find(E.par0, x), r1 = uf_find(E.par1, x);
+      const int r0 = uf_find_h(E.par0, x), r1 = uf_find_h(E.par1, x);
       uf_store(E.deg0, x, r0);
       uf_store(E.deg1, x, r1);
       diff += r0 != r1;
@@ -1295,15 +1354,14 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
     pr[0] += (int)t2[0];
     pr[1] += (int)t2[1];
   }
-  // the LMCC: non-covered nodes per component (layer-0 label = layer-1 label at the fixed point)
+  // the LMCC: non-covered nodes per component (layer-0 label = layer-1 label at the fixed point);
+  // the largest count is the maximum over the adds' results (each word's last add sees its total)
+  long long best = 0;
   for (int xb = T.gt - lane_id(); xb < n; xb += T.gs) {
     const int x = xb + lane_id();
     const bool on = x < n && !E.covered(x);
-    agg_add1(cnt, on ? uf_load(E.deg0, x) : 0, on);
+    best = max(best, (long long)agg_add1_max(cnt, on ? uf_load(E.deg0, x) : 0, on));
   }
-  if (grid_sync(p, *T.target, T.flag)) return true;
-  long long best = 0;
-  for (int x = T.gt; x < n; x += T.gs) best = max(best, (long long)uf_load(cnt, x));
   const long long vb[1] = {best};
   long long tb[1];
   if (team_reduce<1>(p, T, vb, 1u, tb, nullptr)) return true;

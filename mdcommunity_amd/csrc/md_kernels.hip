@@ -2731,6 +2731,8 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
         T.tmp = (int*)(scr + S_M);
         T.acc = nullptr;
         T.t = 0;
+        T.prof_any = p.prof != nullptr && pstep < p.prof_cap ? p.prof + (size_t)pstep * PROF_SLOTS + 80 : nullptr;
+        T.t0any = 0;
         if (p.prof != nullptr && blockIdx.x == 0 && pstep < p.prof_cap) {
           T.acc = p.prof + (size_t)pstep * PROF_SLOTS + 80;
           if (threadIdx.x == 0) p.prof[(size_t)pstep * PROF_SLOTS + 87] = wall_clock64();

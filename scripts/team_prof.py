@@ -43,3 +43,5 @@ print("  per round us: union %.1f label %.1f prune %.1f" % (np.median(us(81) / r
                                                           np.median(us(83) / np.maximum(rd - 1, 1))))
 tot_team = R[:, 87].sum() / 1e5
 print("  team steps %.1f ms of the %.1f ms rollout kernel (the rest: decisions, barriers, forward passes)" % (tot_team, ms))
+print("  union pass: workgroup 0's own work %.1f us per round, slowest workgroup %.1f us (one round's max, median over steps)" % (
+    np.median(R[:, 88] / rd) / 100, np.median(R[:, 89]) / 100))
