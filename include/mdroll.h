@@ -167,6 +167,31 @@ md_status md_profile_read(md_ctx* ctx, uint64_t* out, int capacity_steps, int32_
 /* Library build string (arch, version). */
 const char* md_version(void);
 
+/* ---------------------------------------------------------------- synthetic graph generator
+ * Geometric Multiplex Model (U/GMM.py:6-68 with U/Hyperbolic.py:18-117, g = 0.5, nu = 0.2,
+ * gamma = 2.5, T = 0.4, kbar ~ U(2, 10)) on the device, SURVEY.md §8(f3).  Context-free (own
+ * device allocations; errors in md_gmm_last_error()).  mdcommunity_amd.gmm_gpu drives them. */
+const char* md_gmm_last_error(void);
+
+/* Per-node values of n_graphs graphs of n nodes: kbar_out [G][2], kappa_out / theta_out
+ * [G][2][n] (layer 0 then the conditioned layer 1: GMM.py:10-25).  Randomness: Philox4x32-10
+ * streams keyed by seeds[G] (not the reference's numpy stream), or -- for checks against the
+ * reference's own functions -- the caller's uniforms [4][G][n] (kappa1, kappa2, theta1, theta2)
+ * and kbar_in [G][2]. */
+md_status md_gmm_nodes(int device, int n_graphs, int n, const uint64_t* seeds, const double* uniforms,
+                       const double* kbar_in, double* kbar_out, double* kappa_out, double* theta_out);
+
+/* Links of n_layers layers of n nodes (CreateNetworks, U/Hyperbolic.py:101-117): pairs (i < j)
+ * in row-major order, kept when u < 1 / (1 + r^(1/T)); kappa / theta [L][n], mu [L].  Edges
+ * (u < v, lexicographic: the reference's networkx order) to edges_out [L][edge_cap][2], counts
+ * to edge_count [L].  uniforms [L][n(n-1)/2]: the reference's pair stream (exact mode; pairs
+ * within a relative 1e-9 of the threshold go to amb_out [L][amb_cap] / amb_count [L] for the
+ * caller to re-decide with the reference's own expression); else Philox pair streams keyed by
+ * seeds [L/2] (layers 2g, 2g + 1 of graph g). */
+md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, const double* theta, const double* mu,
+                       const double* uniforms, const uint64_t* seeds, int32_t* edges_out, int64_t* edge_count,
+                       int64_t edge_cap, int64_t* amb_out, int64_t* amb_count, int64_t amb_cap);
+
 /*
  * Diagnostic environment knobs, read once by md_create.  None changes any result (every
  * combination is covered by the GPU tests, which check identical rollouts); they select

@@ -46,24 +46,33 @@ def _conditional_theta(theta1, u, n, g=G_CORR):
     return np.mod(theta1 + two_pi * ell / n, two_pi)
 
 
+def link_mu(temp, kbar):
+    """CreateNetworks' mu (U/Hyperbolic.py:101-117)."""
+    return np.sin(temp * np.pi) / (2 * np.pi * temp * kbar)
+
+
+def link_keep(kappa, theta, temp, kbar, u, iu, ju):
+    """The link test of CreateNetworks for the pairs (iu, ju) with their uniforms u (also used
+    by gmm_gpu to re-decide the pairs the device flags as within rounding of the threshold)."""
+    n = len(kappa)
+    two_pi = 2 * np.pi
+    dtheta = n / (two_pi) * np.abs(np.pi - np.abs(np.pi - np.abs(theta[iu] - theta[ju])))
+    mu = link_mu(temp, kbar)
+    r = dtheta / (mu * kappa[iu] * kappa[ju])
+    return u < (1.0 / (1.0 + np.power(r, 1.0 / temp)))
+
+
 def _links(kappa, theta, temp, kbar, u):
     """CreateNetworks (U/Hyperbolic.py:101-117): pairs (i<j) in row-major order."""
     n = len(kappa)
-    two_pi = 2 * np.pi
     iu, ju = np.triu_indices(n, k=1)
-    dtheta = n / (two_pi) * np.abs(np.pi - np.abs(np.pi - np.abs(theta[iu] - theta[ju])))
-    mu = np.sin(temp * np.pi) / (two_pi * temp * kbar)
-    r = dtheta / (mu * kappa[iu] * kappa[ju])
-    keep = u < (1.0 / (1.0 + np.power(r, 1.0 / temp)))
+    keep = link_keep(kappa, theta, temp, kbar, u, iu, ju)
     return np.stack([iu[keep], ju[keep]], axis=1).astype(np.int32)
 
 
-def gmm_pair(n, seed=None, py_rng=None, np_rng=None):
-    """Two-layer GMM graph on n nodes: returns (edges0, edges1), each [E, 2] int32 with u < v
-    in lexicographic order (the networkx ``G.edges()`` order of the reference's graphs).
-
-    With ``seed`` the streams are ``random.seed(seed); np.random.seed(seed)`` as the
-    reference's callers do; otherwise pass ``random.Random`` / ``RandomState`` instances."""
+def node_values(n, seed=None, py_rng=None, np_rng=None):
+    """The per-node half of gmm_pair: (kbar1, kbar2, kappa1, kappa2, theta1, theta2, np_rng),
+    the numpy stream left where the pair draws start (U/GMM.py:10-25)."""
     if seed is not None:
         py_rng = _pyrandom.Random(seed)
         np_rng = np.random.RandomState(seed)
@@ -74,6 +83,16 @@ def gmm_pair(n, seed=None, py_rng=None, np_rng=None):
     kappa2 = _conditional_kappa(kappa1, np_rng.random_sample(n), kmin1, GAMMA, kmin2, GAMMA)
     theta1 = 2.0 * np.pi * np_rng.random_sample(n)
     theta2 = _conditional_theta(theta1, np_rng.random_sample(n), n)
+    return kbar1, kbar2, kappa1, kappa2, theta1, theta2, np_rng
+
+
+def gmm_pair(n, seed=None, py_rng=None, np_rng=None):
+    """Two-layer GMM graph on n nodes: returns (edges0, edges1), each [E, 2] int32 with u < v
+    in lexicographic order (the networkx ``G.edges()`` order of the reference's graphs).
+
+    With ``seed`` the streams are ``random.seed(seed); np.random.seed(seed)`` as the
+    reference's callers do; otherwise pass ``random.Random`` / ``RandomState`` instances."""
+    kbar1, kbar2, kappa1, kappa2, theta1, theta2, np_rng = node_values(n, seed, py_rng, np_rng)
     npairs = n * (n - 1) // 2
     e0 = _links(kappa1, theta1, TEMP, kbar1, np_rng.random_sample(npairs))
     e1 = _links(kappa2, theta2, TEMP, kbar2, np_rng.random_sample(npairs))
