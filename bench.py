@@ -425,7 +425,7 @@ def rank_main(args):
             dev = "cuda"
         dist = tdist
 
-    from mdcommunity_amd import engine, gmm, parallel
+    from mdcommunity_amd import engine, gmm, gmm_gpu, parallel
 
     if args.cpu_dry_run:
         def make_engine(weights, cost_mode=0):
@@ -505,7 +505,12 @@ def rank_main(args):
     if args.batch_graphs > 0:
         total = args.batch_graphs * world
         lo, hi = parallel.shard(total, rank, world)
-        bgraphs = [(args.n,) + gmm.gmm_pair(args.n, seed=s) for s in range(lo, hi)]
+        if args.cpu_dry_run:
+            bgraphs = [(args.n,) + gmm.gmm_pair(args.n, seed=s) for s in range(lo, hi)]
+        else:
+            # the reference's GMM streams, pair loop on the device (gmm_gpu exact mode: the same
+            # graphs as gmm.gmm_pair, outside the timed region)
+            bgraphs = [(args.n,) + e for e in gmm_gpu.gmm_pairs(args.n, range(lo, hi), exact=True, device=local if world > 1 else 0)]
         beng = make_engine(weights)
         beng.load_graphs(bgraphs)
         run_steps(beng, 1)
