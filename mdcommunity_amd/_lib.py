@@ -6,6 +6,7 @@ if the library or a GPU is missing, every entry point raises.
 """
 import ctypes
 import os
+import weakref
 
 import numpy as np
 
@@ -93,14 +94,19 @@ def _ptr(a, t):
     return a.ctypes.data_as(t) if a is not None else None
 
 
+_NPSEL = []
+
+
 def _numpy_argsort_ptr():
     """Address of numpy's own float64 argsort routine (the one np.argsort runs), from the
     package's _npsel helper; None when the helper is not built (the Python callback is used)."""
-    try:
-        from . import _npsel
-    except ImportError:
-        return None
-    return _npsel.argsort_f64()
+    if not _NPSEL:
+        try:
+            from . import _npsel
+            _NPSEL.append(_npsel.argsort_f64())
+        except ImportError:
+            _NPSEL.append(None)
+    return _NPSEL[0]
 
 
 def _argsort_select(q, n_out):
@@ -125,6 +131,15 @@ class Engine:
         self.node_off = None
         self._cb_error = None
         self.selector = _argsort_select
+        self._tie_native = False  # the argsort routine registered with md_set_tie_argsort (False: none yet)
+        self._views = {}
+        wr = weakref.ref(self)  # no reference cycle through the thunk: close() still runs from __del__
+
+        def cb(user, g, qp, n, n_out, out):
+            eng = wr()
+            return eng._select_cb(user, g, qp, n, n_out, out) if eng is not None else 1
+
+        self._ccb = SELECT_CB_ADDR(cb)  # one C thunk per engine (the hot path reuses it)
 
     def _check(self, st, h="self"):
         if st != MD_OK:
@@ -187,41 +202,39 @@ class Engine:
         self._check(self.lib.md_step(self.h, _ptr(a, _i32p), _ptr(lm, _i32p), _ptr(term, _u8p)))
         return lm, term.astype(bool)
 
+    def _view(self, addr, n, ct, dt):
+        key = (addr, n, dt)
+        a = self._views.get(key)
+        if a is None:
+            a = self._views[key] = np.frombuffer((ct * n).from_address(addr), dtype=dt)
+        return a
+
+    def _select_cb(self, user, g, qp, n, n_out, out):
+        # the row is the library's buffer, valid during the call (the selector must not keep
+        # it); hot path of every tied step, hence the cached views
+        try:
+            q = self._view(qp, n, ctypes.c_double, np.float64)
+            sel = self.selector(q, n_out)
+            o = self._view(out, n_out, ctypes.c_int32, np.int32)
+            o[:] = sel[:n_out]
+            return 0
+        except Exception as ex:  # surfaced after md_rollout returns
+            self._cb_error = ex
+            return 1
+
     def rollout(self, step=1):
         # the default rule np.argsort(-q)[:step] runs on the library's host thread through numpy's
         # own argsort routine; a custom selector goes through the callback
         native = _numpy_argsort_ptr() if self.selector is _argsort_select else None
-        self._check(self.lib.md_set_tie_argsort(self.h, native))
+        if native != self._tie_native:
+            self._check(self.lib.md_set_tie_argsort(self.h, native))
+            self._tie_native = native
         tot = int(self.node_off[-1])
-        seq = np.zeros(tot, np.int32)
-        lm = np.zeros(tot, np.int32)
+        seq = np.empty(tot, np.int32)
+        lm = np.empty(tot, np.int32)
         ln = np.zeros(len(self.n_nodes), np.int32)
         self._cb_error = None
-
-        views = {}
-
-        def view(addr, n, ct, dt):
-            key = (addr, n, dt)
-            a = views.get(key)
-            if a is None:
-                a = views[key] = np.frombuffer((ct * n).from_address(addr), dtype=dt)
-            return a
-
-        def cb(user, g, qp, n, n_out, out):
-            # the row is the library's buffer, valid during the call (the selector must not
-            # keep it); hot path of every tied step, hence the cached views
-            try:
-                q = view(qp, n, ctypes.c_double, np.float64)
-                sel = self.selector(q, n_out)
-                o = view(out, n_out, ctypes.c_int32, np.int32)
-                o[:] = sel[:n_out]
-                return 0
-            except Exception as ex:  # surfaced after md_rollout returns
-                self._cb_error = ex
-                return 1
-
-        ccb = SELECT_CB_ADDR(cb)
-        st = self.lib.md_rollout(self.h, int(step), _ptr(seq, _i32p), _ptr(lm, _i32p), _ptr(ln, _i32p), ccb, None)
+        st = self.lib.md_rollout(self.h, int(step), _ptr(seq, _i32p), _ptr(lm, _i32p), _ptr(ln, _i32p), self._ccb, None)
         if self._cb_error is not None:
             raise self._cb_error
         self._check(st)

@@ -30,6 +30,7 @@ void build_weight_image(const float* w, float* img);
 hipError_t launch_rollout(const Params& p, const float* wimg, int grid, hipStream_t s);
 hipError_t launch_h0(const float* w, float* tab, int dm_lo, int dm_hi, hipStream_t s);
 hipError_t launch_reset(const Params& p, hipStream_t s);
+hipError_t launch_clear(void* const* ptr, const size_t* bytes, int n, hipStream_t s);
 hipError_t set_kernel_attrs();
 }  // namespace md
 
@@ -128,6 +129,9 @@ struct md_ctx {
   HostBuf<int> h_nact, h_act;
   HostBuf<float> h_q;
   HostBuf<float> h_chk;
+  HostBuf<unsigned> h_done;  // launch completion record {tag, error word} (kernel_exit)
+  HostBuf<int> h_gvar;       // GraphVars of the last launch, copied by kernel_exit
+  bool vars_stale = false;   // a launch ended without its completion record
   bool need_gscr = false;
   DevBuf<unsigned long long> prof;
   int prof_cap = 0;
@@ -158,6 +162,7 @@ struct md_ctx {
     apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); nbc.release(); qslot.release(); qg.release(); tr_q.release(); node_w.release();
     sres.release(); qspec.release(); bars.release();
     h_req.release(); h_ans.release(); h_nact.release(); h_act.release(); h_q.release(); h_chk.release();
+    h_done.release(); h_gvar.release();
     ng = 0;
     hinfo.clear();
     hvar.clear();
@@ -184,7 +189,7 @@ md_status fail(md_ctx* c, md_status s, const char* fmt, ...) {
   } while (0)
 
 // Control block layout (ints): [0] barrier counter, [1] error word (zeroed before each launch).
-constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_Q = 2, CTL_SPEC = 8, CTL_TEAM = 12, CTL_WORDS = 16;
+constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_Q = 2, CTL_SPEC = 8, CTL_TEAM = 12, CTL_EXIT = 14, CTL_WORDS = 16;
 constexpr int SPEC_MAX = 32;  // speculative workgroups per launch at most  // CTL_SPEC: u64 request word
 
 Params make_params(md_ctx* c) {
@@ -455,16 +460,26 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
                          ? std::max(0, std::min(c->spec_n, c->cus - grid))
                          : 0;
   HIPCHK(c, hipMemcpyAsync(c->glist.p, gl, sizeof(int) * ngl, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemsetAsync(c->ctl.p, 0, sizeof(int) * CTL_WORDS, c->stream));
-  HIPCHK(c, hipMemsetAsync(c->bars.p, 0, sizeof(unsigned) * c->bars.n, c->stream));
-  // graph-head hand-off granules carry the step as their tag: stale tags from earlier launches
-  // must not match
-  if (n_env > 0) HIPCHK(c, hipMemsetAsync(c->hbuf.p, 0, sizeof(float) * c->hbuf.n, c->stream));
-  if (n_env > 0)  // the slots a launch of this grid can use (split tiles <= tile workgroups / 2)
-    HIPCHK(c, hipMemsetAsync(c->xbuf.p, 0, sizeof(unsigned long long) * 2048 * std::min(XB_SLOTS, grid / 2 + 1), c->stream));
-  if (qmode) {
-    HIPCHK(c, hipMemsetAsync(c->qslot.p, 0, sizeof(unsigned long long) * c->qslot.n, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->qg.p, 0, sizeof(int) * c->qg.n, c->stream));
+  {
+    // per-launch clears in one dispatch: control words, barrier shards; graph-head hand-off
+    // granules carry the step as their tag (stale tags from earlier launches must not match);
+    // the split hand-off slots a launch of this grid can use (split tiles <= tile workgroups / 2);
+    // the work queue
+    void* ptr[6] = {c->ctl.p, c->bars.p, nullptr, nullptr, nullptr, nullptr};
+    size_t bytes[6] = {sizeof(int) * CTL_WORDS, sizeof(unsigned) * c->bars.n, 0, 0, 0, 0};
+    if (n_env > 0) {
+      ptr[2] = c->hbuf.p;
+      bytes[2] = sizeof(float) * c->hbuf.n;
+      ptr[3] = c->xbuf.p;
+      bytes[3] = sizeof(unsigned long long) * 2048 * std::min(XB_SLOTS, grid / 2 + 1);
+    }
+    if (qmode) {
+      ptr[4] = c->qslot.p;
+      bytes[4] = sizeof(unsigned long long) * c->qslot.n;
+      ptr[5] = c->qg.p;
+      bytes[5] = sizeof(int) * c->qg.n;
+    }
+    HIPCHK(c, launch_clear(ptr, bytes, 6, c->stream));
   }
   Params p = make_params(c);
   p.n_main = grid;
@@ -500,15 +515,26 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
     p.endgame = run_mode == RUN_ROLLOUT && c->tie_argsort != nullptr && sel->step == 1 &&
                 c->cost_mode == MD_COST_UNIT && !(c->variant & 2048);
   }
+  // completion record: the last workgroup copies the GraphVars and the error word to mapped
+  // host memory and then writes the launch tag (kernel_exit)
+  const bool rec = c->h_done.h != nullptr && c->h_gvar.h != nullptr;
+  if (rec) {
+    __atomic_store_n(c->h_done.h, 0u, __ATOMIC_RELAXED);
+    p.exit_ctr = (unsigned*)(c->ctl.p + CTL_EXIT);
+    p.h_done = c->h_done.d;
+    p.h_gvar = c->h_gvar.d;
+  }
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   HIPCHK(c, launch_rollout(p, c->wimg.p, grid + n_spec, c->stream));
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-  if (hs) {
-    // serve selection requests while the launch runs
+  // Wait for the launch while serving selection requests (hs): the completion tag is read on
+  // every pass (host memory, no runtime call); the launch's completion event only every 20 us
+  // (a launch that ended without its record: a fault, or an early exit) and, once the tag is
+  // there, until the kernel has retired.
+  bool tagged = false;
+  {
     std::vector<double> qd;
     std::vector<int32_t> acts;
-    // requests are scanned continuously; the launch's completion event (a runtime call) only
-    // every 20 us, and once more after the last scan that found it complete
     auto last = std::chrono::steady_clock::now();
     const auto t_launch = last;
     static const bool host_stats = std::getenv("MD_HOST_STATS") != nullptr;  // diagnostics
@@ -517,35 +543,52 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
     bool done = false;
     while (true) {
       bool served = false;
-      for (int g : v) {
-        const unsigned r = __atomic_load_n(c->h_req.h + g, __ATOMIC_ACQUIRE);
-        if (r != 0 && r != __atomic_load_n(c->h_ans.h + g, __ATOMIC_RELAXED)) {
-          const auto ts = std::chrono::steady_clock::now();
-          serve_request(c, sel, g, r, qd, acts);
-          if (host_stats) {
-            serve_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
-            ++n_served;
+      if (hs) {
+        for (int g : v) {
+          const unsigned r = __atomic_load_n(c->h_req.h + g, __ATOMIC_ACQUIRE);
+          if (r != 0 && r != __atomic_load_n(c->h_ans.h + g, __ATOMIC_RELAXED)) {
+            const auto ts = std::chrono::steady_clock::now();
+            serve_request(c, sel, g, r, qd, acts);
+            if (host_stats) {
+              serve_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
+              ++n_served;
+            }
+            served = true;
           }
-          served = true;
         }
       }
       if (done) break;
+      if (rec && !tagged && __atomic_load_n(c->h_done.h, __ATOMIC_ACQUIRE) == p.launch_seq) tagged = true;
       const auto now = std::chrono::steady_clock::now();
-      if (!served && now - last >= std::chrono::microseconds(20)) {
+      if (tagged || (!served && now - last >= std::chrono::microseconds(20))) {
         last = now;
         const hipError_t q = hipEventQuery(c->ev1);
         if (q != hipSuccess && q != hipErrorNotReady) HIPCHK(c, q);
         done = q == hipSuccess;
       }
-      if (c->poll_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(c->poll_us));
+      if (!hs && !done && !tagged) {
+        if (!rec) {
+          HIPCHK(c, hipEventSynchronize(c->ev1));
+          done = true;
+        }
+      } else if (c->poll_us > 0 && !tagged) {
+        std::this_thread::sleep_for(std::chrono::microseconds(c->poll_us));
+      }
     }
-    if (host_stats)
+    if (hs && host_stats)
       std::fprintf(stderr, "md host: %d requests served in %.3f ms of a %.3f ms launch wait\n", n_served, 1e3 * serve_s,
                    1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t_launch).count());
   }
   int dev_err = 0;
-  HIPCHK(c, hipMemcpyAsync(&dev_err, c->ctl.p + CTL_ERR, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (rec && __atomic_load_n(c->h_done.h, __ATOMIC_ACQUIRE) == p.launch_seq) {
+    dev_err = (int)__atomic_load_n(c->h_done.h + 1, __ATOMIC_RELAXED);
+    constexpr int GVW = (int)(sizeof(GraphVar) / sizeof(int));
+    for (int g : v) std::memcpy(&c->hvar[g], c->h_gvar.h + (size_t)g * GVW, sizeof(GraphVar));
+  } else {
+    c->vars_stale = true;  // launch() pulls every GraphVar
+    HIPCHK(c, hipMemcpyAsync(&dev_err, c->ctl.p + CTL_ERR, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
   float ms = 0.f;
   HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
   c->last_ms += ms;
@@ -565,12 +608,17 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
 }
 
 md_status launch(md_ctx* c, const std::vector<int>& gl, int run_mode, int host_select, Selector* sel = nullptr) {
+  c->vars_stale = false;
   for (size_t i = 0; i < gl.size(); i += G_CAP) {
     const int k = (int)std::min<size_t>(G_CAP, gl.size() - i);
     md_status st = launch_chunk(c, gl.data() + i, k, run_mode, host_select, sel);
-    if (st != MD_OK) return st;
+    if (st != MD_OK) {
+      (void)pull_vars(c);
+      return st;
+    }
   }
-  return pull_vars(c);
+  // the launches' completion records carried their GraphVars; otherwise copy them all back
+  return c->vars_stale ? pull_vars(c) : MD_OK;
 }
 
 void host_first_layer(const float* w, const float* nw, float* out) {
@@ -842,6 +890,8 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->h_act.alloc(c->tot_n));
   HIPCHK(c, c->h_q.alloc(c->tot_n));
   HIPCHK(c, c->h_chk.alloc(2 * (size_t)n_graphs));
+  if (c->h_done.h == nullptr) HIPCHK(c, c->h_done.alloc(2));
+  HIPCHK(c, c->h_gvar.alloc((size_t)n_graphs * (sizeof(GraphVar) / sizeof(int))));
   HIPCHK(c, hipMemcpyAsync(c->ginfo.p, info.data(), sizeof(GraphInfo) * n_graphs, hipMemcpyHostToDevice, c->stream));
   if (c->cost_mode == MD_COST_DEGREE) {
     HIPCHK(c, c->node_w.alloc(2 * tn));
@@ -1015,9 +1065,9 @@ md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, i
     }
     gl.swap(next);
   }
-  std::vector<int> buf(c->tot_n);
-  if (seq_out) HIPCHK(c, hipMemcpy(seq_out, c->tr_action.p, sizeof(int) * c->tot_n, hipMemcpyDeviceToHost));
-  if (lmcc_out) HIPCHK(c, hipMemcpy(lmcc_out, c->tr_rank.p, sizeof(int) * c->tot_n, hipMemcpyDeviceToHost));
+  if (seq_out) HIPCHK(c, hipMemcpyAsync(seq_out, c->tr_action.p, sizeof(int) * c->tot_n, hipMemcpyDeviceToHost, c->stream));
+  if (lmcc_out) HIPCHK(c, hipMemcpyAsync(lmcc_out, c->tr_rank.p, sizeof(int) * c->tot_n, hipMemcpyDeviceToHost, c->stream));
+  if (seq_out || lmcc_out) HIPCHK(c, hipStreamSynchronize(c->stream));
   if (seq_len)
     for (int g = 0; g < c->ng; ++g) seq_len[g] = c->hvar[g].steps;
   return MD_OK;

@@ -117,6 +117,12 @@ struct Params {
   unsigned* bar;                   // error word of the grid barrier (bit 31; zeroed per launch)
   unsigned* bars;                  // grid barrier arrival counters: 8 shards x 64 words (zeroed per launch)
   // host selection hand-shake (mapped pinned host memory; null: end the launch instead)
+  // launch completion record in mapped host memory (null: the host reads the device words):
+  // the last workgroup to exit copies the launch's GraphVars and the error word there, then
+  // writes the launch tag, so the host needs no runtime call to learn that a launch is done
+  unsigned* exit_ctr;              // device: workgroups that finished this launch (cleared per launch)
+  unsigned* h_done;                // mapped host: {launch tag, error word}
+  int* h_gvar;                     // mapped host: GraphVar copies [n_graphs]
   unsigned* h_req;                 // per graph: request tag (device writes)
   unsigned* h_ans;                 // per graph: answer tag (host writes)
   int* h_nact;                     // per graph: actions answered (-1: abort)

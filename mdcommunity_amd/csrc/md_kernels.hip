@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <algorithm>
+
 #include "md_common.h"
 
 namespace md {
@@ -3000,12 +3002,40 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
     __hip_atomic_store((g_u64*)p.spec_req, SPEC_EXIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Completion record (p.h_done): every workgroup drains its stores and counts itself out; the
+// last one copies the launch's GraphVars and the error word to mapped host memory with
+// system-scope stores, drains them, then writes the launch tag.  The host polls the tag
+// instead of querying the runtime, and reads the GraphVars without a copy.
+__device__ __noinline__ void kernel_exit(KParams&) {
+  KParams& p = kp();
+  if (p.h_done == nullptr) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ int last;
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add((g_u32*)p.exit_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  for (int i = threadIdx.x; i < p.nglist * GV_WORDS; i += NTHREADS) {
+    const int g = p.glist[i / GV_WORDS], k = i % GV_WORDS;
+    __hip_atomic_store(p.h_gvar + (size_t)g * GV_WORDS + k, ldc((const int*)(p.gvar + g) + k), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (threadIdx.x == 0)
+    __hip_atomic_store(p.h_done + 1, (unsigned)__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(p.h_done, p.launch_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void __launch_bounds__(NTHREADS, 1) md_rollout_kernel(Params p, const float* __restrict__ wimg) {
   if (!kargs_layout_ok()) {
     if (threadIdx.x == 0) __hip_atomic_store(p.err, ERR_ABI, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   engine_body(kp(), wimg);
+  kernel_exit(kp());
 }
 
 // Batched rollouts through the device work queue (queue_loop); its own entry point so the
@@ -3028,6 +3058,7 @@ __global__ void __launch_bounds__(NTHREADS, 1) md_queue_kernel(Params p, const f
   }
   __syncthreads();
   queue_loop(kpp, lds, wimg);
+  kernel_exit(kpp);
 }
 
 __global__ void __launch_bounds__(NTHREADS, 1) md_env_kernel(Params p, const float* __restrict__ wimg) {
@@ -3036,6 +3067,23 @@ __global__ void __launch_bounds__(NTHREADS, 1) md_env_kernel(Params p, const flo
     return;
   }
   engine_body(kp(), wimg);
+  kernel_exit(kp());
+}
+
+// Clears up to six device ranges (bytes, multiples of 4) in one launch: the per-launch control
+// words, barrier shards and hand-off tags that would otherwise take one memset dispatch each.
+struct ClearList {
+  void* ptr[6];
+  unsigned long long bytes[6];
+  int n;
+};
+__global__ void __launch_bounds__(256) md_clear_kernel(ClearList cl) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+  for (int k = 0; k < cl.n; ++k) {
+    unsigned* w = (unsigned*)cl.ptr[k];
+    const size_t nw = cl.bytes[k] / 4;
+    for (size_t i = t; i < nw; i += stride) w[i] = 0u;
+  }
 }
 
 // Reset every graph in glist to the initial (pre-s0) state.
@@ -3142,6 +3190,23 @@ hipError_t launch_rollout(const Params& p, const float* wimg, int grid, hipStrea
 hipError_t launch_h0(const float* w, float* tab, int dm_lo, int dm_hi, hipStream_t s) {
   if (dm_hi < dm_lo) return hipSuccess;
   hipLaunchKernelGGL(md_h0_kernel, dim3(dm_hi - dm_lo + 1), dim3(256), 0, s, w, tab, dm_lo, dm_hi);
+  return hipGetLastError();
+}
+
+hipError_t launch_clear(void* const* ptr, const size_t* bytes, int n, hipStream_t s) {
+  ClearList cl;
+  size_t tot = 0;
+  cl.n = 0;
+  for (int k = 0; k < n && cl.n < 6; ++k) {
+    if (ptr[k] == nullptr || bytes[k] == 0) continue;
+    cl.ptr[cl.n] = ptr[k];
+    cl.bytes[cl.n] = bytes[k];
+    tot += bytes[k];
+    cl.n++;
+  }
+  if (cl.n == 0) return hipSuccess;
+  const int blocks = (int)std::min<size_t>(1024, (tot / 4 + 255) / 256);
+  hipLaunchKernelGGL(md_clear_kernel, dim3(std::max(1, blocks)), dim3(256), 0, s, cl);
   return hipGetLastError();
 }
 
