@@ -771,7 +771,7 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
     gi.n = n;
     gi.node_off = (int)tn;
     gi.tile_off = (int)tt;
-    gi.pad = 0;
+    gi.gidx = g;
     for (int l = 0; l < 2; ++l) {
       const int64_t ne = eo[l][g + 1] - eo[l][g];
       if (ne < 0) return fail(c, MD_EINVAL, "graph %d layer %d: negative edge count", g, l);

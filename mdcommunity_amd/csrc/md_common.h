@@ -53,7 +53,7 @@ struct GraphInfo {           // immutable after md_load_graphs
   int roff[2];               // into row-pointer arrays (n + 1 entries per graph)
   int coff[2];               // into CSR entry arrays (2 e entries per graph)
   int tile_off;              // into per-tile arrays (ceil(n / 16) tiles per graph)
-  int pad;
+  int gidx;                  // the graph's index (its GraphVar)
 };
 
 struct GraphVar {            // mutable per-graph state

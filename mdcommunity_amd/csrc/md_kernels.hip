@@ -685,6 +685,18 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
 // Gather for one tile: waves 0-3 layer 0, 4-7 layer 1; each wave handles rows 4*(w&3)..+3
 // concurrently, one 16-lane group per row, every lane owning 4 features (float4 loads).
 // it == 1: previous embedding = first-layer table (by degree, unit cost) or static input.
+// Iteration 1, unit cost: first-layer rows by residual degree d (row d of the returned base).
+// The precomputed table of the step's dmax (md_h0_kernel, at load) when it exists -- phase A
+// then copies nothing -- else the graph's own table, rebuilt by phase A.  The dmax load goes
+// out beside the degree loads it is needed with.
+__device__ __forceinline__ const float* first_layer_rows(KParams& p, const GraphInfo& gi, int l) {
+  if (p.h0g != nullptr && !(p.variant & 1)) {  // MD_VARIANT bit 1: the graph's own table (phase A copies)
+    const int dm = ldc(&p.gvar[gi.gidx].dmax[l]);
+    if (dm >= 1 && dm <= p.h0g_dm) return p.h0g + (h0g_row(dm, 1) - 1) * EMB;  // row d at base + d rows
+  }
+  return p.h0tab[l] + (size_t)gi.node_off * EMB;
+}
+
 __device__ __noinline__ void gather_tile(KParams&, const GraphInfo gi, int it, const int*, float*) {
   const int* const rows = (const int*)(lds_base() + L_SCR + S_ROW);
   float* const scr = lds_base() + L_SCR;
@@ -699,8 +711,8 @@ __device__ __noinline__ void gather_tile(KParams&, const GraphInfo gi, int it, c
   const float* hp;
   bool table = false;
   if (it == 1) {
-    hp = p.h0tab[l] + (size_t)gi.node_off * EMB;
     table = p.node_w == nullptr;
+    hp = table ? first_layer_rows(p, gi, l) : p.h0tab[l] + (size_t)gi.node_off * EMB;
   } else {
     hp = p.H[l][(it - 2) & 1] + (size_t)gi.node_off * EMB;
   }
@@ -919,8 +931,8 @@ __device__ __noinline__ void gather_tile2(KParams&, const GraphInfo gi, int it, 
   const float* hp;
   bool table = false;
   if (it == 1) {
-    hp = p.h0tab[l] + (size_t)gi.node_off * EMB;
     table = p.node_w == nullptr;
+    hp = table ? first_layer_rows(p, gi, l) : p.h0tab[l] + (size_t)gi.node_off * EMB;
   } else {
     hp = p.H[l][(it - 2) & 1] + (size_t)gi.node_off * EMB;
   }
@@ -1054,8 +1066,8 @@ __device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it,
   const float* hp;
   bool table = false;
   if (it == 1) {
-    hp = p.h0tab[l] + (size_t)gi.node_off * EMB;
     table = p.node_w == nullptr;
+    hp = table ? first_layer_rows(p, gi, l) : p.h0tab[l] + (size_t)gi.node_off * EMB;
   } else {
     hp = p.H[l][(it - 2) & 1] + (size_t)gi.node_off * EMB;
   }
