@@ -881,7 +881,7 @@ __device__ __forceinline__ void h0_update(KParams& p, const GraphInfo& gi, Graph
       const int dm = l ? dm1 : dm0;
       if (dm == (l ? hd1 : hd0)) continue;
       float* tab = p.h0tab[l] + (size_t)gi.node_off * EMB;  // degrees <= n-1 fit the graph's rows
-      if (dm <= p.h0g_dm && p.h0g != nullptr && !(p.variant & 1)) continue;  // the tiles read the precomputed table
+      if (dm <= p.h0g_dm && p.h0g != nullptr && !(p.variant & 4)) continue;  // the tiles read the precomputed table
       if (dm <= p.h0g_dm) {
         // the table of this dmax is precomputed (md_h0_kernel at load): a 16-byte copy
         const float* src = p.h0g + h0g_row(dm, 1) * EMB;

@@ -690,7 +690,7 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
 // then copies nothing -- else the graph's own table, rebuilt by phase A.  The dmax load goes
 // out beside the degree loads it is needed with.
 __device__ __forceinline__ const float* first_layer_rows(KParams& p, const GraphInfo& gi, int l) {
-  if (p.h0g != nullptr && !(p.variant & 1)) {  // MD_VARIANT bit 1: the graph's own table (phase A copies)
+  if (p.h0g != nullptr && !(p.variant & 4)) {  // MD_VARIANT bit 4: the graph's own table (phase A copies)
     const int dm = ldc(&p.gvar[gi.gidx].dmax[l]);
     if (dm >= 1 && dm <= p.h0g_dm) return p.h0g + (h0g_row(dm, 1) - 1) * EMB;  // row d at base + d rows
   }
