@@ -197,6 +197,12 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  * combination is covered by the GPU tests, which check identical rollouts); they select
  * between equivalent execution strategies for A/B measurement and for exercising fallbacks:
  *   MD_VARIANT        bit mask, default 0:
+ *                       2     one graph too large for LDS: its environment step on one workgroup
+ *                             (and through the work queue) instead of on every workgroup
+ *                             (team_env_step); with 64 and MD_ENV_MODE=0 that step also runs
+ *                             for graphs that fit
+ *                       4     iteration-1 gathers read the graph's own first-layer table (phase A
+ *                             copies the precomputed rows) instead of the precomputed table
  *                       8     per-piece queue-mode profile stamps (md_profile; qprof build)
  *                       16    no neighbour-list cache (every tile rebuilds its lists)
  *                       32    lock-step shared mode instead of the device work queue (> 16 graphs)
