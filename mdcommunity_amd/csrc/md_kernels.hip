@@ -1612,6 +1612,21 @@ __device__ __noinline__ void attention_q_tile(KParams&, float*, float*, const Gr
 
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   const float* wi = lds + L_W;
+#ifdef MD_QPROF
+  // queue-mode piece profile (qprof build, MD_VARIANT bit 8): slots 88.. of the launch record
+  unsigned long long* qa = p.prof != nullptr && p.qmode && (p.variant & 8) ? p.prof + 88 : nullptr;
+  unsigned long long tqa = qa != nullptr ? wall_clock64() : 0ull;
+#define QATS(k)                                                   \
+  do {                                                            \
+    if (qa != nullptr && threadIdx.x == 0) {                      \
+      const unsigned long long now_ = wall_clock64();             \
+      atomicAdd(qa + (k), now_ - tqa);                            \
+      tqa = now_;                                                 \
+    }                                                             \
+  } while (0)
+#else
+#define QATS(k) do {} while (0)
+#endif
   const int w = wave_id(), l = w >> 2, cb = w & 3, lane = lane_id();
   const int ar = lane & 15, ak = lane >> 4;
   const int col = 16 * cb + ar;
@@ -1636,6 +1651,7 @@ __device__ __noinline__ void attention_q_tile(KParams&, float*, float*, const Gr
   }
   __syncthreads();
   TSTAMP(38);
+  QATS(0);
   float* dot = scr + S_DOT;
   float* gate = dot + 48;  // [2][16] weight of the other layer per (layer, row)
   if (w == 0) {
@@ -1668,6 +1684,7 @@ __device__ __noinline__ void attention_q_tile(KParams&, float*, float*, const Gr
   }
   __syncthreads();
   TSTAMP(33);
+  QATS(1);
   TSTAMP(35);
   // mix E_l = F_l + gate * F_other (mul then add, as the reference) fused into the first pass
   // of the row normalisation (each element is read there by exactly one thread)
@@ -1700,8 +1717,10 @@ __device__ __noinline__ void attention_q_tile(KParams&, float*, float*, const Gr
   }
   __syncthreads();
   TSTAMP(39);
+  QATS(2);
   if (htag != 0ull) head_receive(p, lds, g, htag);
   TSTAMP(40);
+  QATS(3);
   {
     // e[a] = sum_b (h[a] * y[b]) * cp[b]: the reference's outer product then x cross_product
     // (net :356-363), a batched [64,64]x[64,1] matmul = an FMA chain over b.  Each thread
@@ -1740,6 +1759,7 @@ __device__ __noinline__ void attention_q_tile(KParams&, float*, float*, const Gr
   }
   __syncthreads();
   TSTAMP(41);
+  QATS(4);
   float* hid = scr + S_HID;
   if (cb < 2) {
     const float* hf = wi + W_IH1 + cb * 16 * 64;
@@ -1771,6 +1791,7 @@ __device__ __noinline__ void attention_q_tile(KParams&, float*, float*, const Gr
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   TSTAMP(42);
+  QATS(5);
   if (threadIdx.x < 64) {
     // q = w0 * Q0 + w1 * Q1 per row, and the tile's arg-max partial by a 16-lane butterfly
     // (max / min index / count / second: order-free, as the sequential scan)
@@ -1799,7 +1820,10 @@ __device__ __noinline__ void attention_q_tile(KParams&, float*, float*, const Gr
     if (lane == 0) stc4(apart_out, 0, make_float4(bm, bs, __int_as_float(bi), __int_as_float(bc)));
   }
   __syncthreads();
+  QATS(6);
+#undef QATS
 }
+
 
 // Phase timestamps of workgroup 0 (diagnostics only; p.prof == nullptr in normal runs).
 #define MD_PROF(slot)                                                                            \

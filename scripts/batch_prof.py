@@ -53,6 +53,8 @@ if len(P) and P[0, 0] == 1 and P[0, 9] > 0:
         env_n = ["stage", "fixed point", "features", "write-back", "h0 table"]
         print("  ENV pieces (WG-ms): " + "  ".join("%s %.1f" % (nm, v) for nm, v in zip(env_n, P[0, 80:85] / 1e5)) +
               " | phase A total %.1f  neighbour lists %.1f" % (P[0, 85] / 1e5, P[0, 86] / 1e5))
+        att_n = ["tanh GEMM", "dots+gates", "mix+norm", "head", "e-chain", "hidden+Q", "arg-max+stores"]
+        print("  attention pieces (WG-ms): " + "  ".join("%s %.1f" % (nm, v) for nm, v in zip(att_n, P[0, 88:95] / 1e5)))
         sys.exit(0)
     wb = P[0, 20:64] / 1e5
     nb_ = int(np.max(np.nonzero(wb)[0])) + 1 if np.any(wb) else 0
