@@ -189,7 +189,7 @@ md_status fail(md_ctx* c, md_status s, const char* fmt, ...) {
   } while (0)
 
 // Control block layout (ints): [0] barrier counter, [1] error word (zeroed before each launch).
-constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_Q = 2, CTL_SPEC = 8, CTL_TEAM = 12, CTL_EXIT = 14, CTL_WORDS = 16;
+constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_Q = 2, CTL_SPEC = 8, CTL_TEAM = 12, CTL_EXIT = 14, CTL_PRE = 16, CTL_WORDS = 24;
 constexpr int SPEC_MAX = 32;  // speculative workgroups per launch at most  // CTL_SPEC: u64 request word
 
 Params make_params(md_ctx* c) {
@@ -490,6 +490,10 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
     p.sres_stride = c->sres_stride;
     p.qspec = c->qspec.p;
     p.qspec_n = (int)c->tot_n;
+    if (!(c->variant & 1)) {  // MD_VARIANT bit 1: no iteration-1 prebuild
+      p.pre_ew = (unsigned long long*)(c->ctl.p + CTL_PRE);
+      p.pre_cw = (unsigned long long*)(c->ctl.p + CTL_PRE + 2);
+    }
   }
   p.qmode = qmode ? 1 : 0;
   p.nglist = ngl;

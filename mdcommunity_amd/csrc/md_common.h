@@ -156,6 +156,13 @@ struct Params {
   int* sres;                       // per speculative workgroup: result slot of sres_stride ints
   int sres_stride;
   float* qspec;                    // [2][qspec_n]: Q of the last two predictions (never masked)
+  // iteration-1 prebuild (single-graph rollouts with speculative steps): phase A publishes the
+  // speculative result it takes as soon as it knows it (pre_ew: {request tag << 32 | node << 16 |
+  // slot}) and, at its end, the same word again when the step's final state is exactly that
+  // result (pre_cw, else 0); the tile workgroups build their rows and alive-neighbour lists from
+  // the result while phase A runs and keep them when the confirmation matches
+  unsigned long long* pre_ew;
+  unsigned long long* pre_cw;
   int qspec_n;                     // total nodes of the loaded batch
 };
 

@@ -992,6 +992,13 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
       if (sts != nullptr && threadIdx.x == 0) sts[71] = wall_clock64();
       spec_slot = E.tmp[A_TMP_WORDS - 1];
       spec_nd = E.tmp[A_TMP_WORDS - 2];
+      if (p.pre_ew != nullptr && threadIdx.x == 0) {
+        // the tile workgroups may build their iteration-1 lists from this result meanwhile
+        const unsigned long long ew = spec_slot >= 0 ? ((unsigned long long)want << 32) | ((unsigned)a << 16) | (unsigned)spec_slot : 0ull;
+        ((volatile unsigned*)(lds_base + L_MISC))[56] = (unsigned)ew;
+        ((volatile unsigned*)(lds_base + L_MISC))[57] = (unsigned)(ew >> 32);
+        if (ew != 0ull) __hip_atomic_store((g_u64*)p.pre_ew, ew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       __syncthreads();
     }
   }

@@ -272,24 +272,40 @@ __device__ __forceinline__ bool md_bok(bool ok, int site) {
 // (~12 ns each, MI355X_MICROARCH.md fanin row), the shards take 1/8 of them each.  Wave 0
 // polls every shard and the error word in one instruction; `target` counts this workgroup's
 // barriers.  Speculative workgroups (blockIdx >= n_main) take no part.
-__device__ __forceinline__ bool grid_sync(KParams& p, unsigned& target, int* flag) {
+__device__ __forceinline__ void grid_arrive(KParams& p, unsigned& target) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   target += 1;
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add((g_u32*)(p.bars + BAR_STRIDE * (blockIdx.x % BAR_SHARDS)), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+// Waits for the barrier `target` (after grid_arrive); *flag = 1 (uniform) when an error was
+// raised anywhere, as grid_sync.  With `watch` set it also returns early when the 8-byte word
+// *watch differs from `seen` (the new value in *seen_out, LDS): the return value is then 2, else
+// 1 (released or error).  One workgroup barrier either way.
+__device__ __forceinline__ int grid_wait(KParams& p, unsigned target, int* flag, const unsigned long long* watch = nullptr,
+                                         unsigned long long seen = 0ull, unsigned long long* seen_out = nullptr) {
+  int* code = flag + 2;  // the word after the caller's flag pair (misc[63] for bflag = misc + 61)
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
-    if (lane == 0)
-      __hip_atomic_fetch_add((g_u32*)(p.bars + BAR_STRIDE * (blockIdx.x % BAR_SHARDS)), 1u, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
     const unsigned want = lane < BAR_SHARDS ? target * (unsigned)((p.n_main - lane + BAR_SHARDS - 1) / BAR_SHARDS) : 0u;
     const g_u32* w = (const g_u32*)(lane < BAR_SHARDS ? p.bars + BAR_STRIDE * lane : p.bar);
     const unsigned long long t0 = wall_clock64();
-    int err = 0;
+    int err = 0, res = 1;
     while (true) {
       const unsigned v = lane <= BAR_SHARDS ? __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
       const bool lag = lane < BAR_SHARDS && v < want;
       if (__ballot(lane == BAR_SHARDS && (v & BAR_ERR))) { err = 1; break; }
       if (!__ballot(lag)) break;
+      if (watch != nullptr) {
+        const unsigned long long x = __hip_atomic_load((const g_u64*)watch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (x != seen) {
+          if (lane == 0) *seen_out = x;
+          res = 2;
+          break;
+        }
+      }
       __builtin_amdgcn_s_sleep(1);
       if (wall_clock64() - t0 > (p.h_req != nullptr ? HOST_TIMEOUT_TICKS : BARRIER_TIMEOUT_TICKS)) {
         if (lane == 0) raise_err(p, ERR_TIMEOUT);
@@ -297,9 +313,17 @@ __device__ __forceinline__ bool grid_sync(KParams& p, unsigned& target, int* fla
         break;
       }
     }
-    if (lane == 0) *flag = err;
+    if (lane == 0) {
+      *flag = err;
+      *code = res;
+    }
   }
   __syncthreads();
+  return *code;
+}
+__device__ __forceinline__ bool grid_sync(KParams& p, unsigned& target, int* flag) {
+  grid_arrive(p, target);
+  grid_wait(p, target, flag);
   return *flag != 0;
 }
 
@@ -517,6 +541,7 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
   if (!(staged && p.n_env > 0)) gv_load(p, g, &gv);
   if (threadIdx.x == 0) {
     misc[5] = 0;
+    misc[56] = misc[57] = 0;  // the speculative result this phase A takes (iteration-1 prebuild)
     if (team_out != nullptr) team_out[2] = 0;
   }
   __syncthreads();
@@ -620,6 +645,7 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
     pend_n = gv.npend;
   }
   __syncthreads();
+  unsigned long long cw = 0ull;  // the prebuild confirmation (see below)
   if (!stop) {
     const int et = gi.e[0] + gi.e[1];
     const bool fits = phase_a_fits_lds(gi.n, et) && !(p.variant & 64);  // 64: force global mode (tests)
@@ -637,6 +663,10 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
     staged = fits;
     int err = fits ? env_step<false>(p, gi, gv, area, pend_n, pend_first, lds, was_staged)
                    : env_step<true>(p, gi, gv, area, pend_n, pend_first, lds, false);
+    // the prebuild confirmation: the state after this phase A is exactly the speculative
+    // result published early (one action, taken from it; an end-game below withdraws it)
+    cw = ((unsigned long long)(unsigned)misc[57] << 32) | (unsigned)misc[56];
+    if (err || pend_n != 1) cw = 0ull;
     if (threadIdx.x == 0) {
       gv.npend = 0;
       if (err) raise_err(p, err);
@@ -658,6 +688,7 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
         }
       } else {
         const int k = host_handshake(p, gi, g, gv.npred, 0.f, gv.n_live, misc, true);
+        cw = 0ull;
         if (k > 0) {
           err = fits ? env_step<false>(p, gi, gv, area, k, -1, lds, true)
                      : env_step<true>(p, gi, gv, area, k, -1, lds, false);
@@ -671,6 +702,8 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
   }
   __syncthreads();
   gv_store(p, g, &gv);
+  if (p.pre_cw != nullptr && threadIdx.x == 0)  // every phase A: a stale confirmation must not match
+    __hip_atomic_store((g_u64*)p.pre_cw, cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   return staged;
 }
@@ -782,8 +815,29 @@ __device__ __noinline__ void gather_tile(KParams&, const GraphInfo gi, int it, c
 // step.  Header (ints at S_NBH): off[2][16], cnt[2][16] (alive, per row), rawb[2][16],
 // rawc[2][16] (CSR extent), tot[2].  Returns false when a layer has more than NB_CAP alive
 // entries (the tile then uses gather_tile).
+// Killed-edge set of an iteration-1 prebuild (CSR positions of one layer, open addressing in LDS).
+constexpr int KH_SIZE = 1024;
+__device__ __forceinline__ unsigned kh_slot(int key) { return ((unsigned)key * 2654435761u) >> 22; }
+__device__ __forceinline__ void kh_insert(lds_i32* h, int key) {
+  unsigned i = kh_slot(key);
+  while (true) {
+    const int prev = uf_cas(h, (int)i, -1, key);
+    if (prev == -1 || prev == key) return;
+    i = (i + 1) & (KH_SIZE - 1);
+  }
+}
+__device__ __forceinline__ bool kh_has(const lds_i32* h, int key) {
+  unsigned i = kh_slot(key);
+  while (true) {
+    const int v = h[i];
+    if (v == key) return true;
+    if (v == -1) return false;
+    i = (i + 1) & (KH_SIZE - 1);
+  }
+}
+
 __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const int*, float*,
-                                            unsigned long long* ts, int L) {
+                                            unsigned long long* ts, int L, bool killed_set = false) {
   float* const scr = lds_base() + L_SCR;
 
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
@@ -795,6 +849,9 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
   lds_u16* nbl = (lds_u16*)(uint16_t*)(scr + S_NBL) + l * NB_CAP;
   const int* adj = p.adj[l] + gi.coff[l];
   const uint8_t* ca = p.calive[l] + gi.coff[l];
+  // killed_set: CSR positions killed by the step in flight (an iteration-1 prebuild during phase
+  // A: its write-back may or may not have reached these flags yet) count as dead
+  const lds_i32* kh = killed_set ? (const lds_i32*)(int*)(scr + S_M) : nullptr;
   // rows' CSR begin / extent are in hdr[64 + 16 l + r] / hdr[96 + 16 l + r] (from the live list)
   TSTAMP(60);
   // CSR-extent prefix per row in LDS (a per-thread array indexed at run time would live in
@@ -841,6 +898,7 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
         fl[k] = ldc(ca + posv[k]);
         nbv[k] = adj[posv[k]];
       }
+      if (kh != nullptr && fl[k] && kh_has(kh, posv[k])) fl[k] = 0;
       if (!MD_BOK(nbv[k] >= 0 && nbv[k] < gi.n, 3)) nbv[k] = 0;
     }
   }
@@ -850,7 +908,7 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
   for (int i = i0 + 4; i < i1; ++i) {
     while (pre[r + 1] <= i) ++r;
     const int pos = hdr[64 + l * 16 + r] + (i - pre[r]);
-    keep += ldc(ca + pos) != 0;
+    keep += ldc(ca + pos) != 0 && !(kh != nullptr && kh_has(kh, pos));
   }
   // exclusive scan of keep over the layer's 256 threads
   int incl = keep;
@@ -901,7 +959,7 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
     while (rs < 16 && pre[rs] == i) hdr[l * 16 + rs++] = o;
     while (pre[r + 1] <= i) ++r;
     const int pos = hdr[64 + l * 16 + r] + (i - pre[r]);
-    if (ldc(ca + pos)) {
+    if (ldc(ca + pos) && !(kh != nullptr && kh_has(kh, pos))) {
       if (o < NB_CAP) nbl[o] = (uint16_t)adj[pos];
       ++o;
     }
@@ -913,6 +971,75 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
   if (t < 16) hdr[32 + l * 16 + t] = (t < 15 ? hdr[l * 16 + t + 1] : tot) - hdr[l * 16 + t];
   const int over = __syncthreads_or(tot > NB_CAP);
   return !over;
+}
+
+// Iteration-1 prebuild of tile j, layer L (single-graph rollouts with speculative steps): while
+// phase A applies the speculative result `ew` names (published as soon as phase A knows it takes
+// it), the tile workgroup builds its rows and alive-neighbour lists from that result -- its live
+// list for the rows, the CSR flags with the result's killed edges removed (phase A's write-back
+// of them may be in flight) -- so iteration 1 starts at the gather when phase A confirms the
+// result (pre_cw).  Returns 1 (rows and lists ready), 2 (rows ready, lists over NB_CAP: the
+// per-row gather), 0 (not built: the result's features not published in time, or too many
+// killed edges for the LDS set).
+__device__ __noinline__ int prebuild_lists(KParams&, const GraphInfo gi, int j, int L, unsigned long long ew) {
+  KParams& p = kp();
+  float* const lds = lds_base();
+  float* const scr = lds + L_SCR;
+  int* rows = (int*)(scr + S_ROW);
+  lds_i32* hdr = (lds_i32*)(int*)(scr + S_NBH);
+  int* misc = (int*)(lds + L_MISC);
+  const int slot = (int)(ew & 0xffffu), a = (int)((ew >> 16) & 0xffffu);
+  const unsigned want = (unsigned)(ew >> 32);
+  const int* sl = p.sres + (size_t)slot * p.sres_stride;
+  const int n = gi.n, et = gi.e[0] + gi.e[1];
+  if (threadIdx.x == 0) {
+    const unsigned long long ft_want = ((unsigned long long)(unsigned)a << 32) | want;
+    const unsigned long long t0 = wall_clock64();
+    int ok = 0;
+    while (true) {
+      if (__hip_atomic_load((const g_u64*)(sl + SRES_FEAT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ft_want) {
+        ok = 1;
+        break;
+      }
+      if (wall_clock64() - t0 > 3000 ||  // 30 us: phase A will not wait for it either
+          (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR))
+        break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const unsigned long long dt = __hip_atomic_load((const g_u64*)sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int nd = (int)(dt >> 48);
+    if (ok && ((unsigned)dt != want || (int)((dt >> 32) & 0xffffu) != a || nd > KH_SIZE / 2)) ok = 0;
+    misc[44] = ok;
+    misc[45] = nd;
+    misc[46] = ldc(sl + 12);  // live nodes
+  }
+  __syncthreads();
+  if (!misc[44]) return 0;
+  const int nd = misc[45], nl = misc[46];
+  lds_i32* kh = (lds_i32*)(int*)(scr + S_M);
+  for (int i = threadIdx.x; i < KH_SIZE; i += NTHREADS) kh[i] = -1;
+  if (threadIdx.x < TILE) {
+    // the tile's rows from the result's live list (entries as in phase A's list)
+    const int r = j * TILE + threadIdx.x;
+    const float4 e = ldc4((const float*)(sl + sres_live(et, n)), min(r, n - 1) * 16);
+    const bool ok = r < nl && MD_BOK(__float_as_int(e.x) >= 0 && __float_as_int(e.x) < n && nl <= n, 6);
+    const unsigned c = (unsigned)__float_as_int(e.w);
+    rows[threadIdx.x] = ok ? __float_as_int(e.x) : -1;
+    hdr[64 + threadIdx.x] = ok ? __float_as_int(e.y) : 0;
+    hdr[96 + threadIdx.x] = ok ? (int)(c & 0xffffu) : 0;
+    hdr[64 + 16 + threadIdx.x] = ok ? __float_as_int(e.z) : 0;
+    hdr[96 + 16 + threadIdx.x] = ok ? (int)(c >> 16) : 0;
+  }
+  __syncthreads();
+  // the killed edges of layer L: both CSR positions into the set
+  for (int i = threadIdx.x; i < nd; i += NTHREADS) {
+    const int v = ldc(sl + SRES_HDR + 3 * i), e = v & 0xffff;
+    if ((e < gi.e[0] ? 0 : 1) != L) continue;
+    kh_insert(kh, ldc(sl + SRES_HDR + 3 * i + 1));
+    kh_insert(kh, ldc(sl + SRES_HDR + 3 * i + 2));
+  }
+  __syncthreads();
+  return build_nb_lists(p, gi, rows, scr, nullptr, L, true) ? 1 : 2;
 }
 
 // Gather for one tile from the alive neighbour lists: per batch the layer's 256 threads stage
@@ -1053,7 +1180,10 @@ __device__ __noinline__ void nbc_store(KParams&, int slot, const float*, bool ok
 // Gather of layer L from its alive neighbour list: the 512 threads stage up to 2 * STG_ROWS
 // neighbour rows per batch (register double buffer as in gather_tile2), 32 lanes per row add
 // two features each in CSR order.
-__device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it, const int*, float*, int L) {
+// deg_ovr / hp_ovr (iteration 1 speculated during phase A): the residual degrees and the
+// first-layer rows of the speculative result instead of the graph's arrays.
+__device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it, const int*, float*, int L,
+                                           const int* deg_ovr = nullptr, const float* hp_ovr = nullptr) {
   const int* const rows = (const int*)(lds_base() + L_SCR + S_ROW);
   float* const scr = lds_base() + L_SCR;
 
@@ -1062,12 +1192,12 @@ __device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it,
   const int w = wave_id(), lane = lane_id(), t = threadIdx.x, l = L;
   const int q = lane & 31;
   const int r = 2 * w + (lane >> 5);
-  const int* deg = p.deg[l] + gi.node_off;
+  const int* deg = deg_ovr != nullptr ? deg_ovr : p.deg[l] + gi.node_off;
   const float* hp;
   bool table = false;
   if (it == 1) {
     table = p.node_w == nullptr;
-    hp = table ? first_layer_rows(p, gi, l) : p.h0tab[l] + (size_t)gi.node_off * EMB;
+    hp = table ? (hp_ovr != nullptr ? hp_ovr : first_layer_rows(p, gi, l)) : p.h0tab[l] + (size_t)gi.node_off * EMB;
   } else {
     hp = p.H[l][(it - 2) & 1] + (size_t)gi.node_off * EMB;
   }
@@ -1224,6 +1354,53 @@ __device__ __noinline__ void normalize_tile_split(float*, float*, int L) {
 }
 
 // Node update for one tile: H' = relu([P.P1 | X.P2] . P3) into S_E (normalised separately).
+// Iteration 1 of tile j, layer L speculated during phase A (after prebuild_lists): the gather
+// with the speculative result's degrees and first-layer rows, the update, the normalisation,
+// the partial sums S0 / S1 and the H1 stores -- the layer-split iteration-1 work exactly.  Its
+// stores land where iteration 1's do and nobody reads them before barrier 1; without phase A's
+// confirmation the tile runs iteration 1 again and overwrites them.  Returns false when the
+// first-layer rows of the result's dmax are not precomputed (nothing done).
+__device__ __noinline__ bool spec_iteration1(KParams&, const GraphInfo gi, int j, int L, unsigned long long ew) {
+  KParams& p = kp();
+  float* const lds = lds_base();
+  float* const scr = lds + L_SCR;
+  const int* rows = (const int*)(scr + S_ROW);
+  const int* sl = p.sres + (size_t)(ew & 0xffffu) * p.sres_stride;
+  const int n = gi.n, et = gi.e[0] + gi.e[1];
+  const float* hp = nullptr;
+  if (p.node_w == nullptr) {  // unit cost: rows by degree, from the precomputed table of the result's dmax
+    const int dm = ldc(sl + 13 + L);
+    if (p.h0g == nullptr || (p.variant & 4) || dm < 1 || dm > p.h0g_dm) return false;
+    hp = p.h0g + (h0g_row(dm, 1) - 1) * EMB;
+  }
+  gather_tile2s(p, gi, 1, rows, scr, L, sl + sres_deg(et) + L * n, hp);
+  __syncthreads();
+  update_tile_split(lds + L_W, scr, L);
+  __syncthreads();
+  normalize_tile_split(scr + S_E, scr, L);
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int c = threadIdx.x;
+    const float* ate = scr + S_E + L * 64 * LDT + c * LDT;
+    const float* atx = scr + S_X + L * 64 * LDT + c * LDT;
+    const int nv = tile_rows_valid(rows);
+    const float s_new = col_sum16(ate, nv), s_old = col_sum16(atx, nv);
+    float* sp = p.spart + (size_t)(gi.tile_off + j) * 384;
+    stc(sp + L * 64 + c, s_old);        // S0 (first-layer input)
+    stc(sp + 128 + L * 64 + c, s_new);  // S1
+  }
+  {
+    const int w = wave_id(), lane = lane_id();
+    float* hb = p.H[L][0] + (size_t)gi.node_off * EMB;
+    const int r = 4 * (w & 3) + (lane >> 4), q4 = lane & 15;
+    const int v = rows[r];
+    const float* e = scr + S_E + L * 64 * LDT + 4 * q4 * LDT + r;
+    if (v >= 0 && w < 4) stc4(hb, v * 256 + q4 * 16, make_float4(e[0], e[LDT], e[2 * LDT], e[3 * LDT]));
+  }
+  __syncthreads();
+  return true;
+}
+
 __device__ __noinline__ void update_tile(const float*, float*) {
   const float* const wi = lds_base() + L_W;
   float* const scr = lds_base() + L_SCR;
@@ -2733,6 +2910,12 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
   int pstep = 0;
   bool have_q = false, staged = false;
   const int ng = p.nglist;
+  // iteration-1 prebuild (single graph, layer split, speculative steps on): this workgroup's tile
+  // and layer, the last early word seen and the one its current prebuild used
+  const bool pre_tile = ded && ng == 1 && p.pre_ew != nullptr && !is_env && !is_head &&
+                        2 * ((spec_gi.n + TILE - 1) / TILE) <= p.n_main - 2 * p.n_env;
+  const int pre_j = ((int)blockIdx.x - 2 * p.n_env) >> 1, pre_L = ((int)blockIdx.x - 2 * p.n_env) & 1;
+  unsigned long long pre_seen = 0ull, pre_used = 0ull;
   while (true) {
     // ---------------- phase A
     MD_PROF(0);
@@ -2743,7 +2926,7 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
     } else if (team) {
       // one global-mode graph: workgroup 0 decides the actions, then every workgroup runs the
       // environment step (team_env_step) and workgroup 0 finishes phase A
-      int* tq = (int*)(lds + L_MISC) + 54;
+      int* tq = (int*)(lds + L_MISC) + 40;
       if (blockIdx.x == 0) {
         phase_a(p, p.glist[0], have_q, lds, false, tq);
         if (threadIdx.x == 0) {
@@ -2801,7 +2984,27 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
       if (wdirty) load_weights(lds + L_W, wimg);
     }
     MD_PROF(3);
-    const bool errA = grid_sync(p, target, bflag);
+    // iteration-1 prebuild (p.pre_ew): a single graph's tile workgroups wait at barrier A for
+    // the release or for phase A's early word, and build their iteration-1 rows and lists from
+    // the speculative result it names meanwhile
+    int pre_state = 0;
+    bool errA;
+    if (pre_tile) {
+      grid_arrive(p, target);
+      unsigned long long* seen_out = (unsigned long long*)(lds + L_MISC + 42);
+      while (grid_wait(p, target, bflag, p.pre_ew, pre_seen, seen_out) == 2) {
+        pre_seen = *seen_out;
+        if (pre_state == 0 && pre_seen != 0ull) {
+          pre_state = prebuild_lists(p, spec_gi, pre_j, pre_L, pre_seen);
+          if (pre_state) pre_used = pre_seen;
+          // the whole of iteration 1 too (MD_VARIANT bit 128: lists only)
+          if (pre_state == 1 && !(p.variant & 128) && spec_iteration1(p, spec_gi, pre_j, pre_L, pre_seen)) pre_state = 3;
+        }
+      }
+      errA = *bflag != 0;
+    } else {
+      errA = grid_sync(p, target, bflag);
+    }
     MD_PROF(4);
     if (errA) break;
     // ---------------- tile prefix over the launch's graphs
@@ -2815,6 +3018,11 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
     if (spec) {
       const int r = spec_tile * TILE + threadIdx.x;
       spec_e = ldc4((const float*)(p.live + 4 * (size_t)spec_gi.node_off), min(r, spec_gi.n - 1) * 16);
+    }
+    // phase A's confirmation of the speculative result a prebuild used (same round trip)
+    if (pre_state != 0 && threadIdx.x == 64) {
+      const unsigned long long cw = __hip_atomic_load((const g_u64*)p.pre_cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ((int*)(lds + L_MISC))[47] = cw == pre_used ? pre_state : 0;
     }
     bool waiting = false;
     if (threadIdx.x < ng) {
@@ -2831,6 +3039,9 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
     }
     __syncthreads();
     const int ttot = pref[ng];
+    const int pre_ok = pre_state != 0 ? ((int*)(lds + L_MISC))[47] : 0;  // 1 / 2: use the prebuilt rows (and lists)
+    if (p.prof != nullptr && pre_tile && (int)blockIdx.x == twg0 && threadIdx.x == 0 && pstep < p.prof_cap)
+      p.prof[(size_t)pstep * PROF_SLOTS + 78] = 1 + 10 * pre_state + pre_ok;  // diagnostics: prebuild state
     if (ttot == 0) {
       if (!waiting) break;
       // only graphs waiting for a host answer: one more barrier (nobody writes a GraphVar
@@ -2864,6 +3075,11 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
       int cur = ded ? 0x7fffffff : -1;  // graph-list index whose virtual node / graph head is loaded
       const bool sit = split;  // this iteration runs one layer per workgroup
       for (int t = t0; t < t1; ++t) {
+        // iteration 1 done during phase A from the confirmed speculative result
+        if (it == 1 && pre_ok == 3 && split && t == pre_j && L == pre_L) {
+          nb_ok = true;  // its lists (in LDS) serve iterations 2 and 3
+          continue;
+        }
         const int gl = tile_graph(pref, ng, t);
         const int g = p.glist[gl];
         const GraphInfo gi = p.ginfo[g];
@@ -2905,7 +3121,8 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
           cw = ldc(src + NBC_HDR + (threadIdx.x >> 8) * NBC_LWORDS + (threadIdx.x & 255));
           if (threadIdx.x < 67) ch = ldc(src + threadIdx.x);
         }
-        if (it == 1 || t1 - t0 > 1 || !ded) {
+        const bool prebuilt = it == 1 && (pre_ok == 1 || pre_ok == 2) && split && t == pre_j && L == pre_L;
+        if ((it == 1 || t1 - t0 > 1 || !ded) && !prebuilt) {
           if (threadIdx.x < TILE) {
             const int r = j * TILE + threadIdx.x;
             int nl;
@@ -2958,6 +3175,8 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
               for (int i = 256 + (int)threadIdx.x; i < nw1; i += NTHREADS) words[NBC_LWORDS + i] = ldc(src + NBC_LWORDS + i);
               __syncthreads();
             }
+          } else if (prebuilt) {
+            nb_ok = pre_ok == 1;  // (2: lists over NB_CAP, the per-row gather)
           } else if (it == 1 || t1 - t0 > 1 || !ded) {
             nb_ok = !(p.variant & 16) && build_nb_lists(p, gi, rows, scr, ts, sit ? L : -1);
             if (multi) nbc_store(p, t, scr, nb_ok);

@@ -46,3 +46,10 @@ print("features copied in %d of %d profiled steps" % (int((P[:, 75] > 0).sum()),
 print("hit slots (rank + 1):", np.bincount(rows[:, 70][chk].astype(int), minlength=17).tolist())
 late = us(69, 71)[chk]
 print("waits > 5 us: %d; largest %s" % ((late > 5).sum(), np.round(np.sort(late)[-8:], 1).tolist()))
+pre = P[:, 78]
+pre = pre[pre > 0] - 1
+if len(pre):
+    print("iteration-1 prebuild per step (first tile workgroup): whole iteration used %d, lists used %d, built but not "
+          "confirmed %d, not built %d of %d steps" % (int(np.sum(pre % 10 == 3)), int(np.sum((pre % 10 > 0) & (pre % 10 < 3))),
+                                                  int(np.sum((pre // 10 > 0) & (pre % 10 == 0))), int(np.sum(pre // 10 == 0)),
+                                                  len(pre)), flush=True)

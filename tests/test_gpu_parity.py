@@ -379,3 +379,26 @@ def test_grid_wide_environment_step(monkeypatch):
             e.close()
     for name in ("er100", "gmm200_s7", "er300_dense", "gmm1000_s0"):
         assert out[("64", name)] == out[("66", name)], name
+
+
+def test_iteration1_prebuild_same_rollouts(monkeypatch):
+    """Single-graph rollouts build iteration 1 (rows, alive-neighbour lists, and the whole
+    first message-passing iteration) during phase A from the speculative result phase A
+    announces, and keep it when phase A confirms it.  The rollouts equal the ones without it
+    (MD_VARIANT bit 1) and with lists only (bit 128), and the certified sequences."""
+    out = {}
+    for variant in ("0", "1", "128"):
+        monkeypatch.setenv("MD_VARIANT", variant)
+        e = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
+        try:
+            for name in ("gmm1000_s0", "gmm1000_s1", "gmm1000_s2", "er1000"):
+                z = load_golden(name)
+                e.load_graphs([(int(z["n_nodes"]), z["edges0"], z["edges1"])])
+                e.reset()
+                seq, ranks = e.rollout()[0]
+                out[(variant, name)] = (seq.tolist(), ranks.tolist())
+                assert seq.tolist() == load_cert(name)["gpu_seq"].tolist(), (variant, name)
+        finally:
+            e.close()
+    for name in ("gmm1000_s0", "gmm1000_s1", "gmm1000_s2", "er1000"):
+        assert out[("0", name)] == out[("1", name)] == out[("128", name)], name
