@@ -189,7 +189,7 @@ md_status fail(md_ctx* c, md_status s, const char* fmt, ...) {
   } while (0)
 
 // Control block layout (ints): [0] barrier counter, [1] error word (zeroed before each launch).
-constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_Q = 2, CTL_SPEC = 8, CTL_TEAM = 12, CTL_EXIT = 14, CTL_PRE = 16, CTL_WORDS = 24;
+constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_Q = 2, CTL_SPEC = 8, CTL_TEAM = 12, CTL_EXIT = 14, CTL_PRE = 64, CTL_WORDS = 96;  // CTL_PRE on a line of its own
 constexpr int SPEC_MAX = 32;  // speculative workgroups per launch at most  // CTL_SPEC: u64 request word
 
 Params make_params(md_ctx* c) {
