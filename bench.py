@@ -85,6 +85,10 @@ def parse(argv=None):
                     help="processes of the batch CPU baseline (1 torch thread each; capped by the CPUs available)")
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="launcher/rank/gather plumbing on the CPU: gloo backend, host stub engine, no GPU")
+    ap.add_argument("--rehearse-shared-gpu", action="store_true",
+                    help="N > 1 ranks on fewer GPUs (rank r on GPU r mod the visible count, gloo for the "
+                         "collectives): the multi-rank path with the real engine on a one-GPU box; not a "
+                         "scaling measurement (the line says so)")
     return ap.parse_args(argv)
 
 
@@ -414,7 +418,7 @@ def rank_main(args):
     backend = None
     if world > 1:
         import torch.distributed as tdist
-        if args.cpu_dry_run:
+        if args.cpu_dry_run or args.rehearse_shared_gpu:
             backend = "gloo"
             tdist.init_process_group("gloo")
         else:
@@ -433,8 +437,15 @@ def rank_main(args):
     else:
         from mdcommunity_amd import _lib
 
+        if args.rehearse_shared_gpu:
+            import torch
+            ndev = max(1, torch.cuda.device_count())  # counts devices without initialising one
+            gpu = local % ndev
+        else:
+            gpu = local if world > 1 else 0
+
         def make_engine(weights, cost_mode=_lib.MD_COST_UNIT):
-            return _lib.Engine(weights, device=local if world > 1 else 0, cost_mode=cost_mode)
+            return _lib.Engine(weights, device=gpu, cost_mode=cost_mode)
 
     weights = engine.load_weights(engine.DEFAULT_UNIT)
     eng = make_engine(weights)
@@ -510,7 +521,7 @@ def rank_main(args):
         else:
             # the reference's GMM streams, pair loop on the device (gmm_gpu exact mode: the same
             # graphs as gmm.gmm_pair, outside the timed region)
-            bgraphs = [(args.n,) + e for e in gmm_gpu.gmm_pairs(args.n, range(lo, hi), exact=True, device=local if world > 1 else 0)]
+            bgraphs = [(args.n,) + e for e in gmm_gpu.gmm_pairs(args.n, range(lo, hi), exact=True, device=gpu)]
         beng = make_engine(weights)
         beng.load_graphs(bgraphs)
         run_steps(beng, 1)
@@ -607,6 +618,9 @@ def rank_main(args):
             },
             "rccl_world": dist.get_world_size() if dist is not None else 1,
             "backend": backend,
+            # ranks sharing GPUs (--rehearse-shared-gpu): plumbing rehearsal, the value is not a
+            # scaling figure
+            "rehearsal_shared_gpu": bool(args.rehearse_shared_gpu),
             "audc": audc,
             "audc_match": (audc == golden["audc"]) if have else None,
             # equal to the reference's sequence up to its pinned divergence step (an exact tie or a

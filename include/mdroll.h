@@ -197,6 +197,8 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  * combination is covered by the GPU tests, which check identical rollouts); they select
  * between equivalent execution strategies for A/B measurement and for exercising fallbacks:
  *   MD_VARIANT        bit mask, default 0:
+ *                       1     single-graph rollouts: no iteration-1 prebuild during phase A (the
+ *                             tiles build their rows, lists and iteration 1 after barrier A)
  *                       2     one graph too large for LDS: its environment step on one workgroup
  *                             (and through the work queue) instead of on every workgroup
  *                             (team_env_step); with 64 and MD_ENV_MODE=0 that step also runs
@@ -207,6 +209,8 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *                       16    no neighbour-list cache (every tile rebuilds its lists)
  *                       32    lock-step shared mode instead of the device work queue (> 16 graphs)
  *                       64    environment state in HBM even when it fits in LDS
+ *                       128   iteration-1 prebuild limited to the rows and neighbour lists (the
+ *                             first message-passing iteration runs after barrier A)
  *                       256   push single-item stages instead of running them inline (queue mode)
  *                       512..1536 (bits 9-10 = 1..3)  tiles per queue work item (default 2)
  *                       2048  K2 end-game shortcut off (one forward pass per removal step)
