@@ -88,6 +88,7 @@ struct md_ctx {
   int team_size_req = 0;
   int env_mode = 1;  // 1: dedicated environment workgroups for small batches
   int variant = 0;   // diagnostics knob (MD_VARIANT)
+  int pair_on = 1;   // queue mode: paired tiles (MD_PAIR=0: one tile at a time)
   double last_ms = 0.0;
   int last_launches = 0;
 
@@ -496,6 +497,7 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
     }
   }
   p.qmode = qmode ? 1 : 0;
+  p.qpair = c->pair_on ? 1 : 0;
   p.nglist = ngl;
   p.n_env = n_env;
   p.variant = c->variant;
@@ -662,6 +664,7 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   c->cost_mode = cost_mode;
   if (const char* v = std::getenv("MD_VARIANT")) c->variant = std::atoi(v);
   if (const char* v = std::getenv("MD_ENV_MODE")) c->env_mode = std::atoi(v);
+  if (const char* v = std::getenv("MD_PAIR")) c->pair_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_HOST_HANDSHAKE")) c->host_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_POLL_US")) c->poll_us = std::atoi(v);
   if (const char* v = std::getenv("MD_H0G")) c->h0g_on = std::atoi(v) != 0;

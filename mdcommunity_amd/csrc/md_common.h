@@ -143,6 +143,7 @@ struct Params {
   int prof_cap;                    // steps of 16 timestamp slots available in prof
   int nbc_gstride;                 // queue mode: cache slot = graph slot * nbc_gstride + tile
   int qmode;                       // 1: batch rollout through the device work queue (queue_loop)
+  int qpair;                       // queue mode: a 2-tile item's tiles run jointly (queue_pair; MD_PAIR)
   unsigned* qctl;                  // queue mode: {head ticket, tail ticket, running graphs}
   unsigned long long* qslot;       // queue mode: Q_CAP item slots {ticket + 1, item}
   int* qg;                         // queue mode: per graph slot {tiles done in the stage, tiles}

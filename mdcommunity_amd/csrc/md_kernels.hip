@@ -84,6 +84,29 @@ constexpr int NB_CAP = NB_CAP_ENTRIES;      // alive neighbour entries per layer
 constexpr int S_END = S_NBL + NB_CAP;
 constexpr int STG_ROWS = 68;                // neighbour rows per layer staged per batch ([S_M, S_HID))
 constexpr int L_TOTAL = L_SCR + S_END;      // floats of dynamic LDS per workgroup
+// Paired tiles (queue mode, md_kernels.hip queue_pair): the two tiles of a 2-tile work item run
+// every piece once for their 32 rows.  Transposed blocks [layer][row block][K][LDT] (a row
+// block = one tile's 16 rows, the single-tile layout twice); M aliases P and X once their
+// reads are done, E aliases M, the attention features F the dead X, the hidden layer the
+// dead E, and the gather stages its neighbour rows in P and X before it writes them.  The
+// first tile keeps its lists at S_NBH, the second at P2_NB1.
+constexpr int P2_P = 0;                         // [2][2][64][17] gathered neighbour sums
+constexpr int P2_X = 2 * 2 * 64 * LDT;          // [2][2][64][17] own embedding
+constexpr int P2_M = 0;                         // [2][2][128][17] [P.P1 | X.P2]
+constexpr int P2_E = 0;                         // [2][2][64][17] new embedding / attention output
+constexpr int P2_F = P2_X;                      // [2][2][64][17] tanh features / Q-head input
+constexpr int P2_HID = 0;                       // [2][32][33]
+constexpr int P2_STG = 0;                       // gather staging, [2][STG_ROWS][16] float4
+constexpr int P2_ROW = 2 * P2_X;                // [32] node id per row (int)
+constexpr int P2_RED = P2_ROW + 32;             // [2][32][8] sum-of-squares partials
+constexpr int P2_DOT = P2_RED + 512;            // [32][3] gate dot products, [2][32] gates at +96
+constexpr int P2_Q = P2_DOT + 160;              // [2][32]
+constexpr int P2_FLAG = P2_Q + 64;              // ints: [0] lists cached, [1..2] lists ok, [8..15] wave totals
+constexpr int P2_NB1 = S_NBH - (S_END - S_NBH); // second tile's list region (header + lists)
+static_assert(P2_FLAG + 16 <= P2_NB1, "paired-tile scratch below the second list region");
+static_assert(2 * STG_ROWS * 64 <= 2 * P2_X, "paired gather staging inside P, X");
+static_assert(2 * 32 * 33 <= P2_X, "paired hidden layer inside the E region");
+__device__ __forceinline__ int p2b(int l, int rb, int K) { return (l * 2 + rb) * K * LDT; }
 // phase A uses [L_W, L_TOTAL) (weights are reloaded afterwards)
 constexpr int A_WORDS = L_TOTAL - L_W;
 constexpr int A_TMP_WORDS = 1024;
@@ -836,17 +859,20 @@ __device__ __forceinline__ bool kh_has(const lds_i32* h, int key) {
   }
 }
 
+// nbo: the header and lists at S_NBH + nbo / S_NBL + nbo (a paired tile's second list region),
+// tmpo: 8 words of wave totals at that scratch offset.
 __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const int*, float*,
-                                            unsigned long long* ts, int L, bool killed_set = false) {
+                                            unsigned long long* ts, int L, bool killed_set = false,
+                                            int nbo = 0, int tmpo = S_RED) {
   float* const scr = lds_base() + L_SCR;
 
   KParams& p = kp();  // kernel arguments through the implicit-argument SGPRs (uniform)
   // L < 0: both layers (waves 0-3 layer 0, 4-7 layer 1); L = 0 / 1: that layer, all waves
   const int NT = L < 0 ? 256 : NTHREADS;
   const int w = wave_id(), l = L < 0 ? w >> 2 : L, lane = lane_id(), t = L < 0 ? threadIdx.x & 255 : threadIdx.x;
-  lds_i32* hdr = (lds_i32*)(int*)(scr + S_NBH);
-  lds_i32* tmp = (lds_i32*)(int*)(scr + S_RED);  // [2][4] wave totals
-  lds_u16* nbl = (lds_u16*)(uint16_t*)(scr + S_NBL) + l * NB_CAP;
+  lds_i32* hdr = (lds_i32*)(int*)(scr + S_NBH + nbo);
+  lds_i32* tmp = (lds_i32*)(int*)(scr + tmpo);  // [2][4] wave totals
+  lds_u16* nbl = (lds_u16*)(uint16_t*)(scr + S_NBL + nbo) + l * NB_CAP;
   const int* adj = p.adj[l] + gi.coff[l];
   const uint8_t* ca = p.calive[l] + gi.coff[l];
   // killed_set: CSR positions killed by the step in flight (an iteration-1 prebuild during phase
@@ -1153,13 +1179,13 @@ __device__ __noinline__ void gather_tile2(KParams&, const GraphInfo gi, int it, 
 // Iteration 1 of a workgroup with several tiles: its tiles' alive neighbour lists and
 // headers go to the tile's cache slot (agent-scope stores), so iterations 2 and 3 reload them
 // in one round trip instead of rebuilding them from the CSR flags.
-__device__ __noinline__ void nbc_store(KParams&, int slot, const float*, bool ok) {
+__device__ __noinline__ void nbc_store(KParams&, int slot, const float*, bool ok, int nbo = 0) {
   float* const scr = lds_base() + L_SCR;
 
   KParams& p = kp();
   int* dst = p.nbc + (size_t)slot * NBC_INTS;
-  const lds_i32* hdr = (const lds_i32*)(const int*)(scr + S_NBH);
-  const lds_i32* words = (const lds_i32*)(const int*)(scr + S_NBL);
+  const lds_i32* hdr = (const lds_i32*)(const int*)(scr + S_NBH + nbo);
+  const lds_i32* words = (const lds_i32*)(const int*)(scr + S_NBL + nbo);
   const int t = threadIdx.x;
   if (t < 64) stc(dst + t, hdr[t]);
   else if (t < 66) stc(dst + t, hdr[128 + t - 64]);
@@ -2434,6 +2460,680 @@ __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int
 #undef QTS
 }
 
+// ------------------------------------------------------------------ paired tiles (queue mode)
+// A 2-tile work item (tiles j, j + 1 of one graph) runs header, gather, update, normalisation,
+// sums / stores and the attention + Q head once for its 32 rows instead of twice for 16: one
+// chain of memory and LDS round trips and workgroup barriers per item instead of two, each
+// MFMA weight fragment read from LDS serves both row blocks, and the waves run two
+// independent MFMA chains.  Every element is computed by the same operations in the same
+// order as the single-tile pieces (the MFMA chains per 16-row block, the CSR-order neighbour
+// sums, the torch-order norms, per-tile partial sums and arg-max partials), so results are
+// identical (GPU test: MD_PAIR=0 against the default).
+
+// Gather of both tiles from their alive-neighbour lists: the layer's two lists staged as one
+// concatenated list (batches of STG_ROWS rows per layer, register double buffer as
+// gather_tile2); thread (row r, quad) adds rows r and 16 + r in list (CSR) order.
+__device__ __noinline__ void gather_pair(KParams&, const GraphInfo gi, int it) {
+  float* const scr = lds_base() + L_SCR;
+  const int* const rows = (const int*)(scr + P2_ROW);
+
+  KParams& p = kp();
+  const int w = wave_id(), l = w >> 2, lane = lane_id(), t = threadIdx.x & 255;
+  const int grp = lane >> 4, qd = lane & 15;
+  const int* deg = p.deg[l] + gi.node_off;
+  const float* hp;
+  bool table = false;
+  if (it == 1) {
+    table = p.node_w == nullptr;
+    hp = table ? first_layer_rows(p, gi, l) : p.h0tab[l] + (size_t)gi.node_off * EMB;
+  } else {
+    hp = p.H[l][(it - 2) & 1] + (size_t)gi.node_off * EMB;
+  }
+  const lds_i32* h0 = (const lds_i32*)(const int*)(scr + S_NBH);
+  const lds_i32* h1 = (const lds_i32*)(const int*)(scr + P2_NB1);
+  const lds_u16* nb0 = (const lds_u16*)(const uint16_t*)(scr + S_NBL) + l * NB_CAP;
+  const lds_u16* nb1 = (const lds_u16*)(const uint16_t*)(scr + P2_NB1 + (S_NBL - S_NBH)) + l * NB_CAP;
+  const int r = 4 * (w & 3) + grp;
+  float4 own[2], acc[2];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    own[rb] = make_float4(0.f, 0.f, 0.f, 0.f);
+    acc[rb] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int v = rows[16 * rb + r];
+    if (v >= 0) {
+      const int ov = table ? ldc(deg + v) : v;
+      if (MD_BOK(v < gi.n && ov >= 0 && ov < gi.n, 1)) own[rb] = ldc4(hp, ov * 256 + qd * 16);
+    }
+  }
+  const int t0 = h0[128 + l], totl = t0 + h1[128 + l];
+  const int nbat = (max(h0[128] + h1[128], h0[129] + h1[129]) + STG_ROWS - 1) / STG_ROWS;
+  const int off0 = h0[l * 16 + r], cnt0 = h0[32 + l * 16 + r];
+  const int off1 = t0 + h1[l * 16 + r], cnt1 = h1[32 + l * 16 + r];
+  float4* stg = (float4*)(scr + P2_STG) + l * STG_ROWS * 16;
+  auto issue = [&](int b, float4 (&x)[5], bool (&ok)[5]) {
+    const int base = b * STG_ROWS;
+    int src[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int k = t + 256 * i, row = base + (k >> 4);
+      src[i] = -1;
+      if (b < nbat && k < STG_ROWS * 16 && row < totl) {
+        const int id = row < t0 ? nb0[row] : nb1[row - t0];
+        src[i] = MD_BOK(id < gi.n, 4) ? (table ? ldc(deg + id) : id) : -1;
+        if (!MD_BOK(src[i] < gi.n, 5)) src[i] = -1;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      ok[i] = src[i] >= 0;
+      if (ok[i]) x[i] = ldc4(hp, src[i] * 256 + ((t + 256 * i) & 15) * 16);
+    }
+  };
+  auto add_range = [&](float4& a, int lo, int hi, int base) {
+    int k = lo;
+    for (; k + 8 <= hi; k += 8) {
+      float4 y[8];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) y[jj] = stg[(k + jj - base) * 16 + qd];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        a.x = a.x + y[jj].x;
+        a.y = a.y + y[jj].y;
+        a.z = a.z + y[jj].z;
+        a.w = a.w + y[jj].w;
+      }
+    }
+    for (; k < hi; ++k) {
+      const float4 y = stg[(k - base) * 16 + qd];
+      a.x = a.x + y.x;
+      a.y = a.y + y.y;
+      a.z = a.z + y.z;
+      a.w = a.w + y.w;
+    }
+  };
+  auto consume = [&](int b, const float4 (&x)[5], const bool (&ok)[5]) {
+    const int base = b * STG_ROWS;
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+      if (ok[i]) stg[t + 256 * i] = x[i];
+    __syncthreads();
+    add_range(acc[0], max(off0, base), min(off0 + cnt0, base + STG_ROWS), base);
+    add_range(acc[1], max(off1, base), min(off1 + cnt1, base + STG_ROWS), base);
+    __syncthreads();
+  };
+  float4 xa[5], xb[5];
+  bool oka[5], okb[5];
+  if (nbat > 0) issue(0, xa, oka);
+  for (int b = 0; b < nbat; b += 2) {
+    issue(b + 1, xb, okb);
+    consume(b, xa, oka);
+    if (b + 1 >= nbat) break;
+    issue(b + 2, xa, oka);
+    consume(b + 1, xb, okb);
+  }
+  const int c = 4 * qd;
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    float* atp = scr + P2_P + p2b(l, rb, 64);
+    float* atx = scr + P2_X + p2b(l, rb, 64);
+    atp[(c + 0) * LDT + r] = acc[rb].x;
+    atp[(c + 1) * LDT + r] = acc[rb].y;
+    atp[(c + 2) * LDT + r] = acc[rb].z;
+    atp[(c + 3) * LDT + r] = acc[rb].w;
+    atx[(c + 0) * LDT + r] = own[rb].x;
+    atx[(c + 1) * LDT + r] = own[rb].y;
+    atx[(c + 2) * LDT + r] = own[rb].z;
+    atx[(c + 3) * LDT + r] = own[rb].w;
+  }
+}
+
+// Gather of both tiles straight from the CSR (a list over NB_CAP entries): gather_tile per row
+// block.
+__device__ __noinline__ void gather_pair_csr(KParams&, const GraphInfo gi, int it) {
+  float* const scr = lds_base() + L_SCR;
+  const int* const rows = (const int*)(scr + P2_ROW);
+
+  KParams& p = kp();
+  const int w = wave_id(), l = w >> 2, lane = lane_id();
+  const int grp = lane >> 4, qd = lane & 15;
+  const int* rp = p.rowptr[l] + gi.roff[l];
+  const int* adj = p.adj[l] + gi.coff[l];
+  const uint8_t* ca = p.calive[l] + gi.coff[l];
+  const int* deg = p.deg[l] + gi.node_off;
+  const float* hp;
+  bool table = false;
+  if (it == 1) {
+    table = p.node_w == nullptr;
+    hp = table ? first_layer_rows(p, gi, l) : p.h0tab[l] + (size_t)gi.node_off * EMB;
+  } else {
+    hp = p.H[l][(it - 2) & 1] + (size_t)gi.node_off * EMB;
+  }
+  const int r = 4 * (w & 3) + grp;
+  for (int rb = 0; rb < 2; ++rb) {
+    const int v = rows[16 * rb + r];
+    int rbeg = 0, rend = 0;
+    float4 own = {0.f, 0.f, 0.f, 0.f}, acc = {0.f, 0.f, 0.f, 0.f};
+    if (v >= 0) {
+      rbeg = rp[v];
+      rend = rp[v + 1];
+      const int ov = table ? ldc(deg + v) : v;
+      if (MD_BOK(v < gi.n && ov >= 0 && ov < gi.n, 1)) own = ldc4(hp, ov * 256 + qd * 16);
+    }
+    int nch = (rend - rbeg + 15) >> 4;
+    nch = max(nch, __shfl_xor(nch, 16, 64));
+    nch = max(nch, __shfl_xor(nch, 32, 64));
+    for (int ch = 0; ch < nch; ++ch) {
+      const int e = rbeg + 16 * ch + qd;
+      int nb = -1;
+      if (e < rend && ldc(ca + e)) nb = adj[e];
+      if (table && nb >= 0) nb = ldc(deg + nb);
+      const unsigned long long m = __ballot(nb >= 0);
+      unsigned gm = (unsigned)(m >> (16 * grp)) & 0xFFFFu;
+      while (__any(gm != 0)) {
+        int jx[4] = {-1, -1, -1, -1};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (gm) {
+            const int b = __builtin_ctz(gm);
+            gm &= gm - 1;
+            jx[k] = b;
+          }
+        }
+        int src[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) src[k] = __shfl(nb, 16 * grp + (jx[k] < 0 ? 0 : jx[k]), 64);
+        float4 x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = jx[k] >= 0 ? ldc4(hp, src[k] * 256 + qd * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (jx[k] >= 0) {
+            acc.x = acc.x + x[k].x;
+            acc.y = acc.y + x[k].y;
+            acc.z = acc.z + x[k].z;
+            acc.w = acc.w + x[k].w;
+          }
+        }
+      }
+    }
+    float* atp = scr + P2_P + p2b(l, rb, 64);
+    float* atx = scr + P2_X + p2b(l, rb, 64);
+    const int c = 4 * qd;
+    atp[(c + 0) * LDT + r] = acc.x;
+    atp[(c + 1) * LDT + r] = acc.y;
+    atp[(c + 2) * LDT + r] = acc.z;
+    atp[(c + 3) * LDT + r] = acc.w;
+    atx[(c + 0) * LDT + r] = own.x;
+    atx[(c + 1) * LDT + r] = own.y;
+    atx[(c + 2) * LDT + r] = own.z;
+    atx[(c + 3) * LDT + r] = own.w;
+  }
+}
+
+// Node update of both row blocks: wave (layer, column block) runs the chains of update_tile for
+// each block on one set of weight fragments (four independent chains, then two).
+__device__ __noinline__ void update_pair() {
+  const float* const wi = lds_base() + L_W;
+  float* const scr = lds_base() + L_SCR;
+
+  const int w = wave_id(), l = w >> 2, cb = w & 3, lane = lane_id();
+  const int ar = lane & 15, ak = lane >> 4;
+  const float* p1 = wi + W_IP1 + cb * 16 * 64;
+  const float* p2 = wi + W_IP2 + cb * 16 * 64;
+  const float* p3 = wi + W_IP3 + cb * 32 * 64;
+  const int col = 16 * cb + ar;
+  f4 a1[2], a2[2];
+  {
+    float xa[2][16], xb[2][16], wa[16], wb[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        xa[rb][s] = scr[P2_P + p2b(l, rb, 64) + (4 * s + ak) * LDT + ar];
+        xb[rb][s] = scr[P2_X + p2b(l, rb, 64) + (4 * s + ak) * LDT + ar];
+      }
+      wa[s] = p1[s * 64 + lane];
+      wb[s] = p2[s * 64 + lane];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      a1[rb] = f4{0.f, 0.f, 0.f, 0.f};
+      a2[rb] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        a1[rb] = mfma16(xa[rb][s], wa[s], a1[rb]);
+        a2[rb] = mfma16(xb[rb][s], wb[s], a2[rb]);
+      }
+    }
+  }
+  __syncthreads();  // every P / X read done: M overwrites them
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    float* atm = scr + P2_M + p2b(l, rb, 128);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      atm[col * LDT + 4 * ak + r] = a1[rb][r];
+      atm[(64 + col) * LDT + 4 * ak + r] = a2[rb][r];
+    }
+  }
+  __syncthreads();
+  f4 a3[2];
+  {
+    float xm[2][32], wc[32];
+#pragma unroll
+    for (int s = 0; s < 32; ++s) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) xm[rb][s] = scr[P2_M + p2b(l, rb, 128) + (4 * s + ak) * LDT + ar];
+      wc[s] = p3[s * 64 + lane];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) a3[rb] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 32; ++s) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) a3[rb] = mfma16(xm[rb][s], wc[s], a3[rb]);
+    }
+  }
+  __syncthreads();  // every M read done: E overwrites it
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    float* ate = scr + P2_E + p2b(l, rb, 64);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ate[col * LDT + 4 * ak + r] = fmaxf(a3[rb][r], 0.f);
+  }
+}
+
+// Row normalisation of both blocks of E in place (normalize_tile's order).
+__device__ __noinline__ void normalize_pair() {
+  float* const scr = lds_base() + L_SCR;
+  float* red = scr + P2_RED;
+  {
+    const int t = threadIdx.x, l = t >> 8, row = (t >> 3) & 31, jj = t & 7;
+    const float* a = scr + P2_E + p2b(l, row >> 4, 64);
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float v = a[(8 * i + jj) * LDT + (row & 15)];
+      acc = fmaf(v, v, acc);
+    }
+    red[(l * 32 + row) * 8 + jj] = acc;
+  }
+  __syncthreads();
+  const int w = wave_id(), l = w >> 2, cb = w & 3, lane = lane_id();
+  const int col = 16 * cb + (lane & 15), rq = lane >> 4;
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    float* a = scr + P2_E + p2b(l, rb, 64);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * rq + r;
+      const float den = fmaxf(sqrtf(sumsq8_finish(red + (l * 32 + 16 * rb + row) * 8)), 1e-12f);
+      a[col * LDT + row] = a[col * LDT + row] / den;
+    }
+  }
+}
+
+// Iteration 3 of both tiles: attention_q_tile's pieces for 32 rows; the arg-max partials stay
+// per tile (tiles j, j + 1).
+__device__ __noinline__ void attention_q_pair(KParams&, const GraphInfo gi, int g, int j) {
+  float* const lds = lds_base();
+  float* const scr = lds + L_SCR;
+  const int* const rows = (const int*)(scr + P2_ROW);
+
+  KParams& p = kp();
+  const float* wi = lds + L_W;
+#ifdef MD_QPROF
+  unsigned long long* qa = p.prof != nullptr && (p.variant & 8) ? p.prof + 88 : nullptr;
+  unsigned long long tqa = qa != nullptr ? wall_clock64() : 0ull;
+#define QATS(k)                                                   \
+  do {                                                            \
+    if (qa != nullptr && threadIdx.x == 0) {                      \
+      const unsigned long long now_ = wall_clock64();             \
+      atomicAdd(qa + (k), now_ - tqa);                            \
+      tqa = now_;                                                 \
+    }                                                             \
+  } while (0)
+#else
+#define QATS(k) do {} while (0)
+#endif
+  const int w = wave_id(), l = w >> 2, cb = w & 3, lane = lane_id();
+  const int ar = lane & 15, ak = lane >> 4;
+  const int col = 16 * cb + ar;
+  {
+    // F_l = tanh(E_l . T + b)
+    const float* tf = wi + W_IT + cb * 16 * 64;
+    float xa[2][16], wa[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) xa[rb][s] = scr[P2_E + p2b(l, rb, 64) + (4 * s + ak) * LDT + ar];
+      wa[s] = tf[s * 64 + lane];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    f4 a[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) a[rb] = mfma16(xa[rb][s], wa[s], a[rb]);
+    }
+    const float b = wi[W_ITB + col];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      float* atf = scr + P2_F + p2b(l, rb, 64);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) atf[col * LDT + 4 * ak + r] = tanhf(a[rb][r] + b);
+    }
+  }
+  __syncthreads();
+  QATS(0);
+  float* dot = scr + P2_DOT;
+  float* gate = dot + 96;  // [2][32] weight of the other layer per (layer, row)
+  if (w < 2) {
+    // wave rb: the gate dot products and gates of row block rb
+    const int rb = w;
+    if (lane < 48) {
+      const int row = lane & 15, kind = lane >> 4;  // 0: F0F0, 1: F1F1, 2: F0F1
+      const float* fa = scr + P2_F + p2b(kind == 1 ? 1 : 0, rb, 64);
+      const float* fb = scr + P2_F + p2b(kind == 0 ? 0 : 1, rb, 64);
+      float a = 0.f;
+#pragma unroll
+      for (int h = 0; h < 64; h += 32) {
+        float xa[32], xb[32], ww[32];
+#pragma unroll
+        for (int c = 0; c < 32; ++c) {
+          xa[c] = fa[(h + c) * LDT + row];
+          xb[c] = fb[(h + c) * LDT + row];
+          ww[c] = wi[W_ILW + h + c];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = 0; c < 32; ++c) a = fmaf(xa[c] * xb[c], ww[c], a);
+      }
+      dot[(16 * rb + row) * 3 + kind] = a;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are done
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 32) {
+      const int ll = lane >> 4, row = 16 * rb + (lane & 15);
+      gate[ll * 32 + row] = other_gate(ll, dot[row * 3 + 0], dot[row * 3 + 1], dot[row * 3 + 2], wi[W_ILB]);
+    }
+  }
+  __syncthreads();
+  QATS(1);
+  {
+    // mix E_l = F_l + gate * F_other fused into the first pass of the row normalisation
+    float* red = scr + P2_RED;
+    const int t = threadIdx.x;
+    const int ll = t >> 8, row = (t >> 3) & 31, jj = t & 7, rb = row >> 4, rr = row & 15;
+    const float* f = scr + P2_F + p2b(ll, rb, 64);
+    const float* o = scr + P2_F + p2b(1 - ll, rb, 64);
+    float* e = scr + P2_E + p2b(ll, rb, 64);
+    const float gt = gate[ll * 32 + row];
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = 8 * i + jj;
+      const float v = f[c * LDT + rr] + gt * o[c * LDT + rr];
+      e[c * LDT + rr] = v;
+      acc = fmaf(v, v, acc);
+    }
+    red[(ll * 32 + row) * 8 + jj] = acc;
+    __syncthreads();
+#pragma unroll
+    for (int b2 = 0; b2 < 2; ++b2) {
+      float* at = scr + P2_E + p2b(l, b2, 64);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rw = 4 * ak + r;
+        const float den = fmaxf(sqrtf(sumsq8_finish(red + (l * 32 + 16 * b2 + rw) * 8)), 1e-12f);
+        at[col * LDT + rw] = at[col * LDT + rw] / den;
+      }
+    }
+  }
+  __syncthreads();
+  QATS(2);
+  head_receive(p, lds, g, 1ull);
+  QATS(3);
+  {
+    // e[a] = sum_b (h[a] * y[b]) * cp[b] (attention_q_tile's chains, eight per thread)
+    const int ll = threadIdx.x >> 8, t = threadIdx.x & 255;
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    f2v h[4], acc[4];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = t + 256 * k, row = idx >> 6, a = idx & 63;
+      h[k >> 1][k & 1] = scr[P2_E + p2b(ll, row >> 4, 64) + a * LDT + (row & 15)];
+      acc[k >> 1][k & 1] = 0.f;
+    }
+    const float4* y4 = (const float4*)(lds + L_YS + ll * 64);
+    const float4* c4 = (const float4*)(wi + W_ICP);
+#pragma unroll 4
+    for (int b4 = 0; b4 < 16; ++b4) {
+      const float4 yv = y4[b4], cv = c4[b4];
+      const float ys[4] = {yv.x, yv.y, yv.z, yv.w}, cs[4] = {cv.x, cv.y, cv.z, cv.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f2v yy = {ys[q], ys[q]}, cc = {cs[q], cs[q]};
+#pragma unroll
+        for (int k2 = 0; k2 < 4; ++k2) acc[k2] = __builtin_elementwise_fma(h[k2] * yy, cc, acc[k2]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = t + 256 * k, row = idx >> 6, a = idx & 63;
+      scr[P2_F + p2b(ll, row >> 4, 64) + a * LDT + (row & 15)] = acc[k >> 1][k & 1];
+    }
+  }
+  __syncthreads();
+  QATS(4);
+  float* hid = scr + P2_HID;
+  if (cb < 2) {
+    const float* hf = wi + W_IH1 + cb * 16 * 64;
+    float xa[2][16], wa[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) xa[rb][s] = scr[P2_F + p2b(l, rb, 64) + (4 * s + ak) * LDT + ar];
+      wa[s] = hf[s * 64 + lane];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    f4 a[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) a[rb] = mfma16(xa[rb][s], wa[s], a[rb]);
+    }
+    // hid overwrites the (dead) E region only, not the F being read
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hid[(l * 32 + 16 * rb + 4 * ak + r) * 33 + col] = fmaxf(a[rb][r], 0.f);
+  }
+  __syncthreads();
+  float* ql = scr + P2_Q;
+  if (threadIdx.x < 64) {
+    const int ll = threadIdx.x >> 5, row = threadIdx.x & 31;
+    const float* gs = lds + L_GS;
+    float a = fma_chain<32>(0.f, 0, [&](int k) { return hid[(ll * 32 + row) * 33 + k]; },
+                            [&](int k) { return wi[W_IW2 + k]; });
+    for (int k = 0; k < 4; ++k) a = fmaf(gs[4 + ll * 4 + k], wi[W_IW2 + 32 + k], a);
+    ql[ll * 32 + row] = a;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  QATS(5);
+  if (threadIdx.x < 64) {
+    // q = w0 * Q0 + w1 * Q1 per row, and each tile's arg-max partial by a 16-lane butterfly
+    const float* gs = lds + L_GS;
+    const int ln = threadIdx.x;
+    float bm = NEG_INF, bs = NEG_INF;
+    int bi = 0x7fffffff, bc = 0;
+    if (ln < 32) {
+      const int v = rows[ln];
+      if (v >= 0) {
+        const float qq = gs[0] * ql[ln] + gs[1] * ql[32 + ln];
+        stc(p.q + gi.node_off + v, qq);
+        if (p.qspec != nullptr)
+          stc(p.qspec + (size_t)(((const int*)(lds + L_MISC))[60] & 1) * p.qspec_n + gi.node_off + v, qq);
+        bm = qq;
+        bi = v;
+        bc = 1;
+      }
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      const float m2 = __shfl_xor(bm, o, 64), s2 = __shfl_xor(bs, o, 64);
+      const int i2 = __shfl_xor(bi, o, 64), c2 = __shfl_xor(bc, o, 64);
+      if (c2 != 0) argmax_combine(bm, bs, bi, bc, m2, s2, i2, c2);
+    }
+    // (stc4 takes a wave-uniform base: the tile goes in the byte offset)
+    if (ln == 0 || ln == 16)
+      stc4(p.apart + (size_t)(gi.tile_off + j) * 4, (ln >> 4) * 16, make_float4(bm, bs, __int_as_float(bi), __int_as_float(bc)));
+  }
+  __syncthreads();
+  QATS(6);
+#undef QATS
+}
+
+// Queue work item of tiles j and j + 1 of graph g (slot gl), iteration it: queue_tile for both
+// at once.
+__device__ __noinline__ void queue_pair(KParams&, float* lds, int g, int gl, int it, int j) {
+  KParams& p = kp();
+  float* scr = lds + L_SCR;
+  int* rows = (int*)(scr + P2_ROW);
+  const GraphInfo gi = p.ginfo[g];
+  lds_i32* flag = (lds_i32*)(int*)(scr + P2_FLAG);
+#ifdef MD_QPROF
+  unsigned long long* qd = p.prof != nullptr && (p.variant & 8) ? p.prof + 20 + 8 * (it - 1) : nullptr;
+  unsigned long long tqd = qd != nullptr ? wall_clock64() : 0ull;
+#else
+  constexpr unsigned long long* qd = nullptr;
+  unsigned long long tqd = 0ull;
+#endif
+#define QTS(k)                                                    \
+  do {                                                            \
+    if (qd != nullptr && threadIdx.x == 0) {                      \
+      const unsigned long long now_ = wall_clock64();             \
+      atomicAdd(qd + (k), now_ - tqd);                            \
+      tqd = now_;                                                 \
+    }                                                             \
+  } while (0)
+  const int t = threadIdx.x;
+  const int slot0 = gl * p.nbc_gstride + j;
+  const int nbo[2] = {0, P2_NB1 - S_NBH};
+  bool cacheable[2], want[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    cacheable[b] = slot0 + b < p.nbc_slots && !(p.variant & 16);
+    want[b] = cacheable[b] && (it > 1 || !(p.variant & 4096));
+  }
+  // both tiles' cached lists (first 256 words per layer), headers and the "built" flag in one
+  // round trip, with the rows from the live list
+  int cw[2] = {0, 0}, ch = 0, built = 0;
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+    if (want[b]) cw[b] = ldc(p.nbc + (size_t)(slot0 + b) * NBC_INTS + NBC_HDR + (t >> 8) * NBC_LWORDS + (t & 255));
+  const int hb = t >> 7, hi = t & 127;
+  if (hb < 2 && hi < 67 && want[hb]) ch = ldc(p.nbc + (size_t)(slot0 + hb) * NBC_INTS + hi);
+  if (it == 1 && t == 67 && (want[0] || want[1])) built = ldc(p.qg + 2 * G_CAP + gl);
+  if (t < 2 * TILE) {
+    const int r = j * TILE + t;
+    lds_i32* hdr = (lds_i32*)(int*)(scr + S_NBH + nbo[t >> 4]);
+    const int rr = t & 15;
+    const int nl = ldc(&p.gvar[g].n_live);
+    const float4 e = ldc4((const float*)(p.live + 4 * (size_t)gi.node_off), min(r, gi.n - 1) * 16);
+    const bool ok = r < nl && MD_BOK(__float_as_int(e.x) >= 0 && __float_as_int(e.x) < gi.n && nl <= gi.n, 6);
+    const unsigned c = (unsigned)__float_as_int(e.w);
+    rows[t] = ok ? __float_as_int(e.x) : -1;
+    hdr[64 + rr] = ok ? __float_as_int(e.y) : 0;
+    hdr[96 + rr] = ok ? (int)(c & 0xffffu) : 0;
+    hdr[64 + 16 + rr] = ok ? __float_as_int(e.z) : 0;
+    hdr[96 + 16 + rr] = ok ? (int)(c >> 16) : 0;
+  }
+  if (t == 67) flag[0] = it > 1 || built;
+  __syncthreads();
+  bool cached[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) cached[b] = want[b] && flag[0] != 0;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    if (cached[b]) {
+      lds_i32* hdr = (lds_i32*)(int*)(scr + S_NBH + nbo[b]);
+      ((lds_i32*)(int*)(scr + S_NBL + nbo[b]))[(t >> 8) * NBC_LWORDS + (t & 255)] = cw[b];
+      if (hb == b) {
+        if (hi < 64) hdr[hi] = ch;
+        else if (hi < 66) hdr[128 + hi - 64] = ch;
+        else if (hi == 66) flag[1 + b] = ch;
+      }
+    }
+  }
+  __syncthreads();
+  QTS(0);
+  bool nb_ok[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    if (cached[b]) {
+      nb_ok[b] = flag[1 + b] != 0;
+      const lds_i32* hdr = (const lds_i32*)(const int*)(scr + S_NBH + nbo[b]);
+      const int nw0 = (hdr[128] + 1) >> 1, nw1 = (hdr[129] + 1) >> 1;
+      if (nb_ok[b] && (nw0 > 256 || nw1 > 256)) {
+        const int* src = p.nbc + (size_t)(slot0 + b) * NBC_INTS + NBC_HDR;
+        lds_i32* words = (lds_i32*)(int*)(scr + S_NBL + nbo[b]);
+        for (int i = 256 + t; i < nw0; i += NTHREADS) words[i] = ldc(src + i);
+        for (int i = 256 + t; i < nw1; i += NTHREADS) words[NBC_LWORDS + i] = ldc(src + NBC_LWORDS + i);
+        __syncthreads();
+      }
+    } else {
+      nb_ok[b] = !(p.variant & 16) && build_nb_lists(p, gi, nullptr, nullptr, nullptr, -1, false, nbo[b], P2_FLAG + 8);
+      if (cacheable[b]) nbc_store(p, slot0 + b, scr, nb_ok[b], nbo[b]);
+    }
+  }
+  QTS(1);
+  if (nb_ok[0] && nb_ok[1]) gather_pair(p, gi, it);
+  else gather_pair_csr(p, gi, it);
+  __syncthreads();
+  if (it == 1 && t < 256) {
+    // S0 (first-layer input) partial sums before the update overwrites X
+    const int b = t >> 7, l = (t >> 6) & 1, c = t & 63;
+    const float s_old = col_sum16(scr + P2_X + p2b(l, b, 64) + c * LDT, tile_rows_valid(rows + 16 * b));
+    stc(p.spart + (size_t)(gi.tile_off + j + b) * 384 + l * 64 + c, s_old);
+  }
+  QTS(2);
+  update_pair();
+  __syncthreads();
+  QTS(3);
+  normalize_pair();
+  __syncthreads();
+  QTS(4);
+  if (it < 3) {
+    if (t < 256) {
+      const int b = t >> 7, l = (t >> 6) & 1, c = t & 63;
+      const float s_new = col_sum16(scr + P2_E + p2b(l, b, 64) + c * LDT, tile_rows_valid(rows + 16 * b));
+      stc(p.spart + (size_t)(gi.tile_off + j + b) * 384 + (it == 1 ? 128 : 256) + l * 64 + c, s_new);  // S1 / S2
+    }
+    const int w = wave_id(), l = w >> 2, lane = lane_id();
+    float* hbuf = p.H[l][(it - 1) & 1] + (size_t)gi.node_off * EMB;
+    const int r = 4 * (w & 3) + (lane >> 4), q4 = lane & 15;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int v = rows[16 * rb + r];
+      const float* e = scr + P2_E + p2b(l, rb, 64) + 4 * q4 * LDT + r;
+      if (v >= 0) stc4(hbuf, v * 256 + q4 * 16, make_float4(e[0], e[LDT], e[2 * LDT], e[3 * LDT]));
+    }
+    __syncthreads();
+  }
+  QTS(5);
+  if (it == 3) attention_q_pair(p, gi, g, j);
+  QTS(6);
+#undef QTS
+}
+
 // Virtual-node chain Y1..Y3 from the tile partial sums S0..S2 and the graph head of graph g,
 // published as tagged granules (tag 1) for its iteration-3 tiles.
 // Virtual-node chain of graph g in two items: part 1 (Y1, Y2 from the iteration-1 partial sums
@@ -2605,7 +3305,10 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
     if (kind == QK_TILE || (kind == QK_VN && it == 1)) {
       // a task of a stage: iteration-1/2/3 tiles; stage 2 also counts virtual-node part 1
       if (kind == QK_TILE) {
-        for (int k = 0; k <= q_item_extra(item); ++k) queue_tile(p, lds, g, gl, it, j + k);
+        const int ex = q_item_extra(item);
+        if (ex == 1 && p.qpair) queue_pair(p, lds, g, gl, it, j);
+        else
+          for (int k = 0; k <= ex; ++k) queue_tile(p, lds, g, gl, it, j + k);
       } else {
         queue_vn(p, lds, g, 1);
       }

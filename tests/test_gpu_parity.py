@@ -402,3 +402,44 @@ def test_iteration1_prebuild_same_rollouts(monkeypatch):
             e.close()
     for name in ("gmm1000_s0", "gmm1000_s1", "gmm1000_s2", "er1000"):
         assert out[("0", name)] == out[("1", name)] == out[("128", name)], name
+
+
+def _hub_layer(n, hub, hub_deg, rng):
+    m = 2 * n
+    u = rng.integers(0, n, size=3 * m)
+    v = rng.integers(0, n, size=3 * m)
+    e = sorted({(min(a, b), max(a, b)) for a, b in zip(u.tolist(), v.tolist()) if a != b})[:m]
+    nb = rng.choice(np.setdiff1d(np.arange(n), [hub]), size=hub_deg, replace=False)
+    return np.array(sorted(set(e) | {(min(hub, int(x)), max(hub, int(x))) for x in nb}), np.int32)
+
+
+@pytest.mark.parametrize("cost", ["unit", "degree"])
+def test_paired_tiles_match_single_tiles(monkeypatch, cost):
+    """Queue mode runs the two tiles of a 2-tile work item jointly (queue_pair: 32 rows per
+    piece); MD_PAIR=0 runs them one after the other (queue_tile).  Same rollouts, for unit and
+    degree cost, on a batch with a hub graph whose tiles overflow the LDS neighbour lists
+    (the per-row CSR gather) and with odd tile counts (a last single-tile item)."""
+    rng = np.random.default_rng(5)
+    hub = (3000, _hub_layer(3000, 3, 2400, rng), _hub_layer(3000, 3, 2400, rng))
+    names = ["gmm200_s7", "er100", "er300_dense", "gmm1000_s1"]
+    graphs = [(int(z["n_nodes"]), z["edges0"], z["edges1"]) for z in map(load_golden, names)]
+    batch = [hub] + [graphs[i % len(graphs)] for i in range(19)]
+    w, mode = ((engine.load_weights(engine.DEFAULT_UNIT), _lib.MD_COST_UNIT) if cost == "unit" else
+               (engine.load_weights(engine.DEFAULT_DEGREE), _lib.MD_COST_DEGREE))
+    node_w = None
+    if cost == "degree":
+        from mdcommunity_amd import graph as mgraph
+        node_w = mgraph.node_weight_array([mgraph.Graph_test.from_edges(n, e0, e1) for n, e0, e1 in batch])
+    out = {}
+    for pair in ("0", "1"):
+        monkeypatch.setenv("MD_PAIR", pair)
+        e = _lib.Engine(w, cost_mode=mode)
+        try:
+            e.load_graphs(batch, node_w=node_w)
+            e.reset()
+            out[pair] = [(s.tolist(), r.tolist()) for s, r in e.rollout()]
+        finally:
+            e.close()
+    assert len(out["1"]) == len(batch)
+    for i, (a, b) in enumerate(zip(out["0"], out["1"])):
+        assert a == b, i
