@@ -2695,7 +2695,6 @@ __device__ __noinline__ void update_pair() {
       wa[s] = p1[s * 64 + lane];
       wb[s] = p2[s * 64 + lane];
     }
-    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
       a1[rb] = f4{0.f, 0.f, 0.f, 0.f};
@@ -2709,6 +2708,15 @@ __device__ __noinline__ void update_pair() {
         a2[rb] = mfma16(xb[rb][s], wb[s], a2[rb]);
       }
     }
+    // the LDS reads of k-steps s + 4.. issue under the MFMAs of step s (-0.9 ms per 256-graph
+    // launch against all reads first)
+    __builtin_amdgcn_sched_group_barrier(0x100, 24, 0);
+#pragma unroll
+    for (int s = 0; s < 12; ++s) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
   }
   __syncthreads();  // every P / X read done: M overwrites them
 #pragma unroll
@@ -2730,7 +2738,6 @@ __device__ __noinline__ void update_pair() {
       for (int rb = 0; rb < 2; ++rb) xm[rb][s] = scr[P2_M + p2b(l, rb, 128) + (4 * s + ak) * LDT + ar];
       wc[s] = p3[s * 64 + lane];
     }
-    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) a3[rb] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -2738,6 +2745,13 @@ __device__ __noinline__ void update_pair() {
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) a3[rb] = mfma16(xm[rb][s], wc[s], a3[rb]);
     }
+    __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+#pragma unroll
+    for (int s = 0; s < 28; ++s) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
   }
   __syncthreads();  // every M read done: E overwrites it
 #pragma unroll

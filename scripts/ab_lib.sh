@@ -1,8 +1,9 @@
-# A/B of two builds on one box: MD_LIB=<alt .so> vs the in-tree libmdroll.so, alternating.
-set -e
-ALT=${1:-mdcommunity_amd/libmdroll_ab.so}
-NB=${2:-256}
+# A/B of two library builds on the batch timer, alternating: bash scripts/ab_lib.sh A.so B.so [graphs]
+set -o pipefail
+mkdir -p gpurun_out
 for r in 1 2; do
-  echo "in-tree:"; timeout -k 10 60 python scripts/batch_prof.py $NB | grep "^batch"
-  echo "alt ($ALT):"; MD_LIB=$ALT timeout -k 10 60 python scripts/batch_prof.py $NB | grep "^batch"
+  for lib in "$1" "$2"; do
+    echo "== $lib" >> gpurun_out/ab_lib.log
+    MD_LIB=$PWD/$lib timeout -k 10 100 python -u scripts/batch_time.py ${3:-256} 7 >> gpurun_out/ab_lib.log 2>&1 || exit 1
+  done
 done

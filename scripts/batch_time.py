@@ -1,0 +1,27 @@
+"""Best-of-K kernel time of one queue-mode launch over the C3 batch (256 GMM N=1000 graphs,
+seeds 0..255, device generator exact mode); optional second column with another env setting:
+  python scripts/batch_time.py [graphs] [reps] [ENV=VAL,...]"""
+import os, sys, time
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+nb = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 7
+if len(sys.argv) > 3:
+    for kv in sys.argv[3].split(","):
+        k, v = kv.split("=")
+        os.environ[k] = v
+from mdcommunity_amd import _lib, engine, gmm_gpu
+W = engine.load_weights(engine.DEFAULT_UNIT)
+graphs = [(1000,) + e for e in gmm_gpu.gmm_pairs(1000, range(nb), exact=True)]
+eng = _lib.Engine(W)
+eng.load_graphs(graphs)
+eng.reset(); out = eng.rollout()
+rem = sum(len(o[0]) for o in out)
+ts = []
+for _ in range(reps):
+    eng.reset(); eng.rollout(); ts.append(eng.last_timing()[0])
+ts.sort()
+print("batch %d (%s): removals %d, kernel ms best %.2f median %.2f -> %.0f removals/s" % (
+    nb, sys.argv[3] if len(sys.argv) > 3 else "default", rem, ts[0], ts[len(ts) // 2], rem / ts[len(ts) // 2] * 1e3), flush=True)
+eng.close()
