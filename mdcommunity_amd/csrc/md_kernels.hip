@@ -96,15 +96,16 @@ constexpr int P2_M = 0;                         // [2][2][128][17] [P.P1 | X.P2]
 constexpr int P2_E = 0;                         // [2][2][64][17] new embedding / attention output
 constexpr int P2_F = P2_X;                      // [2][2][64][17] tanh features / Q-head input
 constexpr int P2_HID = 0;                       // [2][32][33]
-constexpr int P2_STG = 0;                       // gather staging, [2][STG_ROWS][16] float4
-constexpr int P2_ROW = 2 * P2_X;                // [32] node id per row (int)
+constexpr int P2_NB1 = S_NBH - (S_END - S_NBH); // second tile's list region (header + lists)
+constexpr int P2_ROW = P2_NB1 - 784;            // [32] node id per row (int)
 constexpr int P2_RED = P2_ROW + 32;             // [2][32][8] sum-of-squares partials
 constexpr int P2_DOT = P2_RED + 512;            // [32][3] gate dot products, [2][32] gates at +96
 constexpr int P2_Q = P2_DOT + 160;              // [2][32]
 constexpr int P2_FLAG = P2_Q + 64;              // ints: [0] lists cached, [1..2] lists ok, [8..15] wave totals
-constexpr int P2_NB1 = S_NBH - (S_END - S_NBH); // second tile's list region (header + lists)
-static_assert(P2_FLAG + 16 <= P2_NB1, "paired-tile scratch below the second list region");
-static_assert(2 * STG_ROWS * 64 <= 2 * P2_X, "paired gather staging inside P, X");
+constexpr int P2_STG = 0;                       // gather staging, [2][STG2_ROWS][16] float4 (P, X and beyond)
+constexpr int STG2_ROWS = 88, STG2_LD = (STG2_ROWS * 16 + 255) / 256;  // rows per layer, loads per thread
+static_assert(P2_FLAG + 16 == P2_NB1 && 2 * P2_X <= P2_ROW, "paired-tile scratch below the second list region");
+static_assert(2 * STG2_ROWS * 64 <= P2_ROW, "paired gather staging below the row ids");
 static_assert(2 * 32 * 33 <= P2_X, "paired hidden layer inside the E region");
 __device__ __forceinline__ int p2b(int l, int rb, int K) { return (l * 2 + rb) * K * LDT; }
 // phase A uses [L_W, L_TOTAL) (weights are reloaded afterwards)
@@ -2506,25 +2507,25 @@ __device__ __noinline__ void gather_pair(KParams&, const GraphInfo gi, int it) {
     }
   }
   const int t0 = h0[128 + l], totl = t0 + h1[128 + l];
-  const int nbat = (max(h0[128] + h1[128], h0[129] + h1[129]) + STG_ROWS - 1) / STG_ROWS;
+  const int nbat = (max(h0[128] + h1[128], h0[129] + h1[129]) + STG2_ROWS - 1) / STG2_ROWS;
   const int off0 = h0[l * 16 + r], cnt0 = h0[32 + l * 16 + r];
   const int off1 = t0 + h1[l * 16 + r], cnt1 = h1[32 + l * 16 + r];
-  float4* stg = (float4*)(scr + P2_STG) + l * STG_ROWS * 16;
-  auto issue = [&](int b, float4 (&x)[5], bool (&ok)[5]) {
-    const int base = b * STG_ROWS;
-    int src[5];
+  float4* stg = (float4*)(scr + P2_STG) + l * STG2_ROWS * 16;
+  auto issue = [&](int b, float4 (&x)[STG2_LD], bool (&ok)[STG2_LD]) {
+    const int base = b * STG2_ROWS;
+    int src[STG2_LD];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
+    for (int i = 0; i < STG2_LD; ++i) {
       const int k = t + 256 * i, row = base + (k >> 4);
       src[i] = -1;
-      if (b < nbat && k < STG_ROWS * 16 && row < totl) {
+      if (b < nbat && k < STG2_ROWS * 16 && row < totl) {
         const int id = row < t0 ? nb0[row] : nb1[row - t0];
         src[i] = MD_BOK(id < gi.n, 4) ? (table ? ldc(deg + id) : id) : -1;
         if (!MD_BOK(src[i] < gi.n, 5)) src[i] = -1;
       }
     }
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
+    for (int i = 0; i < STG2_LD; ++i) {
       ok[i] = src[i] >= 0;
       if (ok[i]) x[i] = ldc4(hp, src[i] * 256 + ((t + 256 * i) & 15) * 16);
     }
@@ -2551,18 +2552,18 @@ __device__ __noinline__ void gather_pair(KParams&, const GraphInfo gi, int it) {
       a.w = a.w + y.w;
     }
   };
-  auto consume = [&](int b, const float4 (&x)[5], const bool (&ok)[5]) {
-    const int base = b * STG_ROWS;
+  auto consume = [&](int b, const float4 (&x)[STG2_LD], const bool (&ok)[STG2_LD]) {
+    const int base = b * STG2_ROWS;
 #pragma unroll
-    for (int i = 0; i < 5; ++i)
+    for (int i = 0; i < STG2_LD; ++i)
       if (ok[i]) stg[t + 256 * i] = x[i];
     __syncthreads();
-    add_range(acc[0], max(off0, base), min(off0 + cnt0, base + STG_ROWS), base);
-    add_range(acc[1], max(off1, base), min(off1 + cnt1, base + STG_ROWS), base);
+    add_range(acc[0], max(off0, base), min(off0 + cnt0, base + STG2_ROWS), base);
+    add_range(acc[1], max(off1, base), min(off1 + cnt1, base + STG2_ROWS), base);
     __syncthreads();
   };
-  float4 xa[5], xb[5];
-  bool oka[5], okb[5];
+  float4 xa[STG2_LD], xb[STG2_LD];
+  bool oka[STG2_LD], okb[STG2_LD];
   if (nbat > 0) issue(0, xa, oka);
   for (int b = 0; b < nbat; b += 2) {
     issue(b + 1, xb, okb);
@@ -2828,13 +2829,13 @@ __device__ __noinline__ void attention_q_pair(KParams&, const GraphInfo gi, int 
       for (int rb = 0; rb < 2; ++rb) xa[rb][s] = scr[P2_E + p2b(l, rb, 64) + (4 * s + ak) * LDT + ar];
       wa[s] = tf[s * 64 + lane];
     }
-    __builtin_amdgcn_sched_barrier(0);
     f4 a[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) a[rb] = mfma16(xa[rb][s], wa[s], a[rb]);
     }
+    __builtin_amdgcn_sched_barrier(0);
     const float b = wi[W_ITB + col];
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
@@ -2955,13 +2956,13 @@ __device__ __noinline__ void attention_q_pair(KParams&, const GraphInfo gi, int 
       for (int rb = 0; rb < 2; ++rb) xa[rb][s] = scr[P2_F + p2b(l, rb, 64) + (4 * s + ak) * LDT + ar];
       wa[s] = hf[s * 64 + lane];
     }
-    __builtin_amdgcn_sched_barrier(0);
     f4 a[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) a[rb] = mfma16(xa[rb][s], wa[s], a[rb]);
     }
+    __builtin_amdgcn_sched_barrier(0);
     // hid overwrites the (dead) E region only, not the F being read
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
