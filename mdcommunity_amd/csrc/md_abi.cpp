@@ -89,6 +89,7 @@ struct md_ctx {
   int env_mode = 1;  // 1: dedicated environment workgroups for small batches
   int variant = 0;   // diagnostics knob (MD_VARIANT)
   int pair_on = 1;   // queue mode: paired tiles (MD_PAIR=0: one tile at a time)
+  int qpark = 8;     // queue mode: at most this many graphs left -> the lock-step kernel (MD_QPARK, 0 = off)
   double last_ms = 0.0;
   int last_launches = 0;
 
@@ -498,6 +499,7 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
   }
   p.qmode = qmode ? 1 : 0;
   p.qpair = c->pair_on ? 1 : 0;
+  p.qpark = c->qpark;
   p.nglist = ngl;
   p.n_env = n_env;
   p.variant = c->variant;
@@ -665,6 +667,7 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_VARIANT")) c->variant = std::atoi(v);
   if (const char* v = std::getenv("MD_ENV_MODE")) c->env_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_PAIR")) c->pair_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MD_QPARK")) c->qpark = std::max(0, std::min(16, std::atoi(v)));
   if (const char* v = std::getenv("MD_HOST_HANDSHAKE")) c->host_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_POLL_US")) c->poll_us = std::atoi(v);
   if (const char* v = std::getenv("MD_H0G")) c->h0g_on = std::atoi(v) != 0;
@@ -1048,6 +1051,12 @@ md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, i
     std::vector<int> next;
     for (int g : gl) {
       GraphVar& v = c->hvar[g];
+      if (v.status == ST_RUN) {
+        // left by a queue-mode launch at its tail: the next launch continues it
+        v.npend = 0;
+        next.push_back(g);
+        continue;
+      }
       if (v.status != ST_NEED_HOST) continue;
       const GraphInfo& gi = c->hinfo[g];
       if (!cb && !c->tie_argsort)

@@ -3267,7 +3267,20 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
         if (threadIdx.x == 0) raise_err(p, ERR_LIVE_MISMATCH);
         break;
       }
-      if (st == ST_RUN) {
+      // The launch's tail (every graph admitted, at most p.qpark still running): the graph
+      // leaves the queue after this environment step and the host continues it in the
+      // lock-step kernel (dedicated environment workgroups, speculative steps for a single
+      // graph), whose per-step latency with few graphs is 1.5-2.5x lower; a launch begins
+      // with phase A without an action, so the rollout continues exactly from this state.
+      bool park = false;
+      // (a launch of at most p.qpark graphs never parks: each launch makes progress)
+      if (st == ST_RUN && p.qpark > 0 && ng > p.qpark) {
+        if (threadIdx.x == 0)
+          bc[6] = ldc((const int*)(p.qctl + QC_ADMIT)) >= ng && ldc((const int*)(p.qctl + QC_REM)) <= p.qpark;
+        __syncthreads();
+        park = bc[6] != 0;
+      }
+      if (st == ST_RUN && !park) {
         if (threadIdx.x == 0) {  // one decision for the workgroup
           int t = q_tiles_per_item(p);
           if (t > 1 && ldc((const int*)(p.qctl + QC_ADMIT)) >= ng && ldc((const int*)(p.qctl + QC_REM)) <= q_tail(p)) t = 1;

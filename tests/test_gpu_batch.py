@@ -88,20 +88,22 @@ def check_goldens(mr, outs):
 
 
 @pytest.mark.timeout(240)
-def test_c3_256_graphs_one_queue_launch(graphs, weights, single):
-    """configs[2]: 256 graphs in one queue-mode launch == 256 single-graph rollouts."""
+def test_c3_256_graphs_one_queue_launch_and_tail(graphs, weights, single):
+    """configs[2]: 256 graphs in one queue-mode launch (its last <= 8 running graphs continue
+    in one lock-step launch, MD_QPARK) == 256 single-graph rollouts."""
     mr, outs, launches = batch_rollout(weights, graphs[:256])
-    assert launches == 1
+    assert launches == 2
     assert sum(len(s) for s, _ in outs) > 256 * 20
     check_against_single(mr, outs, single, 0)
     check_goldens(mr, outs)
 
 
 @pytest.mark.timeout(240)
-def test_c5_slice_512_graphs_one_queue_launch(graphs, weights, single):
-    """configs[4]'s per-GPU slice: 512 graphs (G_CAP) in one launch == single-graph rollouts."""
+def test_c5_slice_512_graphs_one_queue_launch_and_tail(graphs, weights, single):
+    """configs[4]'s per-GPU slice: 512 graphs (G_CAP) in one queue launch and its lock-step
+    tail launch == single-graph rollouts."""
     mr, outs, launches = batch_rollout(weights, graphs)
-    assert launches == 1
+    assert launches == 2
     check_against_single(mr, outs, single, 0)
     check_goldens(mr, outs)
 
@@ -114,3 +116,17 @@ def test_shard_blocks_equal_whole(graphs, weights, single):
     lo, hi = parallel.shard(512, 1, 2)
     mr, outs, _ = batch_rollout(weights, graphs[lo:hi])
     check_against_single(mr, outs, single, lo)
+
+
+@pytest.mark.timeout(240)
+def test_tail_handoff_off_same_rollouts(graphs, weights, monkeypatch):
+    """MD_QPARK=0 (the whole batch in one queue launch) gives the same rollouts as the default
+    hand-off of the last running graphs to the lock-step kernel."""
+    monkeypatch.setenv("MD_QPARK", "0")
+    mr0, outs0, launches0 = batch_rollout(weights, graphs[:64])
+    monkeypatch.setenv("MD_QPARK", "16")
+    mr1, outs1, launches1 = batch_rollout(weights, graphs[:64])
+    assert launches0 == 1 and launches1 == 2
+    assert np.array_equal(mr0, mr1)
+    for a, b in zip(outs0, outs1):
+        assert a[0].tolist() == b[0].tolist() and a[1].tolist() == b[1].tolist()
