@@ -221,6 +221,10 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *                       bits 16+  queue-mode admission limit (graphs running at once)
  *   MD_ENV_MODE       0: no dedicated environment workgroups for small batches (shared
  *                     mode); default 1
+ *   MD_PAIR           0: queue-mode work items run their two tiles one after the other
+ *                     instead of jointly (default 1)
+ *   MD_QPARK          queue mode: once every graph is admitted and at most this many still
+ *                     run, they continue in one lock-step launch (default 8, 0 = off, <= 16)
  *   MD_HOST_HANDSHAKE 0: end the launch on a tie and relaunch after the host selection
  *                     (default 1: in-kernel hand-shake through mapped host memory)
  *   MD_POLL_US        host-thread polling interval of the hand-shake (µs)
