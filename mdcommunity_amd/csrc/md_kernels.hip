@@ -3293,7 +3293,9 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
 #ifdef MD_QPROF
         const unsigned long long tqb = wall_clock64();
 #endif
-        const bool built = lds_env && !(p.variant & (4096 | 16)) && env_build_lists(p, p.ginfo[g], gl);
+        // (in the tail -- one tile per item -- the iteration-1 tiles build their own lists: the
+        // environment item is on the graph's critical path and most workgroups are idle)
+        const bool built = lds_env && !(p.variant & (4096 | 16)) && tpi > 1 && env_build_lists(p, p.ginfo[g], gl);
 #ifdef MD_QPROF
         if (qp != nullptr && (p.variant & 8) && threadIdx.x == 0) atomicAdd(qp + 86, wall_clock64() - tqb);
 #endif
