@@ -130,3 +130,30 @@ def test_tail_handoff_off_same_rollouts(graphs, weights, monkeypatch):
     assert np.array_equal(mr0, mr1)
     for a, b in zip(outs0, outs1):
         assert a[0].tolist() == b[0].tolist() and a[1].tolist() == b[1].tolist()
+
+
+@pytest.mark.timeout(240)
+def test_multi_node_steps_batch_tail_handoff(graphs, weights, monkeypatch):
+    """step > 1 (every prediction through the host selection, several removals per step) on a
+    queue-mode batch: the graphs handed to the lock-step kernel at the tail (MD_QPARK) keep
+    their rollouts -- same as MD_QPARK=0 and as each graph's own single-graph rollout."""
+    sel = graphs[:24]
+
+    def run(park, batch):
+        monkeypatch.setenv("MD_QPARK", park)
+        eng = _lib.Engine(weights)
+        try:
+            outs = []
+            for gs in ([sel] if batch else [[g] for g in sel]):
+                eng.load_graphs(gs)
+                eng.reset()
+                outs += [(s.tolist(), r.tolist()) for s, r in eng.rollout(step=3)]
+            return outs, eng.last_timing()[1]
+        finally:
+            eng.close()
+
+    parked, launches = run("16", True)
+    whole, _ = run("0", True)
+    single, _ = run("0", False)
+    assert launches >= 2
+    assert parked == whole == single
