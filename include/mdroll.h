@@ -225,6 +225,8 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *                     instead of jointly (default 1)
  *   MD_QPARK          queue mode: once every graph is admitted and at most this many still
  *                     run, they continue in one lock-step launch (default 8, 0 = off, <= 16)
+ *   MD_QXCD           1: queue mode with 8 XCD-affine work rings (a graph's items stay on the
+ *                     workgroups of one XCD; default 0: one ring)
  *   MD_HOST_HANDSHAKE 0: end the launch on a tie and relaunch after the host selection
  *                     (default 1: in-kernel hand-shake through mapped host memory)
  *   MD_POLL_US        host-thread polling interval of the hand-shake (µs)

@@ -90,6 +90,7 @@ struct md_ctx {
   int variant = 0;   // diagnostics knob (MD_VARIANT)
   int pair_on = 1;   // queue mode: paired tiles (MD_PAIR=0: one tile at a time)
   int qpark = 8;     // queue mode: at most this many graphs left -> the lock-step kernel (MD_QPARK, 0 = off)
+  int qxcd = 0;      // queue mode: 8 XCD-affine work rings (MD_QXCD=1)
   double last_ms = 0.0;
   int last_launches = 0;
 
@@ -191,7 +192,8 @@ md_status fail(md_ctx* c, md_status s, const char* fmt, ...) {
   } while (0)
 
 // Control block layout (ints): [0] barrier counter, [1] error word (zeroed before each launch).
-constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_Q = 2, CTL_SPEC = 8, CTL_TEAM = 12, CTL_EXIT = 14, CTL_PRE = 64, CTL_WORDS = 96;  // CTL_PRE on a line of its own
+constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_Q = 2, CTL_SPEC = 8, CTL_TEAM = 12, CTL_EXIT = 14, CTL_PRE = 64,
+              CTL_RING = 96, CTL_WORDS = 96 + 32 * 8;  // CTL_PRE and each ring's tickets on lines of their own
 constexpr int SPEC_MAX = 32;  // speculative workgroups per launch at most  // CTL_SPEC: u64 request word
 
 Params make_params(md_ctx* c) {
@@ -238,6 +240,8 @@ Params make_params(md_ctx* c) {
   p.err = c->ctl.p + CTL_ERR;
   p.qctl = (unsigned*)(c->ctl.p + CTL_Q);
   p.qslot = c->qslot.p;
+  p.qring = (unsigned*)(c->ctl.p + CTL_RING);
+  p.qrings = c->qxcd ? 8 : 1;
   p.qg = c->qg.p;
   p.nbc_gstride = c->nbc_gstride;
   p.glist = c->glist.p;
@@ -668,6 +672,7 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_ENV_MODE")) c->env_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_PAIR")) c->pair_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_QPARK")) c->qpark = std::max(0, std::min(16, std::atoi(v)));
+  if (const char* v = std::getenv("MD_QXCD")) c->qxcd = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_HOST_HANDSHAKE")) c->host_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_POLL_US")) c->poll_us = std::atoi(v);
   if (const char* v = std::getenv("MD_H0G")) c->h0g_on = std::atoi(v) != 0;
