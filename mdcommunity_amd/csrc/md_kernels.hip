@@ -2570,8 +2570,23 @@ __device__ __noinline__ void gather_pair(KParams&, const GraphInfo gi, int it) {
       a.w = a.w + y.w;
     }
   };
+#ifdef MD_QPROF
+  // (qprof build, iterations 2-3: slot 64 = waiting for a batch's loads, slot 65 = staging
+  // stores + adds + barriers; the next batch's six loads stay in flight)
+  unsigned long long* gw = p.prof != nullptr && (p.variant & 8) && it > 1 ? p.prof + 64 : nullptr;
+#endif
   auto consume = [&](int b, const float4 (&x)[STG2_LD], const bool (&ok)[STG2_LD]) {
     const int base = b * STG2_ROWS;
+#ifdef MD_QPROF
+    unsigned long long tw0 = 0, tw1 = 0;
+    if (gw != nullptr) {
+      tw0 = wall_clock64();
+      if (b + 1 < nbat) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // every thread's loads of this batch are in
+      tw1 = wall_clock64();
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < STG2_LD; ++i)
       if (ok[i]) stg[t + 256 * i] = x[i];
@@ -2579,6 +2594,12 @@ __device__ __noinline__ void gather_pair(KParams&, const GraphInfo gi, int it) {
     add_range(acc[0], max(off0, base), min(off0 + cnt0, base + STG2_ROWS), base);
     add_range(acc[1], max(off1, base), min(off1 + cnt1, base + STG2_ROWS), base);
     __syncthreads();
+#ifdef MD_QPROF
+    if (gw != nullptr && threadIdx.x == 0) {
+      atomicAdd(gw + 0, tw1 - tw0);
+      atomicAdd(gw + 1, wall_clock64() - tw1);
+    }
+#endif
   };
   float4 xa[STG2_LD], xb[STG2_LD];
   bool oka[STG2_LD], okb[STG2_LD];

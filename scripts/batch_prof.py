@@ -56,6 +56,9 @@ if len(P) and P[0, 0] == 1 and P[0, 9] > 0:
         if P[0, 62] > 0:
             print("  paired gather: own loads + first batch in flight %.1f WG-ms, batch loop %.1f WG-ms; %.2f batches and %.0f list entries per gather" % (
                 P[0, 60] / 1e5, P[0, 61] / 1e5, P[0, 62] / max(1, P[0, 10] * 0.5), P[0, 63] / max(1, P[0, 10] * 0.5)))
+        if P[0, 64] > 0:
+            print("  paired gather batches, iterations 2-3 (every thread's loads in, then a barrier): waiting for the loads %.1f WG-ms, staging stores + adds + barriers %.1f WG-ms" % (
+                P[0, 64] / 1e5, P[0, 65] / 1e5))
         att_n = ["tanh GEMM", "dots+gates", "mix+norm", "head", "e-chain", "hidden+Q", "arg-max+stores"]
         print("  attention pieces (WG-ms): " + "  ".join("%s %.1f" % (nm, v) for nm, v in zip(att_n, P[0, 88:95] / 1e5)))
         sys.exit(0)
