@@ -3552,9 +3552,48 @@ __device__ __noinline__ void spec_loop(KParams&) {
     __syncthreads();
     build_alive<false>(E);
     TSTAMP(73);
-    // candidate: the live node of rank k (descending Q, ties by ascending id).  The top
-    // n_spec all have Q >= T, the n_spec-th largest maximum of the 16-node groups (those
-    // maxima are n_spec nodes at >= T), so only the nodes at >= T are ranked.
+    // candidate: the live node of rank k (descending Q, ties by ascending id).  Rank 0 (the
+    // workgroup whose result phase A takes most often) is the arg-max, one block reduction;
+    // ranks >= 1: the top n_spec all have Q >= T, the n_spec-th largest maximum of the 16-node
+    // groups (those maxima are n_spec nodes at >= T), so only the nodes at >= T are ranked.
+    if (k == 0) {
+      float bv = NEG_INF;
+      int bx = 0x7fffffff;
+      for (int x = threadIdx.x; x < n; x += NTHREADS) {
+        const float v = qv[x];
+        if (v > bv) {  // ascending x per thread: the first maximum is the smallest id
+          bv = v;
+          bx = x;
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float v2 = __shfl_xor(bv, o, 64);
+        const int x2 = __shfl_xor(bx, o, 64);
+        if (v2 > bv || (v2 == bv && x2 < bx)) {
+          bv = v2;
+          bx = x2;
+        }
+      }
+      float* wv = gmx;  // the group maxima are not needed for rank 0
+      int* wx = (int*)(gmx + NTHREADS / 64);
+      if (lane_id() == 0) {
+        wv[wave_id()] = bv;
+        wx[wave_id()] = bx;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        float v = wv[0];
+        int x = wx[0];
+        for (int i = 1; i < NTHREADS / 64; ++i)
+          if (wv[i] > v || (wv[i] == v && wx[i] < x)) {
+            v = wv[i];
+            x = wx[i];
+          }
+        misc[3] = v != NEG_INF ? x : -1;
+      }
+      __syncthreads();
+    } else {
     for (int r0 = 0; r0 < n; r0 += NTHREADS) {
       const int x = r0 + (int)threadIdx.x;
       float v = x < n ? qv[x] : NEG_INF;
@@ -3596,6 +3635,7 @@ __device__ __noinline__ void spec_loop(KParams&) {
       if (r == k) misc[3] = x;
     }
     __syncthreads();
+    }
     const int c = misc[3];
     __syncthreads();
     if (c < 0) continue;
