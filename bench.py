@@ -556,8 +556,12 @@ def rank_main(args):
             "graphs_rank0": local_graphs,
             "removals_gathered": int(sum(brem_per_graph)),
             "golden": gold,
-            "roofline": roofline(bflops, bbytes, bk_ms / args.batch_steps, bl / args.batch_steps, None),
+            # per batch step: the queue launch and its tail launch (MD_QPARK) together -- the
+            # algorithmic work and the measured traffic of the whole batch rollout
+            "roofline": roofline(bflops, bbytes, bk_ms / args.batch_steps, 1, None),
         }
+        batch["roofline"]["per"] = "batch step (queue launch + tail launch)"
+        batch["roofline"]["launches_per_step"] = bl / args.batch_steps
         if rank == 0 and args.cpu_dry_run:
             batch["audc_all"] = baudc
             batch["removals_all"] = brem_per_graph
@@ -583,8 +587,12 @@ def rank_main(args):
                               prefix=int(c["prefix"]))
         traffic, traffic_note = load_traffic()
         if batch is not None and traffic is not None and args.batch_graphs == 256 and "batch" in traffic:
-            batch["roofline"]["traffic"] = traffic["batch"].get("hbm_bytes_per_launch")
-            batch["roofline"]["mfma_busy"] = traffic["batch"].get("mfma_busy")
+            tb = traffic["batch"]
+            q, tail = tb.get("hbm_bytes_per_launch"), tb.get("tail_hbm_bytes_per_launch")
+            extra = batch["roofline"]["launches_per_step"] - 1.0
+            if q is not None and (extra < 0.5 or tail is not None):
+                batch["roofline"]["traffic"] = q + (extra * tail if extra >= 0.5 else 0.0)
+            batch["roofline"]["mfma_busy"] = tb.get("mfma_busy")
         have = golden is not None and audc is not None
         k = 0
         if have:

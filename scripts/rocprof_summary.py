@@ -87,6 +87,18 @@ def workload(d, w, lines):
                 vals[c] = v
                 lines.append(f"== {w} {c} per {kernel} dispatch (raw): {[round(x, 1) for x in v]}")
     m = {c: mean(v) for c, v in vals.items()}
+    if w == "batch":
+        # the tail launch of each batch rollout (md_rollout_kernel: the last graphs the queue
+        # hands to the lock-step kernel): its traffic per dispatch, so bench.py can report the
+        # traffic of a whole batch step
+        tv = {}
+        for group in ("fetch", "write"):
+            for path in dbs(os.path.join(d, f"pmc_{group}_{w}")):
+                for c, v in pmc(path, "md_rollout_kernel").items():
+                    tv[c] = v
+                    lines.append(f"== {w} {c} per md_rollout_kernel (tail) dispatch (raw): {[round(x, 1) for x in v]}")
+        if tv.get("FETCH_SIZE") and tv.get("WRITE_SIZE"):
+            out["tail_hbm_bytes_per_launch"] = 2.0 * 1024.0 * mean(tv["FETCH_SIZE"]) + 1024.0 * mean(tv["WRITE_SIZE"])
     if m.get("FETCH_SIZE") is not None and m.get("WRITE_SIZE") is not None:
         out["fetch_bytes_per_launch"] = 2.0 * 1024.0 * m["FETCH_SIZE"]
         out["write_bytes_per_launch"] = 1024.0 * m["WRITE_SIZE"]
