@@ -81,8 +81,20 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-step", action="store_true", help="skip the per-step-protocol comparison rollouts")
     ap.add_argument("--cpu-sample-seconds", type=float, default=12.0)
-    ap.add_argument("--batch-cpu-procs", type=int, default=16,
-                    help="processes of the batch CPU baseline (1 torch thread each; capped by the CPUs available)")
+    ap.add_argument("--batch-cpu-procs", type=int, default=0,
+                    help="processes of the batch CPU baseline (1 torch thread each); 0: the CPUs available to "
+                         "this job (available_cpus())")
+    ap.add_argument("--c5-graphs", type=int, default=4096,
+                    help="graphs of the C5 object (BASELINE configs[4]), strong-scaled: the same graphs at every "
+                         "world size, split contiguously over the ranks (0: skip)")
+    ap.add_argument("--c5-steps", type=int, default=1)
+    ap.add_argument("--rccl", action="store_true",
+                    help="initialise torch.distributed over RCCL (backend nccl) even at world size 1, so the "
+                         "collectives of the multi-GPU path run on the GPU")
+    ap.add_argument("--dist-timeout", type=float, default=600.0, help="seconds before a collective gives up")
+    ap.add_argument("--launch-timeout", type=float, default=0.0,
+                    help="launcher: stop every rank after this many seconds (0: no limit)")
+    ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # tests: this rank exits with 3
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="launcher/rank/gather plumbing on the CPU: gloo backend, host stub engine, no GPU")
     ap.add_argument("--rehearse-shared-gpu", action="store_true",
@@ -103,21 +115,52 @@ def _free_port():
 
 def launch_ranks(args, argv):
     """Spawn `args.gpus` rank processes of this script (one per GPU), relay rank 0's output.
-    The launcher itself never touches a GPU; each rank is a fresh interpreter."""
+    The launcher itself never touches a GPU; each rank is a fresh interpreter.
+
+    Fail-fast: every rank is polled; the first rank to exit non-zero (or the --launch-timeout
+    deadline) terminates the other ranks -- a rank blocked in a collective with a dead peer
+    would otherwise wait until the driver's time limit -- and its status is returned."""
+    import tempfile
     world = args.gpus
     port = _free_port()
     procs = []
+    out_f = tempfile.TemporaryFile()
     for r in range(world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
-                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
-    out, _ = procs[0].communicate()
-    codes = [procs[0].returncode] + [p.wait() for p in procs[1:]]
-    sys.stdout.write(out.decode())
+                                      stdout=out_f if r == 0 else subprocess.DEVNULL))
+    deadline = time.time() + args.launch_timeout if args.launch_timeout > 0 else None
+    status = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            r, status = bad[0]
+            sys.stderr.write(f"bench launcher: rank {r} exited with status {status}; stopping the other ranks\n")
+            break
+        if all(c == 0 for c in codes):
+            break
+        if deadline is not None and time.time() > deadline:
+            status = 124
+            sys.stderr.write(f"bench launcher: ranks still running after {args.launch_timeout:.0f} s; stopping them\n")
+            break
+        time.sleep(0.1)
+    if status != 0:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        t_end = time.time() + 10
+        for p in procs:
+            try:
+                p.wait(max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    out_f.seek(0)
+    sys.stdout.write(out_f.read().decode())
     sys.stdout.flush()
-    bad = [c for c in codes if c != 0]
-    return bad[0] if bad else 0
+    return status
 
 
 # ------------------------------------------------------------------ host stub engine (--cpu-dry-run)
@@ -211,31 +254,73 @@ def _oracle_rollout_seed(job):
     return seed, len(seq), time.time() - t0, score
 
 
-def cpu_baseline_batch(n, procs_wanted, graphs_per_proc=2):
+def available_cpus():
+    """(CPUs this job may use, how that was decided): the scheduler affinity mask, capped by a
+    cgroup CPU quota (cgroup v2 cpu.max / v1 cfs_quota) and by the host share the environment
+    states (OMP_NUM_THREADS) when set -- on a shared GPU box that share, not os.cpu_count(), is
+    what the job owns."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = float(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = float(f.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    n = aff if quota is None else max(1, min(aff, int(quota)))
+    # a host whose CPUs are shared between jobs states the job's share in OMP_NUM_THREADS (the
+    # GPU box sets it to the per-GPU share and asks that worker pools be sized to it)
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    share = int(share) if share.isdigit() and int(share) > 0 else None
+    if share is not None:
+        n = min(n, share)
+    how = (f"affinity {aff}, cgroup quota {'none' if quota is None else f'{quota:g}'}, OMP_NUM_THREADS share "
+           f"{share if share is not None else 'unset'}, os.cpu_count {os.cpu_count()}")
+    return n, how
+
+
+def cpu_baseline_batch(n, procs_wanted=0, graphs_per_proc=1):
     """BASELINE.md §3 / SURVEY.md §8(d): the batch workload on the CPU as P independent
-    1-thread oracle processes (embarrassingly parallel over graphs), on a bounded sample of the
-    batch's seeds (the first P * graphs_per_proc).  Rate = sample removals / pool wall time."""
+    1-thread oracle processes (embarrassingly parallel over graphs), P = the CPUs available to
+    this job (available_cpus) unless `procs_wanted` > 0, on a bounded sample of the batch's
+    seeds (the first P * graphs_per_proc, i.e. at least P graphs).  Rate = sample removals / pool
+    wall time (each job also builds its graph, ~20 ms against seconds of rollout)."""
     import multiprocessing as mp
-    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    P = max(1, min(procs_wanted, avail))
+    avail, how = available_cpus()
+    P = max(1, avail if procs_wanted <= 0 else min(procs_wanted, avail))
     jobs = [(n, s) for s in range(P * graphs_per_proc)]
     ctx = mp.get_context("spawn")  # fresh interpreters: nothing of this GPU process is inherited
     with ctx.Pool(P) as pool:
-        pool.map(_oracle_rollout_seed, [(64, 0)] * P)  # import torch / networkx in every worker
+        pool.map(_oracle_rollout_seed, [(64, 0)] * P, chunksize=1)  # import torch / networkx in every worker
         t0 = time.time()
         res = pool.map(_oracle_rollout_seed, jobs, chunksize=1)
         dt = time.time() - t0
     rem = sum(r[1] for r in res)
+    busy = sum(r[2] for r in res)
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
             cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
     except OSError:
         pass
+    per_core = rem / busy if busy > 0 else 0.0
     return dict(value=rem / dt, unit="removals/s", cores=P, kind="port",
+                per_core_value=per_core,
+                # what the same per-core rate would give on every CPU the host shows (not measured:
+                # the job owns only `cores` of them)
+                full_host_extrapolated_value=per_core * (os.cpu_count() or P),
                 sample=f"{len(jobs)} GMM N={n} graphs (batch seeds 0..{len(jobs) - 1}), {rem} removals, one full "
                        f"oracle rollout each on a pool of {P} processes x 1 torch thread, {dt:.1f} s wall; "
-                       f"{avail} CPUs available to this process, {os.cpu_count()} visible; {cpu_model}",
+                       f"CPUs: {how}; {cpu_model}",
                 audc=[r[3] for r in sorted(res)][:3])
 
 
@@ -267,31 +352,58 @@ def run_steps(eng, steps):
 
 
 def trace_work(eng, n_graphs):
-    flops, nbytes, preds = 0.0, 0.0, 0
+    """Per-prediction algorithmic flops and bytes of the last rollout of each
+    graph, from the device's own trace (live nodes and residual edges at each prediction)."""
+    fl, by = [], []
     for gidx in range(n_graphs):
         tr = eng.trace(gidx)
         for n_t, a0, a1 in zip(tr["n_live"], tr["m0"], tr["m1"]):
-            flops += step_flops(float(n_t), float(a0), float(a1))
-            nbytes += step_bytes(float(n_t), float(a0), float(a1))
-            preds += 1
-    return flops, nbytes, preds
+            fl.append(step_flops(float(n_t), float(a0), float(a1)))
+            by.append(step_bytes(float(n_t), float(a0), float(a1)))
+    return np.asarray(fl, np.float64), np.asarray(by, np.float64)
 
 
-def roofline(flops_per_step, bytes_per_step, kernel_ms_per_step, launches_per_step, traffic):
+def roofline(F, B, kernel_ms_per_step, launches_per_step, traffic):
+    """The kernel's roofline per SURVEY.md §8(d): each prediction t is bound by the larger of
+    F_t / FP32-MFMA peak and B_t / HBM peak; the roofline time of a bench step is the sum of
+    those, and `bound` names the roof whose terms dominate that sum.  `achieved` / `frac` are
+    the algorithmic rate of that roof (bytes/s or flop/s over the measured kernel time);
+    `roofline_time_frac` = Σ_t max(F_t/Pf, B_t/Pb) / kernel time; both roofs' fractions are
+    reported beside it."""
     t = kernel_ms_per_step * 1e-3
-    achieved = flops_per_step / t / 1e12 if t > 0 else 0.0
+    F = np.asarray(F, np.float64)
+    B = np.asarray(B, np.float64)
+    tf = F / (PEAK_FP32_TFLOPS * 1e12)
+    tb = B / (PEAK_HBM_GBS * 1e9)
+    hbm_terms = float(tb[tb >= tf].sum())
+    mfma_terms = float(tf[tf > tb].sum())
+    t_roof = float(np.maximum(tf, tb).sum())
+    Fs, Bs = float(F.sum()), float(B.sum())
+    mfma_frac = Fs / t / (PEAK_FP32_TFLOPS * 1e12) if t > 0 else 0.0
+    hbm_frac = Bs / t / (PEAK_HBM_GBS * 1e9) if t > 0 else 0.0
+    if hbm_terms >= mfma_terms:
+        bound, achieved, peak, unit = "hbm", (Bs / t / 1e9 if t > 0 else 0.0), PEAK_HBM_GBS, "GB/s"
+    else:
+        bound, achieved, peak, unit = "mfma", (Fs / t / 1e12 if t > 0 else 0.0), PEAK_FP32_TFLOPS, "TFLOP/s"
+    per = max(1e-9, launches_per_step)
     return {
-        "bound": "mfma",
+        "bound": bound,
         "achieved": achieved,
-        "peak": PEAK_FP32_TFLOPS,
-        "unit": "TFLOP/s",
-        "frac": achieved / PEAK_FP32_TFLOPS,
+        "peak": peak,
+        "unit": unit,
+        "frac": achieved / peak,
         "traffic": traffic,
-        "algorithmic_flops_per_launch": flops_per_step / max(1e-9, launches_per_step),
-        "algorithmic_bytes_per_launch": bytes_per_step / max(1e-9, launches_per_step),
-        "kernel_ms_per_launch": kernel_ms_per_step / max(1e-9, launches_per_step),
-        "hbm_achieved_GBs": bytes_per_step / t / 1e9 if t > 0 else 0.0,
-        "hbm_frac": (bytes_per_step / t / 1e9) / PEAK_HBM_GBS if t > 0 else 0.0,
+        "roofline_time_frac": t_roof / t if t > 0 else 0.0,
+        "mfma_frac": mfma_frac,
+        "hbm_frac": hbm_frac,
+        "mfma_achieved_TFLOPs": Fs / t / 1e12 if t > 0 else 0.0,
+        "hbm_achieved_GBs": Bs / t / 1e9 if t > 0 else 0.0,
+        "predictions_hbm_bound": int((tb >= tf).sum()),
+        "predictions_mfma_bound": int((tf > tb).sum()),
+        "roofline_ms_per_step": t_roof * 1e3,
+        "algorithmic_flops_per_launch": Fs / per,
+        "algorithmic_bytes_per_launch": Bs / per,
+        "kernel_ms_per_launch": kernel_ms_per_step / per,
     }
 
 
@@ -409,29 +521,119 @@ def real_scale_object(args, make_engine, tmpdir):
 
 
 # ------------------------------------------------------------------ one rank
+def _init_dist(args, world, local):
+    """torch.distributed for this rank: RCCL (backend "nccl") with one GPU per rank, gloo for
+    the CPU dry run and the shared-GPU rehearsal.  `--rccl` initialises RCCL at world size 1 as
+    well (the multi-GPU collectives then run on one GPU).  Returns (dist, device, backend)."""
+    import datetime
+    if world == 1 and not args.rccl:
+        return None, None, None
+    import torch.distributed as tdist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if "MASTER_PORT" not in os.environ:
+        os.environ["MASTER_PORT"] = str(_free_port())
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", str(world))
+    timeout = datetime.timedelta(seconds=args.dist_timeout)
+    if args.cpu_dry_run or args.rehearse_shared_gpu:
+        tdist.init_process_group("gloo", timeout=timeout)
+        return tdist, None, "gloo"
+    import torch
+    torch.cuda.set_device(local)
+    tdist.init_process_group("nccl", timeout=timeout, device_id=torch.device("cuda", local))  # RCCL over xGMI
+    return tdist, "cuda", "nccl"
+
+
+def _graph_source(args, gpu):
+    """Seed -> (n, edges0, edges1) of the reference's GMM generator, cached per process: the
+    device generator in exact mode (gmm_gpu: numpy/random streams on the host, pair loop on the
+    GPU; the same graphs as gmm.gmm_pair), or gmm.gmm_pair in the CPU dry run."""
+    from mdcommunity_amd import gmm, gmm_gpu
+    cache = {}
+
+    def get(seeds):
+        seeds = list(seeds)
+        need = [s for s in seeds if s not in cache]
+        if need:
+            if args.cpu_dry_run:
+                made = [gmm.gmm_pair(args.n, seed=s) for s in need]
+            else:
+                made = gmm_gpu.gmm_pairs(args.n, need, exact=True, device=gpu)
+            for s, e in zip(need, made):
+                cache[s] = (args.n,) + tuple(e)
+        return [cache[s] for s in seeds]
+    return get
+
+
+def many_graph_object(args, name, graphs, lo, steps, rank, world, dist, dev, make_engine, weights, sync,
+                      parallel):
+    """Whole rollouts of this rank's block of graphs (seeds lo..), `steps` timed bench steps after
+    one warm-up; per-graph AUDC and removal counts gathered over the ranks (RCCL all-gather);
+    rate = removals of all ranks / max rank time.  The roofline is per bench step (every launch
+    of the step: queue launches and their tail launches)."""
+    eng = make_engine(weights)
+    eng.load_graphs(graphs)
+    run_steps(eng, 1)
+    sync()
+    tb = time.perf_counter()
+    k_ms, nl, rem, last, _ = run_steps(eng, steps)
+    sync()
+    elapsed = time.perf_counter() - tb
+    F, B = trace_work(eng, len(graphs))
+    mr, outs = last
+    audc = [audc_of(r, m, n) for (n, _, _), m, (_, r) in zip(graphs, mr, outs)]
+    rem_per_graph = [len(sq) for sq, _ in outs]
+    gold = golden_checks([outs[s - lo][0] if lo <= s < lo + len(graphs) else None for s in range(3)],
+                         [audc[s - lo] if lo <= s < lo + len(graphs) else None for s in range(3)]) \
+        if args.n == 1000 else {}
+    local_graphs = len(graphs)
+    local_value = rem / elapsed
+    if dist is not None:
+        audc, rem_per_graph = parallel.gather_results(dist, audc, rem_per_graph, dev)  # RCCL over xGMI
+        elapsed = parallel.max_over_ranks(dist, elapsed, dev)
+        rem = parallel.sum_over_ranks(dist, rem, dev)
+    eng.close()
+    out = {
+        "value": rem / elapsed,
+        "unit": "removals/s",
+        "steps": steps,
+        "ms_per_step": elapsed / steps * 1e3,
+        "removals_per_step": rem / steps,
+        "audc_mean": float(np.mean(audc)) if audc else None,
+        "graphs": len(audc),
+        "graphs_rank0": local_graphs,
+        "rank0_value": local_value,
+        "removals_gathered": int(sum(rem_per_graph)),
+        "golden": gold,
+        "roofline": roofline(F, B, k_ms / steps, nl / steps, None),
+    }
+    out["roofline"]["per"] = "bench step (every launch of the step: queue launches + tail launches)"
+    out["roofline"]["launches_per_step"] = nl / steps
+    return out, audc, rem_per_graph
+
+
 def rank_main(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    dev = None
-    backend = None
-    if world > 1:
-        import torch.distributed as tdist
-        if args.cpu_dry_run or args.rehearse_shared_gpu:
-            backend = "gloo"
-            tdist.init_process_group("gloo")
-        else:
-            import torch
-            backend = "nccl"  # RCCL over xGMI on ROCm
-            torch.cuda.set_device(local)
-            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
-            dev = "cuda"
-        dist = tdist
+    if args.rehearse_shared_gpu and world > 1:
+        # ranks sharing one GPU: persistent kernels with grid barriers must all be resident at
+        # once, so each rank takes only its share of the CUs and no speculative workgroups
+        import torch
+        ndev = max(1, torch.cuda.device_count())  # counts devices without initialising one
+        per_gpu = -(-world // ndev)
+        os.environ["MD_MAX_CUS"] = str(256 // per_gpu)
+        os.environ["MD_SPEC"] = "0"
+    dist, dev, backend = _init_dist(args, world, local)
+    if args.fail_rank == rank:
+        sys.stderr.write(f"rank {rank}: exiting with status 3 (--fail-rank)\n")
+        os._exit(3)
 
-    from mdcommunity_amd import engine, gmm, gmm_gpu, parallel
+    from mdcommunity_amd import engine, gmm, parallel
 
     if args.cpu_dry_run:
+        gpu = None
+
         def make_engine(weights, cost_mode=0):
             return DryEngine()
     else:
@@ -439,14 +641,14 @@ def rank_main(args):
 
         if args.rehearse_shared_gpu:
             import torch
-            ndev = max(1, torch.cuda.device_count())  # counts devices without initialising one
-            gpu = local % ndev
+            gpu = local % max(1, torch.cuda.device_count())
         else:
             gpu = local if world > 1 else 0
 
         def make_engine(weights, cost_mode=_lib.MD_COST_UNIT):
             return _lib.Engine(weights, device=gpu, cost_mode=cost_mode)
 
+    graphs_of = _graph_source(args, gpu)
     weights = engine.load_weights(engine.DEFAULT_UNIT)
     eng = make_engine(weights)
     edges = gmm.gmm_pair(args.n, seed=args.seed)
@@ -462,8 +664,8 @@ def rank_main(args):
     # ---------------- headline: single graph rollouts (configs[1]); --steps 0 skips it (profiling
     # the batch object alone)
     kernel_ms, launches, removals, elapsed, s0_ms = 0.0, 0, 0, 1e-9, 0.0
-    flops = nbytes = 0.0
-    preds, audc, seq = 0, None, np.zeros(0, np.int32)
+    F = B = np.zeros(0)
+    audc, seq = None, np.zeros(0, np.int32)
     if args.steps > 0:
         run_steps(eng, max(0, args.warmup))
         sync()
@@ -471,7 +673,7 @@ def rank_main(args):
         kernel_ms, launches, removals, last, s0_ms = run_steps(eng, args.steps)
         sync()
         elapsed = time.perf_counter() - t0
-        flops, nbytes, preds = trace_work(eng, 1)
+        F, B = trace_work(eng, 1)
         mr, outs = last
         seq, ranks = outs[0]
         audc = audc_of(ranks, mr[0], args.n)
@@ -511,60 +713,35 @@ def rank_main(args):
         max_elapsed = parallel.max_over_ranks(dist, elapsed, dev)
         tot_removals = parallel.sum_over_ranks(dist, removals, dev)
 
-    # ---------------- batch object (configs[2] per GPU; configs[4] shape across ranks)
+    # ---------------- batch object (configs[2]: batch_graphs per GPU, weak-scaled over ranks)
     batch = None
     if args.batch_graphs > 0:
         total = args.batch_graphs * world
         lo, hi = parallel.shard(total, rank, world)
-        if args.cpu_dry_run:
-            bgraphs = [(args.n,) + gmm.gmm_pair(args.n, seed=s) for s in range(lo, hi)]
-        else:
-            # the reference's GMM streams, pair loop on the device (gmm_gpu exact mode: the same
-            # graphs as gmm.gmm_pair, outside the timed region)
-            bgraphs = [(args.n,) + e for e in gmm_gpu.gmm_pairs(args.n, range(lo, hi), exact=True, device=gpu)]
-        beng = make_engine(weights)
-        beng.load_graphs(bgraphs)
-        run_steps(beng, 1)
-        sync()
-        tb = time.perf_counter()
-        bk_ms, bl, brem, blast, _ = run_steps(beng, args.batch_steps)
-        sync()
-        belapsed = time.perf_counter() - tb
-        bflops, bbytes, _ = trace_work(beng, len(bgraphs))
-        bmr, bouts = blast
-        baudc = [audc_of(r, m, n) for (n, _, _), m, (_, r) in zip(bgraphs, bmr, bouts)]
-        brem_per_graph = [len(s) for s, _ in bouts]
-        # reference goldens exist for seeds 0-2 (all on rank 0: contiguous shards)
-        gold = golden_checks([bouts[s - lo][0] if lo <= s < hi else None for s in range(3)],
-                             [baudc[s - lo] if lo <= s < hi else None for s in range(3)]) if args.n == 1000 else {}
-        local_graphs = len(bgraphs)
-        if dist is not None:
-            baudc, brem_per_graph = parallel.gather_results(dist, baudc, brem_per_graph, dev)  # RCCL over xGMI
-            belapsed = parallel.max_over_ranks(dist, belapsed, dev)
-            brem = parallel.sum_over_ranks(dist, brem, dev)
-        beng.close()
-        batch = {
-            "workload": "%d 2-layer GMM graphs N=%d (seeds 0..%d, %d per GPU), full rollouts per step"
-                        % (total, args.n, total - 1, args.batch_graphs),
-            "value": brem / belapsed,
-            "unit": "removals/s",
-            "steps": args.batch_steps,
-            "ms_per_step": belapsed / args.batch_steps * 1e3,
-            "removals_per_step": brem / args.batch_steps,
-            "audc_mean": float(np.mean(baudc)),
-            "graphs": len(baudc),
-            "graphs_rank0": local_graphs,
-            "removals_gathered": int(sum(brem_per_graph)),
-            "golden": gold,
-            # per batch step: the queue launch and its tail launch (MD_QPARK) together -- the
-            # algorithmic work and the measured traffic of the whole batch rollout
-            "roofline": roofline(bflops, bbytes, bk_ms / args.batch_steps, 1, None),
-        }
-        batch["roofline"]["per"] = "batch step (queue launch + tail launch)"
-        batch["roofline"]["launches_per_step"] = bl / args.batch_steps
+        batch, baudc, brem = many_graph_object(args, "batch", graphs_of(range(lo, hi)), lo, args.batch_steps, rank,
+                                               world, dist, dev, make_engine, weights, sync, parallel)
+        batch = dict({"workload": "%d 2-layer GMM graphs N=%d (seeds 0..%d, %d per GPU), full rollouts per step"
+                                  % (total, args.n, total - 1, args.batch_graphs)}, **batch)
+        batch["scaling"] = "weak"
         if rank == 0 and args.cpu_dry_run:
             batch["audc_all"] = baudc
-            batch["removals_all"] = brem_per_graph
+            batch["removals_all"] = brem
+
+    # ---------------- C5 object (configs[4]): the same c5_graphs graphs at every world size,
+    # split contiguously over the ranks (strong scaling); one RCCL all-gather of AUDC + counts
+    c5 = None
+    if args.c5_graphs > 0:
+        lo, hi = parallel.shard(args.c5_graphs, rank, world)
+        c5, caudc, crem = many_graph_object(args, "c5", graphs_of(range(lo, hi)), lo, args.c5_steps, rank, world,
+                                            dist, dev, make_engine, weights, sync, parallel)
+        c5 = dict({"workload": "%d 2-layer GMM graphs N=%d (seeds 0..%d) split over %d GPU(s), %d on rank 0, full "
+                               "rollouts per step" % (args.c5_graphs, args.n, args.c5_graphs - 1, world, hi - lo)},
+                  **c5)
+        c5["scaling"] = "strong"
+        c5["gather_complete"] = c5["graphs"] == args.c5_graphs
+        if rank == 0 and args.cpu_dry_run:
+            c5["audc_all"] = caudc
+            c5["removals_all"] = crem
 
     # ---------------- degree-cost variant (configs[3] shape: the D/ agent on a synthetic N=1000
     # multiplex, the GMM seed-0 graph; real testReal inputs are absent), single graph, rank 0
@@ -576,6 +753,14 @@ def rank_main(args):
         import tempfile
         with tempfile.TemporaryDirectory() as td:
             real = real_scale_object(args, make_engine, td)
+
+    # the collectives themselves, checked: a gather of known per-rank data must come back whole
+    dist_check = None
+    if dist is not None:
+        blk = parallel.shard(64, rank, world)
+        ga, gr = parallel.gather_results(dist, [float(i) + 0.5 for i in range(*blk)], list(range(*blk)), dev)
+        dist_check = dict(backend=backend, world=dist.get_world_size(),
+                          gather_ok=ga == [float(i) + 0.5 for i in range(64)] and gr == list(range(64)))
 
     if rank == 0:
         golden = None
@@ -593,12 +778,13 @@ def rank_main(args):
             if q is not None and (extra < 0.5 or tail is not None):
                 batch["roofline"]["traffic"] = q + (extra * tail if extra >= 0.5 else 0.0)
             batch["roofline"]["mfma_busy"] = tb.get("mfma_busy")
+            batch["roofline"]["traffic_note"] = traffic_note
         have = golden is not None and audc is not None
         k = 0
         if have:
             while k < min(len(seq), len(golden["seq"])) and seq[k] == golden["seq"][k]:
                 k += 1
-        rl = roofline(flops, nbytes, kernel_ms / max(1, args.steps), launches / max(1, args.steps),
+        rl = roofline(F, B, kernel_ms / max(1, args.steps), launches / max(1, args.steps),
                       traffic.get("hbm_bytes_per_launch") if traffic else None)
         rl["traffic_note"] = traffic_note
         if traffic:
@@ -626,6 +812,7 @@ def rank_main(args):
             },
             "rccl_world": dist.get_world_size() if dist is not None else 1,
             "backend": backend,
+            "dist_check": dist_check,
             # ranks sharing GPUs (--rehearse-shared-gpu): plumbing rehearsal, the value is not a
             # scaling figure
             "rehearsal_shared_gpu": bool(args.rehearse_shared_gpu),
@@ -638,7 +825,7 @@ def rank_main(args):
             "kernel_ms_per_step": kernel_ms / max(1, args.steps),
             "s0_kernel_ms_per_step": s0_ms / max(1, args.steps),
             "launches_per_step": launches / max(1, args.steps),
-            "predictions_per_step": preds,
+            "predictions_per_step": int(len(F)),
             "pcie_inclusive_value": pcie_rate,
             # K2 end-game picks run in one hand-shake; the same rollouts with one
             # forward pass per removal step, same sequence checked:
@@ -646,6 +833,7 @@ def rank_main(args):
             "per_step_protocol_same_sequence": per_step_same,
             "roofline": rl,
             "batch": batch,
+            "c5": c5,
             "degree": degree,
             "real_scale": real,
             "kernel_src_hash": kernel_src_hash(),
@@ -655,10 +843,13 @@ def rank_main(args):
             cb = cpu_baseline(edges, args.n, args.cpu_sample_seconds)
             line["cpu_baseline"] = cb
             line["vs_cpu_baseline"] = line["value"] / cb["value"]
-            if batch is not None and args.batch_cpu_procs > 0:
+            if batch is not None and args.batch_cpu_procs >= 0:
                 bcb = cpu_baseline_batch(args.n, args.batch_cpu_procs)
                 batch["cpu_baseline"] = bcb
                 batch["vs_cpu_baseline"] = batch["value"] / bcb["value"]
+                if c5 is not None:
+                    c5["vs_cpu_baseline"] = c5["value"] / bcb["value"]
+                    c5["cpu_baseline_note"] = "the batch object's CPU pool (same per-graph work, same generator)"
         print(json.dumps(line), flush=True)
     eng.close()
     if dist is not None:

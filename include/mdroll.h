@@ -167,6 +167,10 @@ md_status md_profile_read(md_ctx* ctx, uint64_t* out, int capacity_steps, int32_
 /* Library build string (arch, version). */
 const char* md_version(void);
 
+/* Number of visible GPUs (0 when there is none or the runtime fails): the agent's
+ * "CUDA: <bool>" line (U/MultiDismantler_torch.py:107, torch.cuda.is_available()). */
+int md_device_count(void);
+
 /* ---------------------------------------------------------------- synthetic graph generator
  * Geometric Multiplex Model (U/GMM.py:6-68 with U/Hyperbolic.py:18-117, g = 0.5, nu = 0.2,
  * gamma = 2.5, T = 0.4, kbar ~ U(2, 10)) on the device, SURVEY.md §8(f3).  Context-free (own
@@ -235,6 +239,8 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *   MD_HOST_STATS     set: print hand-shake timing statistics to stderr
  *   MD_SPEC           speculative environment workgroups of a single-graph rollout (0..32,
  *                     default 16, 0 = off; md_spec_stats)
+ *   MD_MAX_CUS        use at most this many CUs (>= 8; default: all), e.g. for several ranks
+ *                     sharing one GPU, whose persistent grids must be co-resident
  */
 
 #ifdef __cplusplus

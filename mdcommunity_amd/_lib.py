@@ -25,7 +25,7 @@ PROF_SLOTS = 96  # MD_PROF_SLOTS in include/mdroll.h
 EXPORTS = ("md_create", "md_destroy", "md_last_error", "md_set_weights", "md_load_graphs", "md_reset",
            "md_predict", "md_step", "md_rollout", "md_rollout_trace", "md_get_state", "md_set_state",
            "md_set_team_size", "md_set_tie_argsort", "md_last_timing", "md_profile", "md_profile_read",
-           "md_version", "md_spec_stats", "md_gmm_last_error", "md_gmm_nodes", "md_gmm_links")
+           "md_version", "md_device_count", "md_spec_stats", "md_gmm_last_error", "md_gmm_nodes", "md_gmm_links")
 
 _i32p = ctypes.POINTER(ctypes.c_int32)
 _i64p = ctypes.POINTER(ctypes.c_int64)
@@ -75,6 +75,7 @@ def load_library(path=LIB_PATH):
         "md_profile": (ctypes.c_int, [vp, ctypes.c_int]),
         "md_profile_read": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, _i32p]),
         "md_version": (ctypes.c_char_p, []),
+        "md_device_count": (ctypes.c_int, []),
         "md_gmm_last_error": (ctypes.c_char_p, []),
         "md_gmm_nodes": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), _f64p,
                                         _f64p, _f64p, _f64p, _f64p]),
@@ -88,6 +89,11 @@ def load_library(path=LIB_PATH):
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def device_count():
+    """Visible GPUs (md_device_count; 0 without a GPU or when the runtime fails)."""
+    return int(load_library().md_device_count())
 
 
 def _ptr(a, t):

@@ -39,6 +39,9 @@ class MultiDismantler:
         self._engine = None
         self.test_env = MvcEnv(NUM_MAX, cost_mode=self.cost_mode)
         self.model_file = None
+        # the reference constructor's log lines (U/MultiDismantler_torch.py:107,124)
+        print("CUDA:", _lib.device_count() > 0)
+        print("Total number of MultiDismantler_net parameters: {}".format(_lib.MD_WEIGHT_FLOATS))
 
     # ---------------------------------------------------------------- model / graphs
     @property
@@ -140,6 +143,7 @@ class MultiDismantler:
         g = self.TestSet.Get(gid)
         seq, ranks = self._device_rollout(g, step)
         self._replay_scores(g, seq, ranks)
+        print_iterations(len(seq), step)
         return seq, self.test_env.score, self.test_env.MaxCCList
 
     def GetSolBatch(self, graphs, step=1):
@@ -175,6 +179,9 @@ class MultiDismantler:
     # ---------------------------------------------------------------- harnesses
     def Evaluate(self, data_test, data_test_name, data_type, model_file=None, data_root="../../data"):  # noqa: N802
         """testSynthetic harness (:563-600): 20 graphs adj{1,2}_<i>.npy per size."""
+        print("The best model is :%s" % (model_file if model_file is not None
+                                          else _engine.resolve_model(None, self.cost_mode)))
+        sys.stdout.flush()
         self.LoadModel(model_file)
         n_test = 2 if os.getenv("SMOKE_TEST", "0").strip().lower() in ("1", "true", "yes") else 20
         scores, times, costs = [], [], []
@@ -263,6 +270,15 @@ class MultiDismantler:
             fo.write("%.8f\n" % score_std)
         self.ClearTestGraphs()
         return sol, solution_time, score
+
+
+def print_iterations(removals, step):
+    """GetSolution's log (U/MultiDismantler_torch.py:721, D/MultiDismantler_torch.py:692): one
+    ``Iteration:%d`` line per prediction of the loop.  Every prediction but the last applies
+    `step` actions (an iteration stops short only when the graph became terminal), so a rollout
+    of `removals` removals made ceil(removals / step) predictions."""
+    for it in range(-(-removals // step)):
+        print("Iteration:%d" % it)
 
 
 def _edges_in_nx_order(n, order):

@@ -67,6 +67,7 @@ class MultiDismantler(_agent.MultiDismantler):
         g = self.TestSet.Get(gid)
         seq, ranks = self._device_rollout(g, step)
         self._replay_scores(g, seq, ranks)
+        _agent.print_iterations(len(seq), step)
         return seq, self.test_env.score, self.test_env.MaxCCList
 
     def GetSolBatch(self, graphs, step=1):
@@ -91,6 +92,9 @@ class MultiDismantler(_agent.MultiDismantler):
 
     def Evaluate(self, data_test, data_test_name, dirt, model_file=None, data_root="../../data"):  # noqa: N802
         """testSynthetic harness (D/MultiDismantler_torch.py:540-577)."""
+        print("The best model is :%s" % (model_file if model_file is not None
+                                          else _engine.resolve_model(None, self.cost_mode)))
+        sys.stdout.flush()
         self.LoadModel(model_file)
         n_test = 2 if os.getenv("SMOKE_TEST", "0").strip().lower() in ("1", "true", "yes") else 20
         scores, times, costs = [], [], []

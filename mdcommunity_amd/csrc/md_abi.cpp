@@ -508,6 +508,13 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
   p.n_env = n_env;
   p.variant = c->variant;
   p.launch_seq = ++c->launch_seq;
+  if ((c->launch_seq & 0xffffu) == 0) {
+    // speculative-result tags carry the low 16 bits of launch_seq (spec_tag): every 65536
+    // launches the slots are wiped and the all-zero tag value is skipped, so no slot can hold
+    // a tag of an earlier launch that matches this one's
+    p.launch_seq = ++c->launch_seq;
+    if (c->sres.p) HIPCHK(c, hipMemsetAsync(c->sres.p, 0, sizeof(int) * c->sres.n, c->stream));
+  }
   p.run_mode = run_mode;
   p.host_select = host_select;
   const bool hs = sel != nullptr && c->host_mode != 0 && c->h_req.d != nullptr;
@@ -655,6 +662,11 @@ extern "C" {
 
 const char* md_version(void) { return "libmdroll 0.1 (gfx950, HIP " HIP_VERSION_BUILD_NAME ")"; }
 
+int md_device_count(void) {
+  int n = 0;
+  return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
 const char* md_last_error(const md_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 md_status md_create(int device, const float* weights, size_t n_floats, int cost_mode, md_ctx** out) {
@@ -683,6 +695,9 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) { st = MD_EHIP; break; }
     c->cus = prop.multiProcessorCount;
+    // MD_MAX_CUS: use at most this many CUs (one workgroup per CU), e.g. several ranks sharing
+    // one GPU, whose persistent grids must all be resident at once
+    if (const char* v = std::getenv("MD_MAX_CUS")) c->cus = std::max(8, std::min(c->cus, std::atoi(v)));
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { st = MD_EHIP; break; }
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) { st = MD_EHIP; break; }
     if (set_kernel_attrs() != hipSuccess) { st = MD_EHIP; break; }
@@ -925,13 +940,26 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->qslot.alloc(Q_CAP));
   HIPCHK(c, c->qg.alloc(3 * G_CAP));  // stage counter, stage size per graph slot; lists-built flag
   {
-    // speculative-step slots: killed-edge lists of one graph (LDS-mode graphs only)
+    // speculative-step slots: killed-edge lists of one graph, sized by the graphs a single-graph
+    // rollout can run with speculative workgroups (launch_chunk's conditions: the state fits
+    // LDS, word-aligned offsets); none at all when MD_SPEC=0 or no graph qualifies
     int maxw = 0;
-    for (int g = 0; g < n_graphs; ++g) maxw = std::max(maxw, sres_words(info[g].e[0] + info[g].e[1], info[g].n));
+    if (c->spec_n > 0)
+      for (int g = 0; g < n_graphs; ++g) {
+        const int et = info[g].e[0] + info[g].e[1];
+        if (spec_fits_lds_host(info[g].n, et) && info[g].eoff[0] % 4 == 0 && info[g].eoff[1] % 4 == 0 &&
+            info[g].node_off % 4 == 0)
+          maxw = std::max(maxw, sres_words(et, info[g].n));
+      }
     c->sres_stride = ((maxw + 63) / 64) * 64;
-    HIPCHK(c, c->sres.alloc((size_t)SPEC_MAX * c->sres_stride));
-    HIPCHK(c, hipMemset(c->sres.p, 0, sizeof(int) * (size_t)SPEC_MAX * c->sres_stride));
-    HIPCHK(c, c->qspec.alloc(2 * tn));
+    if (maxw > 0) {
+      HIPCHK(c, c->sres.alloc((size_t)SPEC_MAX * c->sres_stride));
+      HIPCHK(c, hipMemset(c->sres.p, 0, sizeof(int) * (size_t)SPEC_MAX * c->sres_stride));
+      HIPCHK(c, c->qspec.alloc(2 * tn));
+    } else {
+      c->sres.release();
+      c->qspec.release();
+    }
   }
   {
     int maxn = 0;
@@ -1044,6 +1072,7 @@ md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, i
   std::vector<float> qrow;
   std::vector<double> qd;
   std::vector<int32_t> acts;
+  std::vector<std::pair<int, int>> before;
   while (!gl.empty()) {
     md_status st = push_vars(c);
     if (st != MD_OK) return st;
@@ -1051,13 +1080,19 @@ md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, i
     sel.cb = cb;
     sel.user = user;
     sel.step = step;
+    before.resize(c->ng);
+    for (int g : gl) before[g] = {c->hvar[g].steps, c->hvar[g].npred};
     st = launch(c, gl, RUN_ROLLOUT, host_select, &sel);
     if (st != MD_OK) return st;
     std::vector<int> next;
     for (int g : gl) {
       GraphVar& v = c->hvar[g];
       if (v.status == ST_RUN) {
-        // left by a queue-mode launch at its tail: the next launch continues it
+        // left by a queue-mode launch at its tail: the next launch continues it -- a launch
+        // always advances a graph it leaves running (it parks only after an environment step),
+        // so an unchanged graph would be relaunched forever
+        if (before[g] == std::make_pair(v.steps, v.npred))
+          return fail(c, MD_ESTATE, "graph %d: a rollout launch left it running without progress", g);
         v.npend = 0;
         next.push_back(g);
         continue;

@@ -16,7 +16,7 @@ HEADER = os.path.join(ROOT, "include", "mdroll.h")
 
 def header_symbols():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:md_status|void|const char\*)\s+(md_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:md_status|void|int|const char\*)\s+(md_\w+)\s*\(", txt, re.M)))
 
 
 @pytest.fixture(scope="module")
@@ -42,6 +42,7 @@ def test_version_and_no_gpu_errors(lib):
     assert bad == _lib.MD_EINVAL  # wrong weight count is rejected before any HIP call
     assert lib.md_reset(None, None) == _lib.MD_EINVAL
     assert lib.md_last_error(None) == b"null context"
+    assert lib.md_device_count() == 0  # no GPU in the build container
 
 
 def test_library_is_gfx950_code_object():

@@ -105,8 +105,8 @@ def test_bench_launcher_world2_gathers_like_one_process():
     batch seeds, gather per-graph AUDC and removal counts and take the max time over ranks —
     through the bench's own launcher, rank body, shard and gather code (gloo + the host stub
     engine in place of the device).  The gathered lists must equal a one-process run."""
-    two = _bench("--gpus", "2", "--batch-graphs", "3")
-    one = _bench("--gpus", "1", "--batch-graphs", "6")
+    two = _bench("--gpus", "2", "--batch-graphs", "3", "--c5-graphs", "5")
+    one = _bench("--gpus", "1", "--batch-graphs", "6", "--c5-graphs", "5")
     assert two["n_gpus"] == 2 and two["rccl_world"] == 2 and two["backend"] == "gloo"
     assert one["n_gpus"] == 1 and one["rccl_world"] == 1
     b2, b1 = two["batch"], one["batch"]
@@ -115,6 +115,14 @@ def test_bench_launcher_world2_gathers_like_one_process():
     assert b2["removals_per_step"] == sum(b1["removals_all"])
     # weak scaling of the headline: each rank runs its own replica
     assert two["config"]["removals_per_step"] == 2 * one["config"]["removals_per_step"]
+    # C5 (configs[4]) is strong-scaled: the same graphs at both world sizes, split over the ranks
+    c2, c1 = two["c5"], one["c5"]
+    assert c2["scaling"] == c1["scaling"] == "strong"
+    assert c2["graphs"] == c1["graphs"] == 5 and c2["graphs_rank0"] == 3 and c1["graphs_rank0"] == 5
+    assert c2["gather_complete"] and c1["gather_complete"]
+    assert c2["audc_all"] == c1["audc_all"] and c2["removals_all"] == c1["removals_all"]
+    assert c2["removals_per_step"] == c1["removals_per_step"]
+    assert two["dist_check"] == {"backend": "gloo", "world": 2, "gather_ok": True}
 
 
 @pytest.mark.timeout(300)
@@ -125,3 +133,43 @@ def test_batch_cpu_baseline_pool():
     cb = bench.cpu_baseline_batch(60, 2, graphs_per_proc=1)
     assert cb["cores"] == 2 and cb["kind"] == "port" and cb["value"] > 0
     assert "2 GMM N=60 graphs" in cb["sample"]
+
+
+@pytest.mark.timeout(300)
+def test_bench_launcher_fails_fast_when_a_rank_dies():
+    """A rank that dies must not leave the others blocked in a collective until the driver's time
+    limit: the launcher polls every rank, stops the siblings on the first non-zero exit and
+    returns that status (rank 1 exits with 3 right after init; rank 0 would wait at its first
+    barrier for the process group's 600 s timeout)."""
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--cpu-dry-run", "--gpus", "2", "--fail-rank", "1",
+           "--n", "40", "--steps", "1", "--warmup", "0", "--batch-graphs", "2", "--c5-graphs", "0",
+           "--degree-steps", "0", "--no-cpu-baseline", "--real-steps", "0"]
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    t0 = time.time()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    dt = time.time() - t0
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert "rank 1 exited with status 3" in r.stderr
+    assert dt < 120, dt
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_available_cpus_and_roofline():
+    import numpy as np
+    import bench
+    n, how = bench.available_cpus()
+    assert 1 <= n <= (os.cpu_count() or n) and "affinity" in how
+    # SURVEY.md §8(d): per-prediction max of the two roofs, bound = the dominating roof
+    F = np.array([157.3e12 * 1e-6, 157.3e12 * 4e-6])   # 1 us, 4 us of MFMA time
+    B = np.array([8e12 * 3e-6, 8e12 * 1e-6])           # 3 us, 1 us of HBM time
+    rl = bench.roofline(F, B, kernel_ms_per_step=0.014, launches_per_step=1, traffic=None)
+    assert abs(rl["roofline_ms_per_step"] - 0.007) < 1e-12
+    assert abs(rl["roofline_time_frac"] - 0.5) < 1e-9
+    assert rl["bound"] == "mfma" and rl["unit"] == "TFLOP/s"   # 4 us of MFMA-bound terms vs 3 us HBM
+    assert abs(rl["frac"] - 5e-6 / 14e-6) < 1e-9 and abs(rl["hbm_frac"] - 4e-6 / 14e-6) < 1e-9
+    assert rl["predictions_hbm_bound"] == 1 and rl["predictions_mfma_bound"] == 1
