@@ -288,7 +288,7 @@ def available_cpus():
     return n, how
 
 
-def cpu_baseline_batch(n, procs_wanted=0, graphs_per_proc=1):
+def cpu_baseline_batch(n, procs_wanted=0, graphs_per_proc=8):
     """BASELINE.md §3 / SURVEY.md §8(d): the batch workload on the CPU as P independent
     1-thread oracle processes (embarrassingly parallel over graphs), P = the CPUs available to
     this job (available_cpus) unless `procs_wanted` > 0, on a bounded sample of the batch's

@@ -1073,6 +1073,7 @@ md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, i
   std::vector<double> qd;
   std::vector<int32_t> acts;
   std::vector<std::pair<int, int>> before;
+  std::vector<int> stalled(c->ng, 0);
   while (!gl.empty()) {
     md_status st = push_vars(c);
     if (st != MD_OK) return st;
@@ -1088,11 +1089,17 @@ md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, i
     for (int g : gl) {
       GraphVar& v = c->hvar[g];
       if (v.status == ST_RUN) {
-        // left by a queue-mode launch at its tail: the next launch continues it -- a launch
-        // always advances a graph it leaves running (it parks only after an environment step),
-        // so an unchanged graph would be relaunched forever
-        if (before[g] == std::make_pair(v.steps, v.npred))
-          return fail(c, MD_ESTATE, "graph %d: a rollout launch left it running without progress", g);
+        // left by a queue-mode launch at its tail: the next launch continues it.  A graph
+        // admitted late may be parked right after its first environment step, which removes
+        // nothing and predicts nothing, but the launch after a park (at most MD_QPARK graphs:
+        // the lock-step kernel, which never parks) always advances it -- a second launch in a
+        // row without progress would mean a graph relaunched forever
+        if (before[g] == std::make_pair(v.steps, v.npred)) {
+          if (++stalled[g] >= 2)
+            return fail(c, MD_ESTATE, "graph %d: two rollout launches in a row left it running without progress", g);
+        } else {
+          stalled[g] = 0;
+        }
         v.npend = 0;
         next.push_back(g);
         continue;
