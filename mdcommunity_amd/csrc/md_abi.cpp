@@ -114,6 +114,7 @@ struct md_ctx {
   DevBuf<unsigned long long> xbuf;
   DevBuf<int> nbc;  // neighbour-list cache slots (tiles of the largest launch)
   int nbc_slots = 0, nbc_gstride = 0;
+  int max_tiles = 0;  // tiles of the largest loaded graph
   DevBuf<unsigned long long> qslot;  // queue-mode work items
   DevBuf<int> qg;                    // queue-mode per-graph stage counters
   // speculative environment steps (single-graph rollouts): result slots, Q of the last two
@@ -437,6 +438,12 @@ void serve_request(md_ctx* c, Selector* sel, int g, unsigned tag, std::vector<do
   __atomic_store_n(c->h_ans.h + g, tag, __ATOMIC_RELEASE);
 }
 
+// Whole-batch rollouts run through the device work queue (MD_VARIANT bit 32: the lock-step
+// shared mode instead) when every loaded graph fits the work items' tile field.
+bool queue_mode_ok(const md_ctx* c, int run_mode) {
+  return run_mode == RUN_ROLLOUT && !(c->variant & 32) && c->max_tiles < Q_MAX_TILES;
+}
+
 md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int host_select, Selector* sel) {
   std::vector<int> v(gl_in, gl_in + ngl);
   // graphs with more edges first: the queue's first round-robin positions go to the longest
@@ -454,7 +461,7 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
   const bool team_env = ngl == 1 && !(c->variant & 2) &&
                         (!phase_a_fits_lds_host(c->hinfo[gl[0]].n, c->hinfo[gl[0]].e[0] + c->hinfo[gl[0]].e[1]) ||
                          (c->variant & 64));
-  const bool qmode = run_mode == RUN_ROLLOUT && n_env == 0 && !(c->variant & 32) && !team_env;
+  const bool qmode = queue_mode_ok(c, run_mode) && n_env == 0 && !team_env;
   const int grid = qmode ? c->cus : grid_size(c, v, n_env);
   // speculative environment workgroups on the CUs a single-graph rollout leaves free
   // (single-node steps only: step > 1 takes several removals per prediction)
@@ -628,8 +635,11 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
 
 md_status launch(md_ctx* c, const std::vector<int>& gl, int run_mode, int host_select, Selector* sel = nullptr) {
   c->vars_stale = false;
-  for (size_t i = 0; i < gl.size(); i += G_CAP) {
-    const int k = (int)std::min<size_t>(G_CAP, gl.size() - i);
+  // a queue-mode batch runs in one launch of up to QG_CAP graphs (one launch tail instead of
+  // one per G_CAP chunk); lock-step launches take G_CAP
+  const size_t cap = queue_mode_ok(c, run_mode) && gl.size() > (size_t)DEDICATED_MAX_GRAPHS ? QG_CAP : G_CAP;
+  for (size_t i = 0; i < gl.size(); i += cap) {
+    const int k = (int)std::min<size_t>(cap, gl.size() - i);
     md_status st = launch_chunk(c, gl.data() + i, k, run_mode, host_select, sel);
     if (st != MD_OK) {
       (void)pull_vars(c);
@@ -904,14 +914,15 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->hbuf.alloc((size_t)n_graphs * 144 * 2));
   HIPCHK(c, c->xbuf.alloc((size_t)XB_SLOTS * 2048));
   {
-    // cache slots: the tiles of the largest possible launch (the G_CAP graphs with most tiles)
-    // (queue mode addresses slot = graph slot * max tiles + tile, the lock-step modes the
-    // launch's tile prefix index: both < min(graphs, G_CAP) * max tiles)
+    // cache slots: one per tile of the loaded graphs (queue mode addresses the graph's own
+    // tiles, tile_off + tile; the lock-step modes the launch's tile prefix index, which is
+    // below the launch's tile count)
     long maxt = 1;
     for (int g = 0; g < n_graphs; ++g) maxt = std::max<long>(maxt, (n_nodes[g] + TILE - 1) / TILE);
-    const long slots = (long)std::min(n_graphs, G_CAP) * maxt;
+    const long slots = (long)tt;
     c->nbc_slots = (int)slots;
     c->nbc_gstride = (int)maxt;
+    c->max_tiles = (int)maxt;
     HIPCHK(c, c->nbc.alloc((size_t)std::max<long>(1, slots) * NBC_INTS));
   }  // split tiles of a launch <= CUs / 2 <= XB_SLOTS
   HIPCHK(c, c->h_req.alloc((size_t)n_graphs));
@@ -938,7 +949,7 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, hipStreamSynchronize(c->stream));
   // queue-mode buffers last (allocation order moves the other buffers' addresses)
   HIPCHK(c, c->qslot.alloc(Q_CAP));
-  HIPCHK(c, c->qg.alloc(3 * G_CAP));  // stage counter, stage size per graph slot; lists-built flag
+  HIPCHK(c, c->qg.alloc(3 * QG_CAP));  // stage counter, stage size per graph slot; lists-built flag
   {
     // speculative-step slots: killed-edge lists of one graph, sized by the graphs a single-graph
     // rollout can run with speculative workgroups (launch_chunk's conditions: the state fits

@@ -15,6 +15,11 @@ constexpr int BP_ITERS = 3;      // max_bp_iter, :62
 constexpr int NTHREADS = 512;    // 8 waves: waves 0-3 work on layer 0, waves 4-7 on layer 1
 constexpr int TILE = 16;         // node rows per MFMA tile (v_mfma_f32_16x16x4_f32)
 constexpr int G_CAP = 512;       // graphs per kernel launch (the host chunks larger batches)
+// queue-mode launches (whole-batch rollouts) take up to QG_CAP graphs: a work item holds a
+// 12-bit graph slot and a 13-bit first tile (graphs of < Q_MAX_TILES tiles; a batch with a
+// larger graph runs in the lock-step kernel)
+constexpr int QG_CAP = 4096;
+constexpr int Q_MAX_TILES = 8192;
 constexpr int PROF_SLOTS = 96;
 constexpr int NB_CAP_ENTRIES = 2052;   // alive neighbour entries per layer kept for a tile (NB_CAP)
 // neighbour-list cache slot: header (off[2][16], cnt[2][16], tot[2], ok) then per layer the u16

@@ -2094,23 +2094,26 @@ __device__ __forceinline__ int tile_graph(const int* pref, int ng, int t) {
 enum : unsigned { QK_ENV = 1, QK_TILE = 2, QK_VN = 3, QK_EXIT = 4 };
 enum : int { QC_HEAD = 0, QC_TAIL = 1, QC_REM = 2, QC_ADMIT = 3 };
 // Graphs running at once in queue mode: the larger of 3/8 of the workgroups and 5/16 of the
-// launch's graphs (sweeps of 64..192 and all: 96 best for 256 GMM N=1000 graphs on 256 CUs,
-// 160 for 512).  MD_VARIANT bits 16+ override.
+// launch's graphs, the latter at most Q_ADMIT_MAX (sweeps of 64..192 and all: 96 best for 256
+// GMM N=1000 graphs on 256 CUs, 160 for 512; for 4096-graph launches see DESIGN.md).
+// MD_VARIANT bits 16+ override.
+constexpr int Q_ADMIT_MAX = 160;
 __device__ __forceinline__ int q_admit(KParams& p) {
   const int v = (int)((unsigned)p.variant >> 16);
-  return v > 0 ? v : max(1, max((int)(3 * gridDim.x) / 8, (5 * p.nglist) / 16));
+  return v > 0 ? v : max(1, max((int)(3 * gridDim.x) / 8, min(Q_ADMIT_MAX, (5 * p.nglist) / 16)));
 }
 __device__ __forceinline__ unsigned q_item(unsigned kind, int it, int gl, int j) {
-  return kind | ((unsigned)it << 3) | ((unsigned)gl << 5) | ((unsigned)j << 15);
+  return kind | ((unsigned)it << 3) | ((unsigned)gl << 5) | ((unsigned)j << 17);
 }
+__device__ __forceinline__ int q_item_gl(unsigned item) { return (int)((item >> 5) & (QG_CAP - 1)); }
 // Tile item i of a stage with nt tiles and tpi tiles per item: first tile j = i * tpi (bits
-// 15-29), the number of further tiles in bits 30-31 (they run back to back on one workgroup:
+// 17-29, < Q_MAX_TILES), the number of further tiles in bits 30-31 (they run back to back on one workgroup:
 // one stage signal and one pop for all of them).
 __device__ __forceinline__ unsigned q_item_tile(int it, int gl, int i, int nt, int tpi) {
   const int j = i * tpi, extra = min(tpi, nt - j) - 1;
   return q_item(QK_TILE, it, gl, j) | ((unsigned)extra << 30);
 }
-__device__ __forceinline__ int q_item_j(unsigned item) { return (int)((item >> 15) & 0x7fffu); }
+__device__ __forceinline__ int q_item_j(unsigned item) { return (int)((item >> 17) & (Q_MAX_TILES - 1)); }
 __device__ __forceinline__ int q_item_extra(unsigned item) { return (int)(item >> 30); }
 // Tiles per item: 2 (MD_VARIANT bits 9-10 = 1..3 override; sweep of 1..4 tiles x admission
 // 96..160 on 256 / 512 graphs: 2 best, -3 % / -5 % against 1).  Per-graph stage size word in
@@ -2224,7 +2227,7 @@ __device__ __noinline__ bool env_build_lists(KParams&, const GraphInfo gi, int g
   const EnvLayout Lo = env_layout(n, et);
   const EnvView<false> E = env_view<false>(p, gi, ia);
   const int nl = ((const GraphVar*)(lds + L_GV))->n_live, nt = (nl + TILE - 1) / TILE;
-  if (Lo.total + 3 * nl + 2 * nt + 8 > A_WORDS || gl * p.nbc_gstride + nt > p.nbc_slots || nl <= 0) return false;
+  if (Lo.total + 3 * nl + 2 * nt + 8 > A_WORDS || gi.tile_off + nt > p.nbc_slots || nl <= 0) return false;
   // scratch after the environment: node of each live position, per-position prefixes of the
   // CSR extent and of the alive count (nl + 1 each), per-tile alive totals of both layers
   int* pn = ia + Lo.total;
@@ -2232,7 +2235,7 @@ __device__ __noinline__ bool env_build_lists(KParams&, const GraphInfo gi, int g
   int* pd = px + nl + 1;
   int* tt = pd + nl + 1;
   int* tmp = E.tmp;
-  int* base_slot = p.nbc + (size_t)gl * p.nbc_gstride * NBC_INTS;
+  int* base_slot = p.nbc + (size_t)gi.tile_off * NBC_INTS;
   {
     // live positions (ascending ids, as the live list)
     const int chunk = (n + NTHREADS - 1) / NTHREADS;
@@ -2386,7 +2389,7 @@ __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int
       tqd = now_;                                                 \
     }                                                             \
   } while (0)
-  const int slot = gl * p.nbc_gstride + j;
+  const int slot = p.ginfo[g].tile_off + j;  // neighbour-list cache slot: the graph's tile
   const bool cacheable = slot < p.nbc_slots && !(p.variant & 16);
   // iteration 1: the environment item built this step's lists when its flag says so (read in
   // the same round trip as the speculative reload)
@@ -2396,7 +2399,7 @@ __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int
     const int* src = p.nbc + (size_t)slot * NBC_INTS;
     cw = ldc(src + NBC_HDR + (threadIdx.x >> 8) * NBC_LWORDS + (threadIdx.x & 255));
     if (threadIdx.x < 67) ch = ldc(src + threadIdx.x);
-    if (it == 1 && threadIdx.x == 67) built = ldc(p.qg + 2 * G_CAP + gl);
+    if (it == 1 && threadIdx.x == 67) built = ldc(p.qg + 2 * QG_CAP + gl);
   }
   if (threadIdx.x < TILE) {
     const int r = j * TILE + threadIdx.x;
@@ -3101,7 +3104,7 @@ __device__ __noinline__ void queue_pair(KParams&, float* lds, int g, int gl, int
     }                                                             \
   } while (0)
   const int t = threadIdx.x;
-  const int slot0 = gl * p.nbc_gstride + j;
+  const int slot0 = p.ginfo[g].tile_off + j;  // neighbour-list cache slots: the graph's tiles
   const int nbo[2] = {0, P2_NB1 - S_NBH};
   bool cacheable[2], want[2];
 #pragma unroll
@@ -3117,7 +3120,7 @@ __device__ __noinline__ void queue_pair(KParams&, float* lds, int g, int gl, int
     if (want[b]) cw[b] = ldc(p.nbc + (size_t)(slot0 + b) * NBC_INTS + NBC_HDR + (t >> 8) * NBC_LWORDS + (t & 255));
   const int hb = t >> 7, hi = t & 127;
   if (hb < 2 && hi < 67 && want[hb]) ch = ldc(p.nbc + (size_t)(slot0 + hb) * NBC_INTS + hi);
-  if (it == 1 && t == 67 && (want[0] || want[1])) built = ldc(p.qg + 2 * G_CAP + gl);
+  if (it == 1 && t == 67 && (want[0] || want[1])) built = ldc(p.qg + 2 * QG_CAP + gl);
   if (t < 2 * TILE) {
     const int r = j * TILE + t;
     lds_i32* hdr = (lds_i32*)(int*)(scr + S_NBH + nbo[t >> 4]);
@@ -3244,12 +3247,20 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
   int* bc = misc + 48;
   const int ng = p.nglist;
   if (blockIdx.x == 0) {
-    // the running graphs start with an environment step (no prediction yet)
-    int* run = (int*)(lds + L_PREF);
-    const int mine = (int)threadIdx.x < ng && ldc(&p.gvar[p.glist[threadIdx.x]].status) == ST_RUN;
+    // the running graphs start with an environment step (no prediction yet); their slots in
+    // order (up to QG_CAP) in the scratch's S_M region, unused before the first item
+    int* run = (int*)(lds + L_SCR + S_M);
+    static_assert(2 * 128 * LDT >= QG_CAP, "running-slot list must fit S_M");
     int tot = 0;
-    const int at = block_excl_scan(mine, (int*)(lds + L_SCR + S_RED), &tot);
-    if (mine) run[at] = threadIdx.x;
+    for (int base = 0; base < ng; base += NTHREADS) {
+      const int s = base + (int)threadIdx.x;
+      const int mine = s < ng && ldc(&p.gvar[p.glist[s]].status) == ST_RUN;
+      int cnt = 0;
+      const int at = block_excl_scan(mine, (int*)(lds + L_SCR + S_RED), &cnt);
+      if (mine) run[tot + at] = s;
+      tot += cnt;
+      __syncthreads();
+    }
     // admission: the first q_admit(p) running graphs (graph slots are ordered longest rollout
     // first) start now; every graph that stops admits the next one, so the long rollouts do
     // not wait behind the whole batch's backlog at every stage
@@ -3314,7 +3325,7 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
       atomicAdd(qp + 8 + (kind & 7u), 1ull);
     }
     if (kind == QK_EXIT || kind == 0u) break;
-    const int it = (int)((item >> 3) & 3u), gl = (int)((item >> 5) & 1023u), j = q_item_j(item);
+    const int it = (int)((item >> 3) & 3u), gl = q_item_gl(item), j = q_item_j(item);
     const int g = p.glist[gl];
     if (kind == QK_ENV) {
 #ifdef MD_QPROF
@@ -3368,7 +3379,7 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
 #endif
         if (threadIdx.x == 0) {
           stc(p.qg + 2 * gl + 1, ni | (nt << 16) | (tpi << 28));
-          stc(p.qg + 2 * G_CAP + gl, built ? 1 : 0);
+          stc(p.qg + 2 * QG_CAP + gl, built ? 1 : 0);
         }
         q_push(p, ni, [&](int i) { return q_item_tile(1, gl, i, nt, tpi); }, bc);
       } else if (st == ST_WAIT_HOST) {

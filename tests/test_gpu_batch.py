@@ -157,3 +157,27 @@ def test_multi_node_steps_batch_tail_handoff(graphs, weights, monkeypatch):
     single, _ = run("0", False)
     assert launches >= 2
     assert parked == whole == single
+
+
+@pytest.mark.timeout(300)
+def test_c5_4096_graphs_one_queue_launch(weights, graphs):
+    """configs[4] at one GPU: all 4096 graphs (seeds 0..4095, the reference's GMM streams made by
+    the device generator in exact mode) in ONE queue launch of QG_CAP graphs (+ its lock-step
+    tail launch) -- per graph the same rollouts as 512-graph launches of the same graphs (seeds
+    0..511 of which test_c5_slice_512 checks against single-graph rollouts), goldens for 0-2."""
+    from mdcommunity_amd import gmm_gpu
+    big = [(N,) + tuple(e) for e in gmm_gpu.gmm_pairs(N, range(4096), exact=True, device=0)]
+    for s in range(0, 4096, 997):  # the device generator reproduces the host's graphs
+        e0, e1 = gmm.gmm_pair(N, seed=s)
+        assert np.array_equal(big[s][1], e0) and np.array_equal(big[s][2], e1)
+    mr, outs, launches = batch_rollout(weights, big)
+    assert launches == 2
+    check_goldens(mr, outs)
+    bad = []
+    for lo in range(0, 4096, 512):
+        cmr, couts, _ = batch_rollout(weights, big[lo:lo + 512])
+        for i, ((seq, ranks), m) in enumerate(zip(couts, cmr)):
+            o = outs[lo + i]
+            if int(m) != int(mr[lo + i]) or seq.tolist() != o[0].tolist() or ranks.tolist() != o[1].tolist():
+                bad.append(lo + i)
+    assert not bad, f"{len(bad)} graphs differ between the 4096-graph launch and 512-graph launches: {bad[:10]}"
