@@ -171,7 +171,9 @@ def test_c5_4096_graphs_one_queue_launch(weights, graphs):
         e0, e1 = gmm.gmm_pair(N, seed=s)
         assert np.array_equal(big[s][1], e0) and np.array_equal(big[s][2], e1)
     mr, outs, launches = batch_rollout(weights, big)
-    assert launches == 2
+    # (+ a lock-step tail launch when graphs were parked: with 4096 graphs the last ones often
+    # end through their K2 end-game hand-shakes before any is parked)
+    assert launches in (1, 2)
     check_goldens(mr, outs)
     bad = []
     for lo in range(0, 4096, 512):
