@@ -91,7 +91,9 @@ def oracle_case(traj, name, cost):
     meta = dict(removals=int(len(seq)), predictions=int(npred), step=step, max_rank=int(g.max_rank),
                 ranks_equal=bool(np.array_equal(oranks, ranks)), score=float(env.score),
                 oracle_seconds=round(time.time() - t0, 1),
-                min_gap=float(np.min(gap)), picks_below_max=int(np.sum(qpick < np.repeat(qmax, step)[:len(seq)])))
+                min_gap=float(np.min(gap)),
+                # step 1: picks below the oracle's max; step k: picks below the oracle's k-th value
+                picks_below_band=int(np.sum(qpick < np.repeat(kth if step > 1 else qmax, step)[:len(seq)])))
     return out, meta
 
 
@@ -118,7 +120,7 @@ def reference_rows(variant, edges_path, seqs):
         env = agent.test_env
         env.s0(g)
         rows = []
-        for t in range(REF_PREDICTIONS):
+        for t in range(min(REF_PREDICTIONS, -(-len(seq) // step))):
             q = agent.PredictWithCurrentQNet([env.graph], [env.action_list], [env.remove_edge])[0]
             rows.append(np.asarray(q, np.float64))
             for a in seq[t * step:(t + 1) * step]:
@@ -157,13 +159,15 @@ def main():
             with np.load(rp) as z:
                 for name in z.files:
                     ref = z[name]
-                    orc = fixture[f"{name}_qrows"][:len(ref)].astype(np.float64)
+                    orc = fixture[f"{name}_qrows"][:len(ref)]
                     live = ref != MASK
-                    d = float(np.max(np.abs(ref[live] - fixture[f"{name}_qrows"][:len(ref)][live].astype(np.float64))))
                     same_mask = bool(np.array_equal(live, orc != np.float32(MASK)))
+                    d = float(np.max(np.abs(ref[live] - orc[live].astype(np.float64))))
+                    bit = bool(np.array_equal(ref.astype(np.float32), orc))
                     fixture[f"{name}_refrows"] = ref.astype(np.float32)
-                    meta["cases"][name].update(ref_vs_oracle_max_abs=d, ref_vs_oracle_same_mask=same_mask)
-                    print(name, "reference vs oracle: max |dQ|", d, "same mask", same_mask, flush=True)
+                    meta["cases"][name].update(ref_predictions=int(len(ref)), ref_vs_oracle_max_abs=d,
+                                               ref_vs_oracle_same_mask=same_mask, ref_vs_oracle_bitexact_f32=bit)
+                    print(name, "reference vs oracle: max |dQ|", d, "same mask", same_mask, "bit-exact", bit, flush=True)
     np.savez_compressed(os.path.join(HERE, "real_scale_certs.npz"), **fixture)
     with open(os.path.join(HERE, "meta_real_scale.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)

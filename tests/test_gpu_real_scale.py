@@ -13,11 +13,18 @@ through the host hand-shake).  Checked against the oracle:
   the graph without the first k + 1 removed nodes, computed from scratch: the fixed point
   only gets finer as nodes are removed, so it does not depend on the path);
 * the sequence is a permutation prefix that ends terminal, and with stepRatio 0.01 each
-  prediction's picks are the host's np.argsort(-q)[:180] of the device's own Q.
+  prediction's picks are the host's np.argsort(-q)[:180] of the device's own Q;
+* whole sequences are certified against tests/golden/real_scale_certs.npz
+  (tests/golden/make_real_scale_certs.py: the oracle teacher-forced along the device's
+  sequences, and the reference itself for the first predictions): LMCC trace and score
+  bit-exact at every removal, every pick inside the oracle's near-tie band, Q within 1e-5 of
+  the oracle's and of the reference's rows.
 """
+import os
 import numpy as np
 import pytest
 
+from conftest import GOLDEN
 from mdcommunity_amd import _lib, agent, engine, graph as mgraph, synth
 from oracle import refenv, refmodel
 
@@ -118,5 +125,85 @@ def test_real_scale_step_ratio(real):
         for t, r in enumerate(rows):
             picks = np.argsort(-r)[:step].tolist()
             assert seq[t * step:(t + 1) * step].tolist() == picks[: len(seq[t * step:(t + 1) * step])], t
+    finally:
+        eng.close()
+
+
+Q_TOL = 1e-5  # north_star: Q within 1e-5
+CERT_CASES = {  # fixture case: (cost mode, checkpoint, step) as scripts/dump_real_scale.py ran them
+    "deg_step1": (_lib.MD_COST_DEGREE, engine.DEFAULT_DEGREE, 1),
+    "unit_step1": (_lib.MD_COST_UNIT, engine.DEFAULT_UNIT_REAL, 1),
+    "unit_ratio0.01": (_lib.MD_COST_UNIT, engine.DEFAULT_UNIT_REAL, max(int(0.01 * N), 1)),
+}
+
+
+@pytest.fixture(scope="module")
+def certs():
+    with np.load(os.path.join(GOLDEN, "real_scale_certs.npz")) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", list(CERT_CASES))
+def test_real_scale_certified_whole_sequence(real, certs, name):
+    """C4 at real size (U/MultiDismantler_torch.py:645-709,676-679; D/MultiDismantler_torch.py:
+    623-681): the device rollout of the N = 18 000 multiplex is the certified sequence, its LMCC
+    trace and score equal the oracle's at every removal (bit-exact), every pick lies in the
+    oracle's near-tie band (a pick the oracle ranks below its max -- or, with 180 picks per
+    prediction, below its 180th value -- by more than 2 x Q_TOL would be a wrong decision), and
+    the device's Q at the first predictions is within Q_TOL of the oracle's and the reference's."""
+    e0, e1, g = real
+    cost, ckpt, step = CERT_CASES[name]
+    c = {k[len(name) + 1:]: v for k, v in certs.items() if k.startswith(name + "_")}
+    eng = _lib.Engine(engine.load_weights(ckpt), cost_mode=cost)
+    try:
+        gg = mgraph.Graph_test.from_edges(N, e0, e1)
+        nw = None
+        if cost == _lib.MD_COST_DEGREE:
+            mgraph.ensure_degree_weights(gg)
+            nw = mgraph.node_weight_array([gg])
+        eng.load_graphs([(N, e0, e1)], node_w=nw)
+        mr = int(eng.reset()[0])
+        assert mr == int(c["max_rank"]) == g.max_rank
+        seq, ranks = eng.rollout(step=step)[0]
+        # the device is deterministic: the certificate is for exactly this sequence
+        assert seq.tolist() == c["seq"].tolist()
+        assert ranks.tolist() == c["ranks"].tolist() == c["oracle_ranks"].tolist()
+        score = 0.0
+        if cost == _lib.MD_COST_DEGREE:  # D/mvc_env.py:127-134
+            tw0, tw1 = sum(gg.weights[0].values()), sum(gg.weights[1].values())
+            for a, r in zip(seq.tolist(), ranks.tolist()):
+                score += -1 * (-int(r) / (mr) * (gg.weights[0][a] / tw0 + gg.weights[1][a] / tw1) / 2.0)
+        else:  # U/mvc_env.py:86,133-137
+            for r in ranks.tolist():
+                score += -1 * (-float(r) / (mr * float(N)))
+        assert score == float(c["oracle_score"])
+        # every pick inside the oracle's near-tie band
+        band = np.repeat(c["kth"] if step > 1 else c["qmax"], step)[:len(seq)]
+        margin = band - c["qpick"]
+        assert float(np.max(margin)) <= 2 * Q_TOL, (int(np.argmax(margin)), float(np.max(margin)))
+        if step == 1:
+            # and exactly the oracle's arg-max wherever the oracle's top-2 gap leaves no doubt
+            clear = c["gap"] > 2 * Q_TOL
+            assert np.all(margin[clear] == 0.0)
+        # Q rows, teacher-forced along the sequence: oracle (first Q_ROWS predictions) and the
+        # reference itself (first predictions)
+        eng.reset()
+        dq_o = dq_r = 0.0
+        for t in range(len(c["qrows"])):
+            q, _, _, _ = eng.predict()
+            live = np.isfinite(q)
+            for rows, which in ((c["qrows"], "o"), (c["refrows"], "r")):
+                if t < len(rows):
+                    ref = rows[t].astype(np.float64)
+                    assert np.array_equal(live, ref != np.float32(refenv.MASK)), (which, t)
+                    d = float(np.max(np.abs(q[live].astype(np.float64) - ref[live])))
+                    if which == "o":
+                        dq_o = max(dq_o, d)
+                    else:
+                        dq_r = max(dq_r, d)
+            for a in seq[t * step:(t + 1) * step]:
+                eng.step(np.asarray([a], np.int32))
+        assert dq_o < Q_TOL and dq_r < Q_TOL, (dq_o, dq_r)
     finally:
         eng.close()
