@@ -27,7 +27,7 @@ import sqlite3
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-KERNELS = {"single": "md_rollout_kernel", "batch": "md_queue_kernel"}
+KERNELS = {"single": "md_rollout_kernel", "batch": "md_queue_kernel", "c5": "md_queue_kernel"}
 CUS, SIMDS, XCDS, PEAK_TF = 256, 4, 8, 157.3
 
 
@@ -81,7 +81,7 @@ def workload(d, w, lines):
             if kernel in k:
                 out["avg_ns"] = v["avg_ns"]
     vals = {}
-    for group in ("fetch", "write", "sq1", "sq2"):
+    for group in ("fetch", "write", "sq1", "sq2", "sq3"):
         for path in dbs(os.path.join(d, f"pmc_{group}_{w}")):
             for c, v in pmc(path, kernel).items():
                 vals[c] = v
@@ -125,7 +125,8 @@ def workload(d, w, lines):
         if m.get("SQ_LDS_IDX_ACTIVE"):
             busy["lds_bank_conflict_frac"] = (m.get("SQ_LDS_BANK_CONFLICT") or 0.0) / m["SQ_LDS_IDX_ACTIVE"]
         for c in ("SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_VALU", "SQ_INSTS_SALU",
-                  "SQ_VALU_MFMA_COEXEC_CYCLES", "SQ_BUSY_CYCLES"):
+                  "SQ_VALU_MFMA_COEXEC_CYCLES", "SQ_BUSY_CYCLES", "SQ_INSTS_FLAT", "SQ_INSTS_SMEM",
+                  "SQ_INSTS_BRANCH", "SQ_WAVES"):
             if m.get(c) is not None:
                 busy[c.lower()] = m[c]
         out["mfma_busy"] = busy
@@ -137,9 +138,10 @@ def main():
     import bench
     d = sys.argv[1]
     lines = [f"kernel sources hash {bench.kernel_src_hash()}"]
-    report = {w: workload(d, w, lines) for w in ("single", "batch")}
+    report = {w: workload(d, w, lines) for w in ("single", "batch", "c5")}
     out = dict(report["single"])
     out["batch"] = report["batch"]
+    out["c5"] = report["c5"]
     out["src_hash"] = bench.kernel_src_hash()
     out["source"] = f"rocprofv3 PMC passes, {os.path.basename(os.path.normpath(d))} (scripts/gpu_profile_round.sh)"
     with open(os.path.join(d, "traffic.json"), "w") as fo:
