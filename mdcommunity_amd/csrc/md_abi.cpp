@@ -139,6 +139,12 @@ struct md_ctx {
   bool need_gscr = false;
   DevBuf<unsigned long long> prof;
   int prof_cap = 0;
+  // dataflow mode (single-graph rollouts without grid barriers, md_kernels.hip df_*): tagged
+  // granule buffer sized for the largest graph that qualifies (df_graph); MD_DF=0 turns it off
+  bool df_on = true;
+  DevBuf<unsigned long long> dfbuf;
+  int df_mt = 0, df_n = 0;
+  std::vector<char> df_graph;
   std::vector<unsigned long long> prof_host;
 
   ~md_ctx() {
@@ -164,7 +170,8 @@ struct md_ctx {
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
     tr_stat.release(); glist.release(); ctl.release(); tpart.release(); q.release(); spart.release();
     apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); nbc.release(); qslot.release(); qg.release(); tr_q.release(); node_w.release();
-    sres.release(); qspec.release(); bars.release();
+    sres.release(); qspec.release(); bars.release(); dfbuf.release();
+    df_graph.clear();
     h_req.release(); h_ans.release(); h_nact.release(); h_act.release(); h_q.release(); h_chk.release();
     h_done.release(); h_gvar.release();
     ng = 0;
@@ -259,6 +266,7 @@ const char* err_name(int e) {
     case 4: return "action out of range";
     case 5: return "host selection failed";
     case 6: return "kernel argument layout differs from the compiled assumption";
+    case 7: return "dataflow mode: a tile's alive-neighbour list exceeded NB_CAP";
     default: return e >= 1000 ? "bounds check failed (debug build; site = code - 1000)" : "unknown device error";
   }
 }
@@ -472,6 +480,10 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
                              c->hinfo[gl[0]].node_off % 4 == 0
                          ? std::max(0, std::min(c->spec_n, c->cus - grid))
                          : 0;
+  // dataflow mode: a single-graph rollout in dedicated mode with the layer split, no grid
+  // barrier (md_kernels.hip df_*; the graph qualified at load, MD_DF=0 keeps the barriers)
+  const bool df = run_mode == RUN_ROLLOUT && n_env == 1 && ngl == 1 && !team_env && c->dfbuf.p != nullptr &&
+                  c->df_graph[gl[0]] && 2 * ((c->hinfo[gl[0]].n + TILE - 1) / TILE) <= grid - 2 && !(c->variant & 16);
   HIPCHK(c, hipMemcpyAsync(c->glist.p, gl, sizeof(int) * ngl, hipMemcpyHostToDevice, c->stream));
   {
     // per-launch clears in one dispatch: control words, barrier shards; graph-head hand-off
@@ -492,6 +504,10 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
       ptr[5] = c->qg.p;
       bytes[5] = sizeof(int) * c->qg.n;
     }
+    if (df) {  // the tagged granules (no tag of an earlier launch may match)
+      ptr[4] = c->dfbuf.p;
+      bytes[4] = sizeof(unsigned long long) * c->dfbuf.n;
+    }
     HIPCHK(c, launch_clear(ptr, bytes, 6, c->stream));
   }
   Params p = make_params(c);
@@ -507,6 +523,11 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
       p.pre_ew = (unsigned long long*)(c->ctl.p + CTL_PRE);
       p.pre_cw = (unsigned long long*)(c->ctl.p + CTL_PRE + 2);
     }
+  }
+  if (df) {
+    p.df = c->dfbuf.p;
+    p.df_mt = c->df_mt;
+    p.df_n = c->df_n;
   }
   p.qmode = qmode ? 1 : 0;
   p.qpair = c->pair_on ? 1 : 0;
@@ -698,6 +719,7 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_HOST_HANDSHAKE")) c->host_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_POLL_US")) c->poll_us = std::atoi(v);
   if (const char* v = std::getenv("MD_H0G")) c->h0g_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MD_DF")) c->df_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_SPEC")) c->spec_n = std::max(0, std::min(SPEC_MAX, std::atoi(v)));
   md_status st = MD_OK;
   do {
@@ -977,6 +999,40 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
     for (int g = 0; g < n_graphs; ++g) maxn = std::max(maxn, (int)n_nodes[g]);
     md_status st = ensure_h0g(c, maxn - 1, false);
     if (st != MD_OK) return st;
+  }
+  {
+    // dataflow mode: a graph qualifies when its single-graph rollout runs with the layer split
+    // (environment in LDS, two tile workgroups per tile) and no tile's alive-neighbour list can
+    // exceed NB_CAP in either layer (the 16 largest degrees sum to at most NB_CAP: a tile's
+    // list holds the alive entries of 16 live rows)
+    c->df_graph.assign(n_graphs, 0);
+    int dn = 0, dmt = 0;
+    if (c->df_on)
+      for (int g = 0; g < n_graphs; ++g) {
+        const GraphInfo& gi = info[g];
+        const int tiles = (gi.n + TILE - 1) / TILE;
+        if (!phase_a_fits_lds_host(gi.n, gi.e[0] + gi.e[1]) || 2 + 2 * tiles > c->cus || tiles > XB_SLOTS) continue;
+        bool ok = true;
+        for (int l = 0; l < 2 && ok; ++l) {
+          const int* rp = rowptr[l].data() + gi.roff[l];
+          std::vector<int> d(gi.n);
+          for (int i = 0; i < gi.n; ++i) d[i] = rp[i + 1] - rp[i];
+          const int k = std::min(gi.n, TILE);
+          std::partial_sort(d.begin(), d.begin() + k, d.end(), std::greater<int>());
+          long s = 0;
+          for (int i = 0; i < k; ++i) s += d[i];
+          ok = s <= NB_CAP_ENTRIES;
+        }
+        if (!ok) continue;
+        c->df_graph[g] = 1;
+        dn = std::max(dn, gi.n);
+        dmt = std::max(dmt, tiles);
+      }
+    if (dn > 0) {
+      HIPCHK(c, c->dfbuf.alloc((size_t)df_granules(dn, dmt)));
+      c->df_n = dn;
+      c->df_mt = dmt;
+    }
   }
   return md_reset(c, nullptr);
 }

@@ -173,7 +173,16 @@ struct Params {
   unsigned long long* pre_ew;
   unsigned long long* pre_cw;
   int qspec_n;                     // total nodes of the loaded batch
+  // dataflow mode (single-graph rollouts in dedicated mode with the layer split, md_kernels.hip
+  // df_*): no grid barrier; the step record, the H rows, the virtual-node and arg-max partials
+  // move as data-tagged granules {value, tag} in this buffer (graph-local node / tile indices,
+  // zeroed per launch; layout df_ap / df_sp / df_hb).  null: the barrier protocol.
+  unsigned long long* df;
+  int df_mt;                       // tiles of the largest graph the buffer is sized for
+  int df_n;                        // nodes of that graph
 };
+// dataflow buffer size (granules) for graphs of at most n nodes / mt tiles
+inline long long df_granules(int n, int mt) { return 64 + 388LL * mt + 4LL * 64 * n; }
 
 // Speculative-step result slot (ints):
 //   [0..1] u64 done tag {nd << 48 | candidate << 32 | request tag}, written last

@@ -120,7 +120,8 @@ static_assert(2 * STG_ROWS * 64 <= S_HID - S_M, "neighbour staging fits [S_M, S_
 
 constexpr float NEG_INF = -__builtin_huge_valf();
 constexpr unsigned long long BARRIER_TIMEOUT_TICKS = 400000000ull;  // 4 s at 100 MHz
-enum : int { ERR_TIMEOUT = 1, ERR_COVERED = 2, ERR_LIVE_MISMATCH = 3, ERR_BADNODE = 4, ERR_HOST = 5, ERR_ABI = 6 };
+enum : int { ERR_TIMEOUT = 1, ERR_COVERED = 2, ERR_LIVE_MISMATCH = 3, ERR_BADNODE = 4, ERR_HOST = 5, ERR_ABI = 6,
+             ERR_DF_LISTS = 7 };
 
 // Kernel arguments of md_rollout_kernel / md_env_kernel, (Params, const float*), read in every
 // device function through the implicit-argument pointer (SGPRs s[8:9] in callees) at a fixed
@@ -266,6 +267,7 @@ __device__ __forceinline__ void gv_store(KParams& p, int g, const GraphVar* src)
   if (threadIdx.x < GV_WORDS) stc((int*)(p.gvar + g) + threadIdx.x, ((const int*)src)[threadIdx.x]);
 }
 
+
 // ------------------------------------------------------------------ grid barrier
 // Monotonic counter: every wave drains its stores (vmcnt), the workgroup syncs, one lane adds
 // to the counter (agent-scope atomic) and polls it with sc1 loads; all data crossing the
@@ -290,6 +292,88 @@ __device__ __forceinline__ bool md_bok(bool ok, int site) {
 #else
 #define MD_BOK(cond, site) true
 #endif
+
+// ------------------------------------------------------------------ dataflow mode: granules
+// Single-graph rollouts in dedicated mode with the layer split run without any grid barrier
+// when p.df is set (md_abi.cpp decides; MD_DF=0 keeps the barriers).  Everything one workgroup
+// hands to another inside a step moves as data-tagged 8-byte granules {value bits (low word),
+// tag (high word)}, each written by ONE sc1 store and polled by the consumer until its tag
+// matches (MI355X_MICROARCH.md price list, handoff-1to1: one round trip, no flag, no drain):
+//   step record  environment workgroup -> all: {status, n_live, confirmation, early word} of
+//                step pstep, tag pstep + 1, after phase A's stores drained (replaces barrier A
+//                and the tiles' read of the GraphVar)
+//   H rows       tiles -> tiles: the iteration-1 / -2 embeddings, 64 granules per node row
+//                (replaces barriers 1 and 2: an iteration waits for exactly its neighbours)
+//   spart        tiles -> graph-head workgroup: virtual-node partial sums S0..S2
+//   apart        tiles -> phase A: the arg-max partial {max, second, index, count}, written
+//                after the tile's q stores drained (replaces barrier 3)
+// Data of step pstep carry tag (pstep + 1) << 1; iteration-1 data that an iteration-1 prebuild
+// wrote from the speculative result (before phase A confirmed it) carry that | 1, and are
+// accepted only when the step record confirms that result (the step's one early word).  The
+// buffer is zeroed before each launch.  Write-after-read safety without barriers: a step's
+// rows and sums are read within the step, and the next step's writers start after the next
+// step record, which phase A publishes only after every active tile's arg-max partial (each
+// written after that tile's last read, and after the layer-1 hand-off and the graph head it
+// waited for) has arrived.
+constexpr int DF_REC = 0;  // record granules: status, n_live, confirmation lo / hi, early word lo / hi
+__device__ __forceinline__ unsigned df_tag(int pstep) { return (unsigned)(pstep + 1) << 1; }
+__device__ __forceinline__ unsigned long long* df_ap(KParams& p) { return p.df + 64; }
+__device__ __forceinline__ unsigned long long* df_sp(KParams& p) { return p.df + 64 + 4 * (size_t)p.df_mt; }
+__device__ __forceinline__ unsigned long long* df_hb(KParams& p, int l, int b) {
+  return p.df + 64 + 388 * (size_t)p.df_mt + (size_t)(2 * l + b) * 64 * p.df_n;
+}
+__device__ __forceinline__ void df_st(unsigned long long* a, float v, unsigned tag) {
+  __hip_atomic_store((g_u64*)a, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool df_ok(unsigned t, unsigned ta, unsigned tb) { return t == ta || t == tb; }
+// granule pair {v0, tag, v1, tag} as loaded by one 16-byte sc1 load
+__device__ __forceinline__ bool df_ok4(const float4& x, unsigned ta, unsigned tb) {
+  return df_ok(__float_as_uint(x.y), ta, tb) && df_ok(__float_as_uint(x.w), ta, tb);
+}
+// the slow path of a granule poll: true when the caller should stop (an error anywhere, or the
+// time-out, which raises one); t0 = the poll's start
+__device__ __forceinline__ bool df_give_up(KParams& p, unsigned long long t0, unsigned long long limit) {
+  if (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR) return true;
+  if (wall_clock64() - t0 > limit) {
+    raise_err(p, ERR_TIMEOUT);
+    return true;
+  }
+  return false;
+}
+// 16-byte granule pair at byte offset off of the (wave-uniform) base, polled until both tags
+// are ta or tb (zeros when the grid gave up)
+__device__ __forceinline__ float4 df_ld4(KParams& p, const float* base, int off, unsigned ta, unsigned tb) {
+  float4 x = ldc4(base, off);
+  if (!df_ok4(x, ta, tb)) {
+    const unsigned long long t0 = wall_clock64();
+    do {
+      __builtin_amdgcn_s_sleep(1);
+      if (df_give_up(p, t0, 400000000ull)) return make_float4(0.f, 0.f, 0.f, 0.f);
+      x = ldc4(base, off);
+    } while (!df_ok4(x, ta, tb));
+  }
+  return x;
+}
+// one granule, polled until its tag is ta or tb; returns its value (0 when the grid gave up)
+__device__ __forceinline__ float df_ld(KParams& p, const unsigned long long* a, unsigned ta, unsigned tb) {
+  unsigned long long g = __hip_atomic_load((const g_u64*)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!df_ok((unsigned)(g >> 32), ta, tb)) {
+    const unsigned long long t0 = wall_clock64();
+    do {
+      __builtin_amdgcn_s_sleep(1);
+      if (df_give_up(p, t0, 400000000ull)) return 0.f;
+      g = __hip_atomic_load((const g_u64*)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } while (!df_ok((unsigned)(g >> 32), ta, tb));
+  }
+  return __uint_as_float((unsigned)g);
+}
+// arg-max partial of tile j written in the step whose tag is tag: {max, second, index, count}
+__device__ __forceinline__ float4 df_apart(KParams& p, int j, unsigned tag) {
+  const float* b = (const float*)df_ap(p);
+  const float4 a = df_ld4(p, b, j * 32, tag, tag), c = df_ld4(p, b, j * 32 + 16, tag, tag);
+  return make_float4(a.x, a.z, c.x, c.z);
+}
 // returns true (uniformly) when an error was raised anywhere in the grid.
 // The arrival counter is sharded over BAR_SHARDS words on lines of their own (workgroup b adds
 // to shard b % BAR_SHARDS): one-word fan-in serialises every arrival at the memory side
@@ -595,7 +679,8 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
       const int lane = threadIdx.x;
       const int nt = (gv.n_live + TILE - 1) / TILE;
       for (int j = lane; j < nt; j += 64) {
-        const float4 ap = ldc4(p.apart, (gi.tile_off + j) * 16);
+        // (dataflow mode: the partials of the previous step, polled as tagged granules)
+        const float4 ap = p.df != nullptr ? df_apart(p, j, (unsigned)misc[60] << 1) : ldc4(p.apart, (gi.tile_off + j) * 16);
         const int c = __float_as_int(ap.w);
         if (c == 0) continue;
         argmax_combine(bm, bs, bi, bc, ap.x, ap.y, __float_as_int(ap.z), c);
@@ -606,13 +691,24 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
         const int i2 = __shfl_xor(bi, o, 64), c2 = __shfl_xor(bc, o, 64);
         if (c2 != 0) argmax_combine(bm, bs, bi, bc, m2, s2, i2, c2);
       }
-    } else if ((int)threadIdx.x < 64 + p.n_spec) {
+    } else if ((int)threadIdx.x < 64 + p.n_spec && p.df == nullptr) {
       // speculative results' tags, read beside the partials (env_step matches them against
       // the chosen node without a round trip of its own)
       const g_u64* tp = (const g_u64*)(p.sres + (size_t)(threadIdx.x - 64) * p.sres_stride);
       unsigned long long* pre = (unsigned long long*)(lds + L_PREF) + 2 * (threadIdx.x - 64);
       pre[0] = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       pre[1] = __hip_atomic_load(tp + SRES_STARTED / 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (p.df != nullptr) {
+      // dataflow mode: phase A starts polling the partials as the step's tiles start, so the
+      // tags are read once every partial has arrived (as fresh as beside barrier mode's partials)
+      __syncthreads();
+      if (threadIdx.x >= 64 && (int)threadIdx.x < 64 + p.n_spec) {
+        const g_u64* tp = (const g_u64*)(p.sres + (size_t)(threadIdx.x - 64) * p.sres_stride);
+        unsigned long long* pre = (unsigned long long*)(lds + L_PREF) + 2 * (threadIdx.x - 64);
+        pre[0] = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pre[1] = __hip_atomic_load(tp + SRES_STARTED / 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     if (threadIdx.x == 0) {
       const int t = gv.npred;
@@ -728,6 +824,10 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
   gv_store(p, g, &gv);
   if (p.pre_cw != nullptr && threadIdx.x == 0)  // every phase A: a stale confirmation must not match
     __hip_atomic_store((g_u64*)p.pre_cw, cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (p.df != nullptr && threadIdx.x == 0) {  // dataflow mode: the confirmation goes into the step record
+    misc[54] = (int)(unsigned)cw;
+    misc[55] = (int)(unsigned)(cw >> 32);
+  }
   __syncthreads();
   return staged;
 }
@@ -1304,6 +1404,110 @@ __device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it,
   atx[(c + 1) * LDT + r] = own.y;
 }
 
+// Dataflow mode, iterations 2-3 of layer L: gather_tile2s with the previous iteration's rows
+// read as tagged granules (df_hb) -- 32 lanes per row, each loading its two features and their
+// tags in one 16-byte load -- polled until every tag is ta or tb, so the gather itself waits for
+// exactly the rows it needs instead of a grid barrier.  Same staging, same adds in CSR order.
+__device__ __noinline__ void gather_df(KParams&, const GraphInfo gi, int it, int L, unsigned ta, unsigned tb) {
+  const int* const rows = (const int*)(lds_base() + L_SCR + S_ROW);
+  float* const scr = lds_base() + L_SCR;
+
+  KParams& p = kp();
+  constexpr int SROWS = 128, NLD = SROWS * 32 / NTHREADS;
+  static_assert(SROWS * 64 <= S_HID - S_M, "dataflow staging fits [S_M, S_HID)");
+  const int w = wave_id(), lane = lane_id(), t = threadIdx.x;
+  const int q = lane & 31;
+  const int r = 2 * w + (lane >> 5);
+  const float* hb = (const float*)df_hb(p, L, it - 2);
+  const lds_i32* hdr = (const lds_i32*)(const int*)(scr + S_NBH);
+  const lds_u16* nbl = (const lds_u16*)(const uint16_t*)(scr + S_NBL) + L * NB_CAP;
+  const int v = rows[r];
+  float4 ox = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (v >= 0 && MD_BOK(v < gi.n, 1)) ox = ldc4(hb, v * 512 + q * 16);
+  float2 acc = {0.f, 0.f};
+  const int myoff = hdr[L * 16 + r], mycnt = hdr[32 + L * 16 + r];
+  const int totl = hdr[128 + L];
+  const int nbat = (totl + SROWS - 1) / SROWS;
+  float2* stg = (float2*)(scr + S_M);
+  const float2* stg2 = (const float2*)(scr + S_M);
+  auto src_of = [&](int base, int i) {
+    const int k = t + NTHREADS * i, row = base + (k >> 5);
+    const int id = nbl[row];
+    return MD_BOK(id < gi.n, 4) ? id * 512 + (k & 31) * 16 : 0;
+  };
+  auto issue = [&](int b, float4 (&x)[NLD], bool (&ok)[NLD]) {
+    const int base = b * SROWS;
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int k = t + NTHREADS * i, row = base + (k >> 5);
+      ok[i] = b < nbat && row < totl;
+      if (ok[i]) x[i] = ldc4(hb, src_of(base, i));
+    }
+  };
+  auto consume = [&](int b, float4 (&x)[NLD], const bool (&ok)[NLD]) {
+    const int base = b * SROWS;
+    // rows whose producer has not stored them yet: poll those (rare once a tile's neighbours
+    // are ahead of it)
+    unsigned bad = 0;
+#pragma unroll
+    for (int i = 0; i < NLD; ++i)
+      if (ok[i] && !df_ok4(x[i], ta, tb)) bad |= 1u << i;
+    if (__any(bad != 0)) {
+      const unsigned long long t0 = wall_clock64();
+      while (__any(bad != 0)) {
+        __builtin_amdgcn_s_sleep(1);
+        if (df_give_up(p, t0, BARRIER_TIMEOUT_TICKS)) break;
+#pragma unroll
+        for (int i = 0; i < NLD; ++i)
+          if (bad & (1u << i)) x[i] = ldc4(hb, src_of(base, i));
+#pragma unroll
+        for (int i = 0; i < NLD; ++i)
+          if ((bad & (1u << i)) && df_ok4(x[i], ta, tb)) bad &= ~(1u << i);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NLD; ++i)
+      if (ok[i]) stg[t + NTHREADS * i] = make_float2(x[i].x, x[i].z);
+    __syncthreads();
+    const int lo = max(myoff, base), hi = min(myoff + mycnt, base + SROWS);
+    int k = lo;
+    for (; k + 8 <= hi; k += 8) {
+      float2 y[8];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) y[jj] = stg2[(k + jj - base) * 32 + q];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        acc.x = acc.x + y[jj].x;
+        acc.y = acc.y + y[jj].y;
+      }
+    }
+    for (; k < hi; ++k) {
+      const float2 y = stg2[(k - base) * 32 + q];
+      acc.x = acc.x + y.x;
+      acc.y = acc.y + y.y;
+    }
+    __syncthreads();
+  };
+  float4 xa[NLD], xb[NLD];
+  bool oka[NLD], okb[NLD];
+  if (nbat > 0) issue(0, xa, oka);
+  for (int b = 0; b < nbat; b += 2) {
+    issue(b + 1, xb, okb);
+    consume(b, xa, oka);
+    if (b + 1 >= nbat) break;
+    issue(b + 2, xa, oka);
+    consume(b + 1, xb, okb);
+  }
+  if (v >= 0 && !df_ok4(ox, ta, tb)) ox = df_ld4(p, hb, v * 512 + q * 16, ta, tb);
+  float* atp = scr + S_P + L * 64 * LDT;
+  float* atx = scr + S_X + L * 64 * LDT;
+  const int c = 2 * q;
+  atp[(c + 0) * LDT + r] = acc.x;
+  atp[(c + 1) * LDT + r] = acc.y;
+  atx[(c + 0) * LDT + r] = ox.x;
+  atx[(c + 1) * LDT + r] = ox.z;
+}
+
 // Node update of layer L: waves 0-3 P.P1 (column block w), waves 4-7 X.P2, then waves 0-3
 // relu(M.P3).  Each output's k-chain is update_tile's.
 __device__ __noinline__ void update_tile_split(const float*, float*, int L) {
@@ -1387,7 +1591,41 @@ __device__ __noinline__ void normalize_tile_split(float*, float*, int L) {
 // stores land where iteration 1's do and nobody reads them before barrier 1; without phase A's
 // confirmation the tile runs iteration 1 again and overwrites them.  Returns false when the
 // first-layer rows of the result's dmax are not precomputed (nothing done).
-__device__ __noinline__ bool spec_iteration1(KParams&, const GraphInfo gi, int j, int L, unsigned long long ew) {
+// Dataflow mode: the outputs of iteration it (1 or 2) of tile j, layer L (graph-local) as tagged
+// granules -- the virtual-node partial sums (S0 and S1 at iteration 1, S2 at 2, the barrier
+// path's values) and the new embedding rows, thread t storing row t / 32's features 2 (t % 32)
+// and 2 (t % 32) + 1 as one 16-byte pair of granules.  Reads E / X in LDS: the caller syncs
+// before overwriting them.
+__device__ __noinline__ void df_store_tile(KParams&, int j, int L, int it, unsigned tag) {
+  KParams& p = kp();
+  float* const scr = lds_base() + L_SCR;
+  const int* rows = (const int*)(scr + S_ROW);
+  if (threadIdx.x < 64) {
+    const int c = threadIdx.x;
+    const float* ate = scr + S_E + L * 64 * LDT + c * LDT;
+    const float* atx = scr + S_X + L * 64 * LDT + c * LDT;
+    const int nv = tile_rows_valid(rows);
+    unsigned long long* sp = df_sp(p) + (size_t)j * 384;
+    const float s_new = col_sum16(ate, nv);
+    if (it == 1) {
+      df_st(sp + L * 64 + c, col_sum16(atx, nv), tag);  // S0 (first-layer input)
+      df_st(sp + 128 + L * 64 + c, s_new, tag);         // S1
+    } else {
+      df_st(sp + 256 + L * 64 + c, s_new, tag);         // S2
+    }
+  }
+  const int rr = threadIdx.x >> 5, c2 = threadIdx.x & 31;
+  const int v = rows[rr];
+  const float* e = scr + S_E + L * 64 * LDT;
+  const float tf = __uint_as_float(tag);
+  if (v >= 0)
+    stc4((float*)df_hb(p, L, it - 1), v * 512 + c2 * 16,
+         make_float4(e[(2 * c2) * LDT + rr], tf, e[(2 * c2 + 1) * LDT + rr], tf));
+}
+
+// dft != 0 (dataflow mode): the outputs go out as granules tagged dft (df_store_tile).
+__device__ __noinline__ bool spec_iteration1(KParams&, const GraphInfo gi, int j, int L, unsigned long long ew,
+                                             unsigned dft = 0) {
   KParams& p = kp();
   float* const lds = lds_base();
   float* const scr = lds + L_SCR;
@@ -1406,6 +1644,11 @@ __device__ __noinline__ bool spec_iteration1(KParams&, const GraphInfo gi, int j
   __syncthreads();
   normalize_tile_split(scr + S_E, scr, L);
   __syncthreads();
+  if (dft != 0) {
+    df_store_tile(p, j, L, 1, dft);
+    __syncthreads();
+    return true;
+  }
   if (threadIdx.x < 64) {
     const int c = threadIdx.x;
     const float* ate = scr + S_E + L * 64 * LDT + c * LDT;
@@ -1512,7 +1755,10 @@ __device__ __noinline__ void normalize_tile(float*, float*) {
 // Sum of one graph's per-tile partial sums (slot) -> out[2][64]: four threads per output each
 // add a contiguous quarter of the tiles in order, then the quarters are added in order
 // (a fixed order, identical in every workgroup).
-__device__ void graph_sum(KParams& p, const GraphInfo& gi, int nt, int slot, float*, float*) {
+// ta != 0 (dataflow mode): the partials are tagged granules (df_sp, graph-local tiles) polled
+// until their tag is ta or tb.
+__device__ void graph_sum(KParams& p, const GraphInfo& gi, int nt, int slot, float*, float*, unsigned ta = 0,
+                          unsigned tb = 0) {
   float* const out = lds_base() + L_SCR + S_HID;
   float* const tmp4 = lds_base() + L_SCR + S_YP;
 
@@ -1521,13 +1767,33 @@ __device__ void graph_sum(KParams& p, const GraphInfo& gi, int nt, int slot, flo
   const int j0 = min(nt, qt * per), j1 = min(nt, j0 + per);
   const float* sp = p.spart + (size_t)gi.tile_off * 384 + slot * 128 + o;
   float a = 0.f;
-  for (int jb = j0; jb < j1; jb += 16) {
-    float x[16];
+  if (ta != 0) {
+    const unsigned long long* sg = df_sp(p) + slot * 128 + o;
+    for (int jb = j0; jb < j1; jb += 16) {
+      unsigned long long gx[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) x[k] = jb + k < j1 ? ldc(sp + (size_t)(jb + k) * 384) : 0.f;
+      for (int k = 0; k < 16; ++k)
+        gx[k] = jb + k < j1 ? __hip_atomic_load((const g_u64*)(sg + (size_t)(jb + k) * 384), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT)
+                            : 0ull;
 #pragma unroll
-    for (int k = 0; k < 16; ++k)
-      if (jb + k < j1) a = a + x[k];
+      for (int k = 0; k < 16; ++k) {
+        if (jb + k < j1) {
+          const float x = df_ok((unsigned)(gx[k] >> 32), ta, tb) ? __uint_as_float((unsigned)gx[k])
+                                                                 : df_ld(p, sg + (size_t)(jb + k) * 384, ta, tb);
+          a = a + x;
+        }
+      }
+    }
+  } else {
+    for (int jb = j0; jb < j1; jb += 16) {
+      float x[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) x[k] = jb + k < j1 ? ldc(sp + (size_t)(jb + k) * 384) : 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (jb + k < j1) a = a + x[k];
+    }
   }
   tmp4[qt * 128 + o] = a;
   __syncthreads();
@@ -1753,8 +2019,9 @@ __device__ __forceinline__ void split_receive(KParams& p, float* scr, int slot, 
 // One iteration of the graph-head workgroup (dedicated mode) for graph g: it == 2 builds
 // Y1, Y2 from the S0 / S1 tile partials of iteration 1; it == 3 builds Y3 from S2, runs the
 // graph head and publishes it.  Same arithmetic as the shared-mode path in the tile loop.
+// ta / tb (dataflow mode): the tags the tiles' partial sums of this step carry (0: barrier mode).
 __device__ __noinline__ void head_iteration(KParams&, float*, float*, int g, int it,
-                                            unsigned long long htag) {
+                                            unsigned long long htag, unsigned ta = 0, unsigned tb = 0) {
   float* const lds = lds_base();
   float* const scr = lds + L_SCR;
 
@@ -1788,13 +2055,13 @@ __device__ __noinline__ void head_iteration(KParams&, float*, float*, int g, int
   float* yw = lds + L_YW;
   if (it == 2) {
     if (threadIdx.x < 128) yw[threadIdx.x] = lds[L_Y0 + (threadIdx.x & 63)];
-    graph_sum(p, gi, nt, 0, sbuf, scr + S_YP);
+    graph_sum(p, gi, nt, 0, sbuf, scr + S_YP, ta, tb);
     vrow_update(lds + L_W, scr, sbuf, yw);  // Y1 from S0
-    graph_sum(p, gi, nt, 1, sbuf, scr + S_YP);
+    graph_sum(p, gi, nt, 1, sbuf, scr + S_YP, ta, tb);
     vrow_update(lds + L_W, scr, sbuf, yw);  // Y2 from S1
   } else {
     HSTAMP(49);
-    graph_sum(p, gi, nt, 2, sbuf, scr + S_YP);
+    graph_sum(p, gi, nt, 2, sbuf, scr + S_YP, ta, tb);
     HSTAMP(50);
     vrow_update(lds + L_W, scr, sbuf, yw);  // Y3 from S2
     HSTAMP(51);
@@ -2021,7 +2288,16 @@ __device__ __noinline__ void attention_q_tile(KParams&, float*, float*, const Gr
       const int i2 = __shfl_xor(bi, o, 64), c2 = __shfl_xor(bc, o, 64);
       if (c2 != 0) argmax_combine(bm, bs, bi, bc, m2, s2, i2, c2);
     }
-    if (lane == 0) stc4(apart_out, 0, make_float4(bm, bs, __int_as_float(bi), __int_as_float(bc)));
+    if (p.df != nullptr) {
+      // dataflow mode: four tagged granules, once this wave's q / qspec stores are done (phase A
+      // and the speculative workgroups read q after seeing the partial)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane < 4)
+        df_st((unsigned long long*)apart_out + lane, lane == 0 ? bm : lane == 1 ? bs : __int_as_float(lane == 2 ? bi : bc),
+              (unsigned)htag << 1);
+    } else if (lane == 0) {
+      stc4(apart_out, 0, make_float4(bm, bs, __int_as_float(bi), __int_as_float(bc)));
+    }
   }
   __syncthreads();
   QATS(6);
@@ -3714,6 +3990,236 @@ __device__ __noinline__ void spec_loop(KParams&) {
 // One body, two entry points so profiles separate the work: md_rollout_kernel runs whole
 // rollouts (RUN_ROLLOUT); md_env_kernel runs single environment steps and predictions
 // (RUN_STEP: MvcEnv.s0 / queued actions, RUN_PREDICT).
+// ------------------------------------------------------------------ dataflow mode: the loops
+// (see "dataflow mode: granules" above).  Per step the environment workgroup runs phase A and
+// publishes the step record; the graph-head workgroup and the tile workgroups wait for it (the
+// tiles building the iteration-1 prebuild from phase A's early word meanwhile), then run the
+// step with every hand-off polled as tagged granules.
+
+// Waits for the step record tagged `tag`: 1 when it is there (its six words in misc[50..55]),
+// 2 when `watch` is set and the early word changed first (new value in the LDS word at
+// L_MISC + 42), 0 on an error anywhere.  Uniform.
+__device__ __noinline__ int df_wait_rec(KParams&, unsigned tag, bool watch) {
+  KParams& p = kp();
+  int* const misc = (int*)(lds_base() + L_MISC);
+  unsigned long long* const seen = (unsigned long long*)(lds_base() + L_MISC + 42);
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const bool w = watch && p.pre_ew != nullptr;
+    const unsigned long long sv = *seen;
+    const unsigned long long t0 = wall_clock64();
+    int res = 0;
+    while (true) {
+      // lanes 0-5: the record's granules, lane 6: the error word, lane 7: the early word
+      unsigned long long g = 0ull;
+      if (lane < 6) g = __hip_atomic_load((const g_u64*)(p.df + DF_REC + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else if (lane == 6) g = __hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else if (lane == 7 && w) g = __hip_atomic_load((const g_u64*)p.pre_ew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__ballot(lane == 6 && (g & BAR_ERR))) break;
+      if (!__ballot(lane < 6 && (unsigned)(g >> 32) != tag)) {
+        if (lane < 6) misc[50 + lane] = (int)(unsigned)g;
+        res = 1;
+        break;
+      }
+      if (w) {
+        const unsigned lo = __shfl((unsigned)g, 7, 64), hi = __shfl((unsigned)(g >> 32), 7, 64);
+        const unsigned long long ew = ((unsigned long long)hi << 32) | lo;
+        if (ew != sv) {
+          if (lane == 0) *seen = ew;
+          res = 2;
+          break;
+        }
+      }
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > (p.h_req != nullptr ? HOST_TIMEOUT_TICKS : BARRIER_TIMEOUT_TICKS)) {
+        if (lane == 0) raise_err(p, ERR_TIMEOUT);
+        break;
+      }
+    }
+    if (lane == 0) misc[49] = res;
+  }
+  __syncthreads();
+  const int r = misc[49];
+  __syncthreads();
+  return r;
+}
+
+// Environment workgroup: phase A, then the step record {status, n_live, confirmation, early
+// word} once phase A's stores are done.
+__device__ __noinline__ void df_env(KParams&) {
+  KParams& p = kp();
+  float* const lds = lds_base();
+  int* const misc = (int*)(lds + L_MISC);
+  const int g = p.glist[0];
+  bool have_q = false, staged = false;
+  unsigned long long last_ew = 0ull;  // the early word as the tiles see it after this phase A
+  for (int pstep = 0;; ++pstep) {
+    MD_PROF(0);
+    if (threadIdx.x == 0) misc[60] = pstep;
+    __syncthreads();
+    staged = phase_a(p, g, have_q, lds, staged);
+    MD_PROF(3);
+    const GraphVar& gv = *(const GraphVar*)(lds + L_GV);
+    if (p.pre_ew != nullptr) {
+      const unsigned long long ew = ((unsigned long long)(unsigned)misc[57] << 32) | (unsigned)misc[56];
+      if (ew != 0ull) last_ew = ew;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of phase A is done
+    __syncthreads();
+    const int st = gv.status;
+    if (threadIdx.x < 6) {
+      const int k = threadIdx.x;
+      const int v = k == 0 ? st : k == 1 ? gv.n_live : k < 4 ? misc[52 + k] : k == 4 ? (int)(unsigned)last_ew : (int)(unsigned)(last_ew >> 32);
+      df_st(p.df + DF_REC + k, __int_as_float(v), (unsigned)(pstep + 1));
+    }
+    // the record lands before any later early word (a tile that sees the next step's early word
+    // sees this record)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) misc[49] = (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR) != 0;
+    __syncthreads();
+    const bool stop = st != ST_RUN || misc[49] != 0;
+    __syncthreads();
+    if (stop) break;
+    have_q = true;
+  }
+  if (p.n_spec > 0 && threadIdx.x == 0)
+    __hip_atomic_store((g_u64*)p.spec_req, SPEC_EXIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Graph-head workgroup: the virtual-node chain and the graph head of each step from the tiles'
+// tagged partial sums (S0 / S1 may come from a confirmed prebuild).
+__device__ __noinline__ void df_head(KParams&) {
+  KParams& p = kp();
+  float* const lds = lds_base();
+  float* const scr = lds + L_SCR;
+  int* const misc = (int*)(lds + L_MISC);
+  const int g = p.glist[0];
+  for (int pstep = 0;; ++pstep) {
+    if (threadIdx.x == 0) misc[60] = pstep;
+    __syncthreads();
+    if (df_wait_rec(p, (unsigned)(pstep + 1), false) != 1 || misc[50] != ST_RUN) break;
+    const unsigned tn = df_tag(pstep), tp = (misc[52] | misc[53]) != 0 ? tn | 1u : tn;
+    head_iteration(p, lds, scr, g, 2, (unsigned long long)(pstep + 1), tn, tp);
+    head_iteration(p, lds, scr, g, 3, (unsigned long long)(pstep + 1), tn, tn);
+  }
+}
+
+// Diagnostics (md_profile): stamps of tile 0's layer-0 workgroup in the step's slots: 4 record
+// seen, 5 iteration 1 done, 23 / 6 iteration-2 gather / all done, 29 / 30 iteration-3 gather /
+// update done, 8 layer-1 rows received, 9 = 10 attention and arg-max partial done.
+#define DF_STAMP(slot)                                                                              \
+  do {                                                                                              \
+    if (p.prof != nullptr && tb == 0 && threadIdx.x == 0 && pstep < p.prof_cap)                     \
+      p.prof[(size_t)pstep * PROF_SLOTS + (slot)] = wall_clock64();                                 \
+  } while (0)
+// Tile workgroup (tile j, layer L) of the layer split.
+__device__ __noinline__ void df_tiles(KParams&) {
+  KParams& p = kp();
+  float* const lds = lds_base();
+  float* const scr = lds + L_SCR;
+  int* const misc = (int*)(lds + L_MISC);
+  int* const rows = (int*)(scr + S_ROW);
+  const int g = p.glist[0];
+  const GraphInfo gi = p.ginfo[g];
+  const int tb = (int)blockIdx.x - 2 * p.n_env, j = tb >> 1, L = tb & 1;
+  unsigned long long* const seen = (unsigned long long*)(lds + L_MISC + 42);
+  if (threadIdx.x == 0) *seen = 0ull;
+  for (int pstep = 0;; ++pstep) {
+    if (threadIdx.x == 0) misc[60] = pstep;
+    __syncthreads();
+    // the step record; meanwhile the iteration-1 prebuild from phase A's early word
+    int pre_state = 0, r;
+    unsigned long long pre_used = 0ull;
+    while ((r = df_wait_rec(p, (unsigned)(pstep + 1), true)) == 2) {
+      const unsigned long long ew = *seen;
+      if (pre_state == 0 && ew != 0ull) {
+        pre_state = prebuild_lists(p, gi, j, L, ew);
+        if (pre_state) pre_used = ew;
+        // the whole of iteration 1 too (MD_VARIANT bit 128: lists only), tagged as prebuilt
+        if (pre_state == 1 && !(p.variant & 128) && spec_iteration1(p, gi, j, L, ew, df_tag(pstep) | 1u)) pre_state = 3;
+      }
+    }
+    if (r != 1 || misc[50] != ST_RUN) break;
+    DF_STAMP(4);
+    const int nl = misc[51];
+    const unsigned long long cw = ((unsigned long long)(unsigned)misc[53] << 32) | (unsigned)misc[52];
+    __syncthreads();
+    // the next step's wait starts from this step's early word: a change is the next phase A's
+    if (threadIdx.x == 0) *seen = ((unsigned long long)(unsigned)misc[55] << 32) | (unsigned)misc[54];
+    if (j >= (nl + TILE - 1) / TILE) continue;
+    const int pre_ok = pre_state != 0 && cw == pre_used ? pre_state : 0;
+    const unsigned tn = df_tag(pstep), tp = cw != 0ull ? tn | 1u : tn;
+    bool nb_ok = true;
+    // iteration 1 (skipped when the confirmed prebuild ran it)
+    if (pre_ok != 3) {
+      if (pre_ok == 0) {
+        if (threadIdx.x < TILE) {
+          const int rr = j * TILE + threadIdx.x;
+          const float4 e = ldc4((const float*)(p.live + 4 * (size_t)gi.node_off), min(rr, gi.n - 1) * 16);
+          const bool ok = rr < nl && MD_BOK(__float_as_int(e.x) >= 0 && __float_as_int(e.x) < gi.n && nl <= gi.n, 6);
+          const unsigned c = (unsigned)__float_as_int(e.w);
+          lds_i32* hdr = (lds_i32*)(int*)(scr + S_NBH);
+          rows[threadIdx.x] = ok ? __float_as_int(e.x) : -1;
+          hdr[64 + threadIdx.x] = ok ? __float_as_int(e.y) : 0;       // layer 0: CSR begin
+          hdr[96 + threadIdx.x] = ok ? (int)(c & 0xffffu) : 0;        //          CSR extent
+          hdr[64 + 16 + threadIdx.x] = ok ? __float_as_int(e.z) : 0;  // layer 1
+          hdr[96 + 16 + threadIdx.x] = ok ? (int)(c >> 16) : 0;
+        }
+        __syncthreads();
+        nb_ok = build_nb_lists(p, gi, rows, scr, nullptr, L);
+      } else {
+        nb_ok = pre_ok == 1;
+      }
+      // (the host enables this mode only when no tile's lists can exceed NB_CAP)
+      if (!nb_ok) {
+        if (threadIdx.x == 0) raise_err(p, ERR_DF_LISTS);
+        break;
+      }
+      gather_tile2s(p, gi, 1, rows, scr, L);
+      __syncthreads();
+      update_tile_split(lds + L_W, scr, L);
+      __syncthreads();
+      normalize_tile_split(scr + S_E, scr, L);
+      __syncthreads();
+      df_store_tile(p, j, L, 1, tn);
+      __syncthreads();
+    }
+    DF_STAMP(5);
+    // iteration 2: the neighbours' iteration-1 rows (a confirmed prebuild's are valid too)
+    gather_df(p, gi, 2, L, tn, tp);
+    __syncthreads();
+    DF_STAMP(23);
+    update_tile_split(lds + L_W, scr, L);
+    __syncthreads();
+    normalize_tile_split(scr + S_E, scr, L);
+    __syncthreads();
+    df_store_tile(p, j, L, 2, tn);
+    __syncthreads();
+    DF_STAMP(6);
+    // iteration 3, then the layer-1 rows to the layer-0 workgroup, which runs the attention and
+    // the Q head and publishes the arg-max partial
+    gather_df(p, gi, 3, L, tn, tn);
+    __syncthreads();
+    DF_STAMP(29);
+    update_tile_split(lds + L_W, scr, L);
+    __syncthreads();
+    normalize_tile_split(scr + S_E, scr, L);
+    __syncthreads();
+    DF_STAMP(30);
+    if (L == 1) {
+      split_publish(p, scr, j, (unsigned long long)(pstep + 1));
+    } else {
+      split_receive(p, scr, j, (unsigned long long)(pstep + 1));
+      DF_STAMP(8);
+      attention_q_tile(p, lds, scr, gi, g, rows, (float*)(df_ap(p) + 4 * (size_t)j), (unsigned long long)(pstep + 1),
+                       nullptr);
+      DF_STAMP(9);
+      DF_STAMP(10);
+    }
+  }
+}
+#undef DF_STAMP
+
 __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict__ wimg) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* scr = lds + L_SCR;
@@ -3752,6 +4258,12 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
       lds[L_Y0 + lane] = x / fmaxf(nr, 1e-12f);
     }
     __syncthreads();
+  }
+  if (p.df != nullptr) {  // dataflow mode (single graph, layer split): no grid barrier
+    if (is_env) df_env(p);
+    else if (is_head) df_head(p);
+    else df_tiles(p);
+    return;
   }
 
   unsigned target = 0;

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Dataflow mode: A/B timing + identity on single-graph fixtures, phase profile, parity tests.
+O=gpurun_out/r03d
+mkdir -p $O
+step() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 $secs "$@" > $O/$name.out 2> $O/$name.err
+  local rc=$?
+  echo "$name rc=$rc" | tee -a $O/steps.txt
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+  return 0
+}
+step df_ab 300 python -u scripts/df_ab.py gmm1000_s0,gmm1000_s1,er1000,gmm200_s7 15
+step df_prof 240 python -u scripts/df_prof.py gmm1000_s0
+step pytest_parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_degree.py -q --timeout 120 --timeout-method thread -p no:cacheprovider
