@@ -142,6 +142,7 @@ struct md_ctx {
   // dataflow mode (single-graph rollouts without grid barriers, md_kernels.hip df_*): tagged
   // granule buffer sized for the largest graph that qualifies (df_graph); MD_DF=0 turns it off
   bool df_on = true;
+  bool df_r0 = false;  // measured: no gain over the early-word prebuild alone
   DevBuf<unsigned long long> dfbuf;
   int df_mt = 0, df_n = 0;
   std::vector<char> df_graph;
@@ -267,6 +268,7 @@ const char* err_name(int e) {
     case 5: return "host selection failed";
     case 6: return "kernel argument layout differs from the compiled assumption";
     case 7: return "dataflow mode: a tile's alive-neighbour list exceeded NB_CAP";
+    case 8: return "dataflow mode: phase A's state differs from its early step record";
     default: return e >= 1000 ? "bounds check failed (debug build; site = code - 1000)" : "unknown device error";
   }
 }
@@ -528,6 +530,7 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
     p.df = c->dfbuf.p;
     p.df_mt = c->df_mt;
     p.df_n = c->df_n;
+    p.df_r0 = c->df_r0 ? 1 : 0;
   }
   p.qmode = qmode ? 1 : 0;
   p.qpair = c->pair_on ? 1 : 0;
@@ -719,7 +722,10 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_HOST_HANDSHAKE")) c->host_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_POLL_US")) c->poll_us = std::atoi(v);
   if (const char* v = std::getenv("MD_H0G")) c->h0g_on = std::atoi(v) != 0;
-  if (const char* v = std::getenv("MD_DF")) c->df_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MD_DF")) {
+    c->df_on = std::atoi(v) != 0;
+    c->df_r0 = std::atoi(v) == 2;  // MD_DF=2: with the prebuild from speculative workgroup 0's result
+  }
   if (const char* v = std::getenv("MD_SPEC")) c->spec_n = std::max(0, std::min(SPEC_MAX, std::atoi(v)));
   md_status st = MD_OK;
   do {
@@ -986,8 +992,9 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
       }
     c->sres_stride = ((maxw + 63) / 64) * 64;
     if (maxw > 0) {
-      HIPCHK(c, c->sres.alloc((size_t)SPEC_MAX * c->sres_stride));
-      HIPCHK(c, hipMemset(c->sres.p, 0, sizeof(int) * (size_t)SPEC_MAX * c->sres_stride));
+      // two slots per speculative workgroup: requests alternate between them (spec_slot_index)
+      HIPCHK(c, c->sres.alloc((size_t)2 * SPEC_SLOTS * c->sres_stride));
+      HIPCHK(c, hipMemset(c->sres.p, 0, sizeof(int) * (size_t)2 * SPEC_SLOTS * c->sres_stride));
       HIPCHK(c, c->qspec.alloc(2 * tn));
     } else {
       c->sres.release();

@@ -176,13 +176,15 @@ struct Params {
   // dataflow mode (single-graph rollouts in dedicated mode with the layer split, md_kernels.hip
   // df_*): no grid barrier; the step record, the H rows, the virtual-node and arg-max partials
   // move as data-tagged granules {value, tag} in this buffer (graph-local node / tile indices,
-  // zeroed per launch; layout df_ap / df_sp / df_hb).  null: the barrier protocol.
+  // zeroed per launch; layout df_ap / df_sp / df_hb, rows and sums by step parity).  null: the
+  // barrier protocol.
   unsigned long long* df;
   int df_mt;                       // tiles of the largest graph the buffer is sized for
   int df_n;                        // nodes of that graph
+  int df_r0;                       // 1: tiles prebuild from speculative workgroup 0's result before phase A picks
 };
 // dataflow buffer size (granules) for graphs of at most n nodes / mt tiles
-inline long long df_granules(int n, int mt) { return 64 + 388LL * mt + 4LL * 64 * n; }
+inline long long df_granules(int n, int mt) { return 64 + 772LL * mt + 8LL * 64 * n; }
 
 // Speculative-step result slot (ints):
 //   [0..1] u64 done tag {nd << 48 | candidate << 32 | request tag}, written last
@@ -195,6 +197,11 @@ inline long long df_granules(int n, int mt) { return 64 + 388LL * mt + 4LL * 64 
 //   [SRES_HDR, +3 nd) killed edges {edge (LDS id) | new state << 16, CSR slot, CSR slot}
 //   [sres_deg, +2 n) residual degrees per layer; [sres_live, +4 n) live-list entries
 constexpr int SRES_HDR = 32, SRES_STARTED = 8, SRES_FEAT = 22;
+// Result slots are double-buffered by the parity of the request's step: slot k of request step
+// ps is k + SPEC_SLOTS * (ps & 1), so the next request never rewrites a slot that the tile
+// workgroups may still be reading for their iteration-1 prebuild.
+constexpr int SPEC_SLOTS = 32;
+__host__ __device__ inline int spec_slot_index(int k, int ps) { return k + SPEC_SLOTS * (ps & 1); }
 __host__ __device__ inline int sres_deg(int et) { return SRES_HDR + 3 * et; }
 __host__ __device__ inline int sres_live(int et, int n) { return (sres_deg(et) + 2 * n + 3) & ~3; }
 __host__ __device__ inline int sres_words(int et, int n) { return sres_live(et, n) + 4 * n; }

@@ -814,11 +814,15 @@ __device__ __forceinline__ void env_stage_lds(const EnvView<false>& E, int n) {
 // state, both CSR flags) is issued here.  The caller has covered the node.
 __device__ __forceinline__ int env_apply_spec(const EnvView<false>& E, const int* slot, int nd, int* pr, int* cc) {
   // the header (and whether the features are published too) in the kill list's round trip
-  int h[5] = {0, 0, 0, 0, 0};
+  int h[5] = {0, 0, 0, 0, 0}, fa[6] = {0, 0, 0, 0, 0, 0};
   unsigned long long ft = 0ull, dt = 0ull;
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int i = 0; i < 5; ++i) h[i] = ldc(slot + 2 + i);
+    // the result's aggregates (live count, dmax, degree sums, mismatch flag): the dataflow
+    // mode's early step record
+#pragma unroll
+    for (int i = 0; i < 6; ++i) fa[i] = ldc(slot + 12 + i);
     ft = __hip_atomic_load((const g_u64*)(slot + SRES_FEAT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     dt = __hip_atomic_load((const g_u64*)slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -847,6 +851,8 @@ __device__ __forceinline__ int env_apply_spec(const EnvView<false>& E, const int
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int i = 0; i < 5; ++i) E.tmp[A_TMP_WORDS - 8 + i] = h[i];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) E.tmp[A_TMP_WORDS - 16 + i] = fa[i];
     // features of the same result already published? (used after this point only)
     E.tmp[A_TMP_WORDS - 3] = (unsigned)ft == (unsigned)dt && (ft >> 32) == ((dt >> 32) & 0xffffu);
   }
@@ -963,7 +969,7 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
         // could, so waiting for it is never slower than computing it here
         // tags as phase A read them beside the arg-max partials (L_PREF, free until the tile
         // prefix), polled again only while a taken result is still running
-        const g_u64* tp = (const g_u64*)(p.sres + (size_t)threadIdx.x * p.sres_stride);
+        const g_u64* tp = (const g_u64*)(p.sres + (size_t)spec_slot_index(threadIdx.x, ps) * p.sres_stride);
         const unsigned long long* pre = (const unsigned long long*)(lds_base + L_PREF) + 2 * threadIdx.x;
         unsigned long long v = pre[0];
         const unsigned long long st = pre[1];
@@ -980,7 +986,7 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
           }
         }
         if (done) {
-          E.tmp[A_TMP_WORDS - 1] = threadIdx.x;
+          E.tmp[A_TMP_WORDS - 1] = spec_slot_index(threadIdx.x, ps);  // the slot, parity included
           E.tmp[A_TMP_WORDS - 2] = (int)(v >> 48);  // killed edges
           if (sts != nullptr) {
             sts[70] = threadIdx.x + 1;
@@ -1032,6 +1038,24 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
       if (k == 0 && spec_slot >= 0) {
         lm = env_apply_spec(E, p.sres + (size_t)spec_slot * p.sres_stride, spec_nd, pr, c);
         if (threadIdx.x == 0) gv.spec_hits += 1;
+        if (p.df != nullptr && pend_n == 1 && p.run_mode == RUN_ROLLOUT && E.tmp[A_TMP_WORDS - 3] && threadIdx.x == 0) {
+          // dataflow mode, early step record: with the result's features published, the state
+          // after this step is known now (live count, and whether it stays running: alive edges
+          // in both layers, no K2 end-game, no live-set mismatch); tile workgroups whose
+          // iteration-1 prebuild used this result start their step on it while this phase A
+          // finishes (the others, and the graph head, wait for the record's "full" granule)
+          const int nl = E.tmp[A_TMP_WORDS - 16], dm0 = E.tmp[A_TMP_WORDS - 15], dm1 = E.tmp[A_TMP_WORDS - 14];
+          const int sd0 = E.tmp[A_TMP_WORDS - 13], sd1 = E.tmp[A_TMP_WORDS - 12], bad = E.tmp[A_TMP_WORDS - 11];
+          const bool eg = p.endgame && p.node_w == nullptr && n < 32768 && nl > 0 && dm0 == 1 && dm1 == 1;
+          volatile int* misc = (volatile int*)(lds_base + L_MISC);
+          if (!bad && sd0 > 0 && sd1 > 0 && !eg && misc[56] != 0) {
+            const unsigned tag = (unsigned)(misc[60] + 1);
+            const int v[6] = {ST_RUN, nl, misc[56], misc[57], misc[56], misc[57]};
+#pragma unroll
+            for (int i = 0; i < 6; ++i) df_st(p.df + DF_REC + i, __int_as_float(v[i]), tag);
+            misc[48] = 1;
+          }
+        }
       } else {
         lm = mcc_fixed_point<GL>(E, pr, acc, a, c);
       }

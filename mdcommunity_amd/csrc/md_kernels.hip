@@ -121,7 +121,7 @@ static_assert(2 * STG_ROWS * 64 <= S_HID - S_M, "neighbour staging fits [S_M, S_
 constexpr float NEG_INF = -__builtin_huge_valf();
 constexpr unsigned long long BARRIER_TIMEOUT_TICKS = 400000000ull;  // 4 s at 100 MHz
 enum : int { ERR_TIMEOUT = 1, ERR_COVERED = 2, ERR_LIVE_MISMATCH = 3, ERR_BADNODE = 4, ERR_HOST = 5, ERR_ABI = 6,
-             ERR_DF_LISTS = 7 };
+             ERR_DF_LISTS = 7, ERR_DF_EARLY = 8 };
 
 // Kernel arguments of md_rollout_kernel / md_env_kernel, (Params, const float*), read in every
 // device function through the implicit-argument pointer (SGPRs s[8:9] in callees) at a fixed
@@ -278,7 +278,10 @@ __device__ __forceinline__ void gv_store(KParams& p, int g, const GraphVar* src)
 constexpr unsigned BAR_ERR = 0x80000000u;
 constexpr int BAR_SHARDS = 8, BAR_STRIDE = 64;  // grid-barrier counter shards, one 256-byte line each
 __device__ __forceinline__ void raise_err(KParams& p, int code) {
-  __hip_atomic_store(p.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the first error wins (later ones are usually its consequences: a workgroup that gave up
+  // waiting on data the failed one never produced)
+  int zero = 0;
+  __hip_atomic_compare_exchange_strong(p.err, &zero, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_fetch_or((g_u32*)p.bar, BAR_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // Debug builds (-DMD_DEBUG_BOUNDS): index checks that raise error 1000 + site instead of
@@ -318,9 +321,19 @@ __device__ __forceinline__ bool md_bok(bool ok, int site) {
 constexpr int DF_REC = 0;  // record granules: status, n_live, confirmation lo / hi, early word lo / hi
 __device__ __forceinline__ unsigned df_tag(int pstep) { return (unsigned)(pstep + 1) << 1; }
 __device__ __forceinline__ unsigned long long* df_ap(KParams& p) { return p.df + 64; }
-__device__ __forceinline__ unsigned long long* df_sp(KParams& p) { return p.df + 64 + 4 * (size_t)p.df_mt; }
-__device__ __forceinline__ unsigned long long* df_hb(KParams& p, int l, int b) {
-  return p.df + 64 + 388 * (size_t)p.df_mt + (size_t)(2 * l + b) * 64 * p.df_n;
+// Rows and virtual-node partial sums are double-buffered by step parity (the parity of a step's
+// data comes from its tag): the iteration-1 prebuild of step t + 1 may start while tiles still
+// read step t's rows.
+__device__ __forceinline__ int df_par(unsigned tag) { return (int)(((tag & 0xffffffu) >> 1) - 1u) & 1; }
+__device__ __forceinline__ unsigned long long* df_sp(KParams& p, int par) {
+  return p.df + 64 + 4 * (size_t)p.df_mt + (size_t)par * 384 * p.df_mt;
+}
+__device__ __forceinline__ unsigned long long* df_hb(KParams& p, int l, int b, int par) {
+  return p.df + 64 + 772 * (size_t)p.df_mt + (size_t)(4 * l + 2 * par + b) * 64 * p.df_n;
+}
+// tag of iteration-1 data a prebuild wrote from the speculative result ew (its slot in bits 24-29)
+__device__ __forceinline__ unsigned df_ptag(unsigned tn, unsigned long long ew) {
+  return tn | 1u | ((unsigned)(ew & 63u) << 24);
 }
 __device__ __forceinline__ void df_st(unsigned long long* a, float v, unsigned tag) {
   __hip_atomic_store((g_u64*)a, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
@@ -693,8 +706,8 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
       }
     } else if ((int)threadIdx.x < 64 + p.n_spec && p.df == nullptr) {
       // speculative results' tags, read beside the partials (env_step matches them against
-      // the chosen node without a round trip of its own)
-      const g_u64* tp = (const g_u64*)(p.sres + (size_t)(threadIdx.x - 64) * p.sres_stride);
+      // the chosen node without a round trip of its own); the previous step's request's slots
+      const g_u64* tp = (const g_u64*)(p.sres + (size_t)spec_slot_index(threadIdx.x - 64, misc[60] - 1) * p.sres_stride);
       unsigned long long* pre = (unsigned long long*)(lds + L_PREF) + 2 * (threadIdx.x - 64);
       pre[0] = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       pre[1] = __hip_atomic_load(tp + SRES_STARTED / 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -702,9 +715,11 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
     if (p.df != nullptr) {
       // dataflow mode: phase A starts polling the partials as the step's tiles start, so the
       // tags are read once every partial has arrived (as fresh as beside barrier mode's partials)
+      if (p.prof != nullptr && threadIdx.x == 0 && misc[60] - 1 < p.prof_cap)  // diagnostics: slot 11 of the step
+        p.prof[(size_t)(misc[60] - 1) * PROF_SLOTS + 11] = wall_clock64();
       __syncthreads();
       if (threadIdx.x >= 64 && (int)threadIdx.x < 64 + p.n_spec) {
-        const g_u64* tp = (const g_u64*)(p.sres + (size_t)(threadIdx.x - 64) * p.sres_stride);
+        const g_u64* tp = (const g_u64*)(p.sres + (size_t)spec_slot_index(threadIdx.x - 64, misc[60] - 1) * p.sres_stride);
         unsigned long long* pre = (unsigned long long*)(lds + L_PREF) + 2 * (threadIdx.x - 64);
         pre[0] = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         pre[1] = __hip_atomic_load(tp + SRES_STARTED / 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1119,12 +1134,21 @@ __device__ __noinline__ int prebuild_lists(KParams&, const GraphInfo gi, int j, 
   const unsigned want = (unsigned)(ew >> 32);
   const int* sl = p.sres + (size_t)slot * p.sres_stride;
   const int n = gi.n, et = gi.e[0] + gi.e[1];
+  lds_i32* kh = (lds_i32*)(int*)(scr + S_M);
+  for (int i = threadIdx.x; i < KH_SIZE; i += NTHREADS) kh[i] = -1;
   if (threadIdx.x == 0) {
+    // the features tag, the done tag and the live count polled together (one round trip when
+    // the result is complete, as it usually is once phase A took it)
     const unsigned long long ft_want = ((unsigned long long)(unsigned)a << 32) | want;
     const unsigned long long t0 = wall_clock64();
     int ok = 0;
+    unsigned long long dt;
+    int nl;
     while (true) {
-      if (__hip_atomic_load((const g_u64*)(sl + SRES_FEAT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ft_want) {
+      const unsigned long long ft = __hip_atomic_load((const g_u64*)(sl + SRES_FEAT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      dt = __hip_atomic_load((const g_u64*)sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      nl = ldc(sl + 12);
+      if (ft == ft_want) {
         ok = 1;
         break;
       }
@@ -1133,37 +1157,61 @@ __device__ __noinline__ int prebuild_lists(KParams&, const GraphInfo gi, int j, 
         break;
       __builtin_amdgcn_s_sleep(1);
     }
-    const unsigned long long dt = __hip_atomic_load((const g_u64*)sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (the features tag is written after the done tag and the live count, but loads of one
+    // round trip are not ordered: the data round trip below reads both again to confirm)
     const int nd = (int)(dt >> 48);
-    if (ok && ((unsigned)dt != want || (int)((dt >> 32) & 0xffffu) != a || nd > KH_SIZE / 2)) ok = 0;
+    // (at most KH_SIZE / 2 CSR slots in the killed-edge set: the probes always find a free entry)
+    if (ok && ((unsigned)dt != want || (int)((dt >> 32) & 0xffffu) != a || nd > KH_SIZE / 4)) ok = 0;
     misc[44] = ok;
     misc[45] = nd;
-    misc[46] = ldc(sl + 12);  // live nodes
+    misc[46] = nl;
   }
   __syncthreads();
   if (!misc[44]) return 0;
   const int nd = misc[45], nl = misc[46];
-  lds_i32* kh = (lds_i32*)(int*)(scr + S_M);
-  for (int i = threadIdx.x; i < KH_SIZE; i += NTHREADS) kh[i] = -1;
+  // the tile's rows from the result's live list (entries as in phase A's list) and every killed
+  // edge's three words, all in one round trip
+  float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (threadIdx.x < TILE) e = ldc4((const float*)(sl + sres_live(et, n)), min(j * TILE + (int)threadIdx.x, n - 1) * 16);
+  constexpr int KPT = (KH_SIZE / 4 + NTHREADS - 1) / NTHREADS;
+  int kv[KPT], k1[KPT], k2[KPT];
+#pragma unroll
+  for (int u = 0; u < KPT; ++u) {
+    const int i = threadIdx.x + u * NTHREADS;
+    if (i < nd) {
+      kv[u] = ldc(sl + SRES_HDR + 3 * i);
+      k1[u] = ldc(sl + SRES_HDR + 3 * i + 1);
+      k2[u] = ldc(sl + SRES_HDR + 3 * i + 2);
+    }
+  }
+  if (threadIdx.x == 0) {
+    const unsigned long long dt2 = __hip_atomic_load((const g_u64*)sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    misc[47] = ((int)(dt2 >> 48) == nd && (unsigned)dt2 == want && ldc(sl + 12) == nl && nl <= n);
+  }
+  __syncthreads();
+  if (!misc[47]) return 0;  // (else not built: the tile builds after the record)
   if (threadIdx.x < TILE) {
-    // the tile's rows from the result's live list (entries as in phase A's list)
+    // entries validated whatever the slot holds: a workgroup that lags may read a slot being
+    // rewritten (its prebuild is then never used, but every address it forms stays in bounds)
     const int r = j * TILE + threadIdx.x;
-    const float4 e = ldc4((const float*)(sl + sres_live(et, n)), min(r, n - 1) * 16);
-    const bool ok = r < nl && MD_BOK(__float_as_int(e.x) >= 0 && __float_as_int(e.x) < n && nl <= n, 6);
     const unsigned c = (unsigned)__float_as_int(e.w);
+    const bool ok = r < nl && __float_as_int(e.x) >= 0 && __float_as_int(e.x) < n && __float_as_int(e.y) >= 0 &&
+                    __float_as_int(e.y) + (int)(c & 0xffffu) <= 2 * gi.e[0] && __float_as_int(e.z) >= 0 &&
+                    __float_as_int(e.z) + (int)(c >> 16) <= 2 * gi.e[1];
     rows[threadIdx.x] = ok ? __float_as_int(e.x) : -1;
     hdr[64 + threadIdx.x] = ok ? __float_as_int(e.y) : 0;
     hdr[96 + threadIdx.x] = ok ? (int)(c & 0xffffu) : 0;
     hdr[64 + 16 + threadIdx.x] = ok ? __float_as_int(e.z) : 0;
     hdr[96 + 16 + threadIdx.x] = ok ? (int)(c >> 16) : 0;
   }
-  __syncthreads();
   // the killed edges of layer L: both CSR positions into the set
-  for (int i = threadIdx.x; i < nd; i += NTHREADS) {
-    const int v = ldc(sl + SRES_HDR + 3 * i), e = v & 0xffff;
-    if ((e < gi.e[0] ? 0 : 1) != L) continue;
-    kh_insert(kh, ldc(sl + SRES_HDR + 3 * i + 1));
-    kh_insert(kh, ldc(sl + SRES_HDR + 3 * i + 2));
+#pragma unroll
+  for (int u = 0; u < KPT; ++u) {
+    const int i = threadIdx.x + u * NTHREADS;
+    if (i < nd && ((kv[u] & 0xffff) < gi.e[0] ? 0 : 1) == L) {
+      kh_insert(kh, k1[u]);
+      kh_insert(kh, k2[u]);
+    }
   }
   __syncthreads();
   return build_nb_lists(p, gi, rows, scr, nullptr, L, true) ? 1 : 2;
@@ -1309,8 +1357,11 @@ __device__ __noinline__ void nbc_store(KParams&, int slot, const float*, bool ok
 // two features each in CSR order.
 // deg_ovr / hp_ovr (iteration 1 speculated during phase A): the residual degrees and the
 // first-layer rows of the speculative result instead of the graph's arrays.
+// dcap: first-layer rows by degree are clamped to [0, dcap] (the prebuild's table of the result's
+// dmax: a prebuild from a slot being rewritten must not address beyond it).
 __device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it, const int*, float*, int L,
-                                           const int* deg_ovr = nullptr, const float* hp_ovr = nullptr) {
+                                           const int* deg_ovr = nullptr, const float* hp_ovr = nullptr,
+                                           int dcap = 0x7fffffff) {
   const int* const rows = (const int*)(lds_base() + L_SCR + S_ROW);
   float* const scr = lds_base() + L_SCR;
 
@@ -1333,7 +1384,7 @@ __device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it,
   const int v = rows[r];
   float2 own = {0.f, 0.f}, acc = {0.f, 0.f};
   if (v >= 0) {
-    const int ov = table ? ldc(deg + v) : v;
+    const int ov = table ? min(max(ldc(deg + v), 0), dcap) : v;
     if (MD_BOK(v < gi.n && ov >= 0 && ov < gi.n, 1)) own = ldc2(hp, ov * 256 + q * 8);
   }
   const int myoff = hdr[l * 16 + r], mycnt = hdr[32 + l * 16 + r];
@@ -1350,7 +1401,7 @@ __device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it,
       src[i] = -1;
       if (b < nbat && k < SROWS * 16 && row < totl) {
         const int id = nbl[row];
-        src[i] = MD_BOK(id < gi.n, 4) ? (table ? ldc(deg + id) : id) : -1;
+        src[i] = MD_BOK(id < gi.n, 4) ? (table ? min(max(ldc(deg + id), 0), dcap) : id) : -1;
         if (!MD_BOK(src[i] < gi.n, 5)) src[i] = -1;
       }
     }
@@ -1418,12 +1469,12 @@ __device__ __noinline__ void gather_df(KParams&, const GraphInfo gi, int it, int
   const int w = wave_id(), lane = lane_id(), t = threadIdx.x;
   const int q = lane & 31;
   const int r = 2 * w + (lane >> 5);
-  const float* hb = (const float*)df_hb(p, L, it - 2);
+  const float* hb = (const float*)df_hb(p, L, it - 2, df_par(ta));
   const lds_i32* hdr = (const lds_i32*)(const int*)(scr + S_NBH);
   const lds_u16* nbl = (const lds_u16*)(const uint16_t*)(scr + S_NBL) + L * NB_CAP;
   const int v = rows[r];
   float4 ox = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (v >= 0 && MD_BOK(v < gi.n, 1)) ox = ldc4(hb, v * 512 + q * 16);
+  if (v >= 0 && MD_BOK(v < gi.n && v < p.df_n, 1)) ox = ldc4(hb, v * 512 + q * 16);
   float2 acc = {0.f, 0.f};
   const int myoff = hdr[L * 16 + r], mycnt = hdr[32 + L * 16 + r];
   const int totl = hdr[128 + L];
@@ -1433,7 +1484,7 @@ __device__ __noinline__ void gather_df(KParams&, const GraphInfo gi, int it, int
   auto src_of = [&](int base, int i) {
     const int k = t + NTHREADS * i, row = base + (k >> 5);
     const int id = nbl[row];
-    return MD_BOK(id < gi.n, 4) ? id * 512 + (k & 31) * 16 : 0;
+    return MD_BOK(id < gi.n && id < p.df_n, 23) ? id * 512 + (k & 31) * 16 : 0;
   };
   auto issue = [&](int b, float4 (&x)[NLD], bool (&ok)[NLD]) {
     const int base = b * SROWS;
@@ -1605,7 +1656,7 @@ __device__ __noinline__ void df_store_tile(KParams&, int j, int L, int it, unsig
     const float* ate = scr + S_E + L * 64 * LDT + c * LDT;
     const float* atx = scr + S_X + L * 64 * LDT + c * LDT;
     const int nv = tile_rows_valid(rows);
-    unsigned long long* sp = df_sp(p) + (size_t)j * 384;
+    unsigned long long* sp = df_sp(p, df_par(tag)) + (size_t)j * 384;
     const float s_new = col_sum16(ate, nv);
     if (it == 1) {
       df_st(sp + L * 64 + c, col_sum16(atx, nv), tag);  // S0 (first-layer input)
@@ -1618,14 +1669,15 @@ __device__ __noinline__ void df_store_tile(KParams&, int j, int L, int it, unsig
   const int v = rows[rr];
   const float* e = scr + S_E + L * 64 * LDT;
   const float tf = __uint_as_float(tag);
-  if (v >= 0)
-    stc4((float*)df_hb(p, L, it - 1), v * 512 + c2 * 16,
+  if (v >= 0 && MD_BOK(v < p.df_n && j < p.df_mt, 21))
+    stc4((float*)df_hb(p, L, it - 1, df_par(tag)), v * 512 + c2 * 16,
          make_float4(e[(2 * c2) * LDT + rr], tf, e[(2 * c2 + 1) * LDT + rr], tf));
 }
 
-// dft != 0 (dataflow mode): the outputs go out as granules tagged dft (df_store_tile).
+// dft != 0 (dataflow mode): the outputs go out as granules tagged dft (df_store_tile); defer:
+// none at all -- they stay in LDS (E, X) for df_store_tile once the result is confirmed.
 __device__ __noinline__ bool spec_iteration1(KParams&, const GraphInfo gi, int j, int L, unsigned long long ew,
-                                             unsigned dft = 0) {
+                                             unsigned dft = 0, bool defer = false) {
   KParams& p = kp();
   float* const lds = lds_base();
   float* const scr = lds + L_SCR;
@@ -1633,17 +1685,19 @@ __device__ __noinline__ bool spec_iteration1(KParams&, const GraphInfo gi, int j
   const int* sl = p.sres + (size_t)(ew & 0xffffu) * p.sres_stride;
   const int n = gi.n, et = gi.e[0] + gi.e[1];
   const float* hp = nullptr;
+  int dm = 0x7fffffff;
   if (p.node_w == nullptr) {  // unit cost: rows by degree, from the precomputed table of the result's dmax
-    const int dm = ldc(sl + 13 + L);
+    dm = ldc(sl + 13 + L);
     if (p.h0g == nullptr || (p.variant & 4) || dm < 1 || dm > p.h0g_dm) return false;
     hp = p.h0g + (h0g_row(dm, 1) - 1) * EMB;
   }
-  gather_tile2s(p, gi, 1, rows, scr, L, sl + sres_deg(et) + L * n, hp);
+  gather_tile2s(p, gi, 1, rows, scr, L, sl + sres_deg(et) + L * n, hp, dm);
   __syncthreads();
   update_tile_split(lds + L_W, scr, L);
   __syncthreads();
   normalize_tile_split(scr + S_E, scr, L);
   __syncthreads();
+  if (defer) return true;
   if (dft != 0) {
     df_store_tile(p, j, L, 1, dft);
     __syncthreads();
@@ -1768,7 +1822,7 @@ __device__ void graph_sum(KParams& p, const GraphInfo& gi, int nt, int slot, flo
   const float* sp = p.spart + (size_t)gi.tile_off * 384 + slot * 128 + o;
   float a = 0.f;
   if (ta != 0) {
-    const unsigned long long* sg = df_sp(p) + slot * 128 + o;
+    const unsigned long long* sg = df_sp(p, df_par(ta)) + slot * 128 + o;
     for (int jb = j0; jb < j1; jb += 16) {
       unsigned long long gx[16];
 #pragma unroll
@@ -3758,7 +3812,6 @@ __device__ __noinline__ void spec_loop(KParams&) {
   const int k = (int)blockIdx.x - p.n_main;
   const GraphInfo gi = p.ginfo[p.glist[0]];
   const int n = gi.n, et = gi.e[0] + gi.e[1];
-  int* slot = p.sres + (size_t)k * p.sres_stride;
   int* ia = (int*)(lds + L_W);
   const EnvView<false> E = env_view<false>(p, gi, ia);
   // ranking scratch after the environment: qv[n] (Q of live nodes, -inf otherwise), gmx[G]
@@ -3793,6 +3846,7 @@ __device__ __noinline__ void spec_loop(KParams&) {
     if (misc[0]) return;
     const unsigned tag = (unsigned)misc[1];
     const int qb = (misc[2] - 1) & 1;  // buffer of the previous prediction
+    int* const slot = p.sres + (size_t)spec_slot_index(k, misc[2]) * p.sres_stride;  // this request's parity
     last = ((unsigned long long)(unsigned)misc[2] << 32) | tag;
     // diagnostics (md_profile): workgroup 0's timeline in the request step's slots 65-68
     unsigned long long* ts = p.prof != nullptr && k == 0 && misc[2] < p.prof_cap ? p.prof + (size_t)misc[2] * PROF_SLOTS : nullptr;
@@ -3996,27 +4050,37 @@ __device__ __noinline__ void spec_loop(KParams&) {
 // tiles building the iteration-1 prebuild from phase A's early word meanwhile), then run the
 // step with every hand-off polled as tagged granules.
 
-// Waits for the step record tagged `tag`: 1 when it is there (its six words in misc[50..55]),
-// 2 when `watch` is set and the early word changed first (new value in the LDS word at
+// Waits for the step record tagged `tag`: 1 when it is there (its six words in misc[50..55];
+// with `full`, also its "full" granule: phase A has finished, not just published the record
+// early), 2 when `watch` is set and the early word changed first (new value in the LDS word at
 // L_MISC + 42), 0 on an error anywhere.  Uniform.
-__device__ __noinline__ int df_wait_rec(KParams&, unsigned tag, bool watch) {
+// With `watch`, also 3 when speculative workgroup 0's result for this step's request (spec_req of
+// step req_step) has its features published and differs from the LDS word at L_MISC + 38 (then
+// updated): the likeliest next state, prebuilt before phase A has picked.
+__device__ __noinline__ int df_wait_rec(KParams&, unsigned tag, bool watch, bool full = false, int req_step = -1) {
   KParams& p = kp();
   int* const misc = (int*)(lds_base() + L_MISC);
   unsigned long long* const seen = (unsigned long long*)(lds_base() + L_MISC + 42);
+  unsigned long long* const tried0 = (unsigned long long*)(lds_base() + L_MISC + 38);
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     const bool w = watch && p.pre_ew != nullptr;
-    const unsigned long long sv = *seen;
+    const bool w0 = w && req_step >= 0 && p.sres != nullptr && p.spec_req != nullptr;
+    const unsigned long long sv = *seen, s0 = *tried0;
     const unsigned long long t0 = wall_clock64();
     int res = 0;
     while (true) {
-      // lanes 0-5: the record's granules, lane 6: the error word, lane 7: the early word
+      // lanes 0-6: the record's granules (6: "full"), lane 8: the error word, lane 7: the early word
       unsigned long long g = 0ull;
-      if (lane < 6) g = __hip_atomic_load((const g_u64*)(p.df + DF_REC + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else if (lane == 6) g = __hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane < 7) g = __hip_atomic_load((const g_u64*)(p.df + DF_REC + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else if (lane == 8) g = __hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else if (lane == 7 && w) g = __hip_atomic_load((const g_u64*)p.pre_ew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (__ballot(lane == 6 && (g & BAR_ERR))) break;
-      if (!__ballot(lane < 6 && (unsigned)(g >> 32) != tag)) {
+      else if (lane == 9 && w0) g = __hip_atomic_load((const g_u64*)p.spec_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else if (lane == 10 && w0)
+        g = __hip_atomic_load((const g_u64*)(p.sres + (size_t)spec_slot_index(0, req_step) * p.sres_stride + SRES_FEAT),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__ballot(lane == 8 && (g & BAR_ERR))) break;
+      if (!__ballot((lane < 6 || (lane == 6 && full)) && (unsigned)(g >> 32) != tag)) {
         if (lane < 6) misc[50 + lane] = (int)(unsigned)g;
         res = 1;
         break;
@@ -4028,6 +4092,20 @@ __device__ __noinline__ int df_wait_rec(KParams&, unsigned tag, bool watch) {
           if (lane == 0) *seen = ew;
           res = 2;
           break;
+        }
+      }
+      if (w0) {
+        const unsigned rlo = __shfl((unsigned)g, 9, 64), rhi = __shfl((unsigned)(g >> 32), 9, 64);
+        const unsigned flo = __shfl((unsigned)g, 10, 64), fhi = __shfl((unsigned)(g >> 32), 10, 64);
+        if ((int)rhi == req_step && rlo == flo && rlo != 0u) {
+          // early word form {request tag << 32 | candidate << 16 | slot}
+          const unsigned long long e0 = ((unsigned long long)rlo << 32) | ((unsigned long long)(fhi & 0xffffu) << 16) |
+                                        (unsigned)spec_slot_index(0, req_step);
+          if (e0 != s0) {
+            if (lane == 0) *tried0 = e0;
+            res = 3;
+            break;
+          }
         }
       }
       __builtin_amdgcn_s_sleep(1);
@@ -4055,7 +4133,10 @@ __device__ __noinline__ void df_env(KParams&) {
   unsigned long long last_ew = 0ull;  // the early word as the tiles see it after this phase A
   for (int pstep = 0;; ++pstep) {
     MD_PROF(0);
-    if (threadIdx.x == 0) misc[60] = pstep;
+    if (threadIdx.x == 0) {
+      misc[60] = pstep;
+      misc[48] = 0;  // set by env_step when it published the step record early
+    }
     __syncthreads();
     staged = phase_a(p, g, have_q, lds, staged);
     MD_PROF(3);
@@ -4067,9 +4148,12 @@ __device__ __noinline__ void df_env(KParams&) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of phase A is done
     __syncthreads();
     const int st = gv.status;
-    if (threadIdx.x < 6) {
+    const bool early = misc[48] != 0;
+    if (early && threadIdx.x == 0 && (st != ST_RUN || (unsigned)misc[54] != (unsigned)last_ew))
+      raise_err(p, ERR_DF_EARLY);  // (cannot happen: the early record promised this state)
+    if (threadIdx.x < 7 && (threadIdx.x == 6 || !early)) {
       const int k = threadIdx.x;
-      const int v = k == 0 ? st : k == 1 ? gv.n_live : k < 4 ? misc[52 + k] : k == 4 ? (int)(unsigned)last_ew : (int)(unsigned)(last_ew >> 32);
+      const int v = k == 0 ? st : k == 1 ? gv.n_live : k < 4 ? misc[52 + k] : k == 4 ? (int)(unsigned)last_ew : k == 5 ? (int)(unsigned)(last_ew >> 32) : 1;
       df_st(p.df + DF_REC + k, __int_as_float(v), (unsigned)(pstep + 1));
     }
     // the record lands before any later early word (a tile that sees the next step's early word
@@ -4097,8 +4181,9 @@ __device__ __noinline__ void df_head(KParams&) {
   for (int pstep = 0;; ++pstep) {
     if (threadIdx.x == 0) misc[60] = pstep;
     __syncthreads();
-    if (df_wait_rec(p, (unsigned)(pstep + 1), false) != 1 || misc[50] != ST_RUN) break;
-    const unsigned tn = df_tag(pstep), tp = (misc[52] | misc[53]) != 0 ? tn | 1u : tn;
+    if (df_wait_rec(p, (unsigned)(pstep + 1), false, true) != 1 || misc[50] != ST_RUN) break;
+    const unsigned long long cw = ((unsigned long long)(unsigned)misc[53] << 32) | (unsigned)misc[52];
+    const unsigned tn = df_tag(pstep), tp = cw != 0ull ? df_ptag(tn, cw) : tn;
     head_iteration(p, lds, scr, g, 2, (unsigned long long)(pstep + 1), tn, tp);
     head_iteration(p, lds, scr, g, 3, (unsigned long long)(pstep + 1), tn, tn);
   }
@@ -4112,6 +4197,20 @@ __device__ __noinline__ void df_head(KParams&) {
     if (p.prof != nullptr && tb == 0 && threadIdx.x == 0 && pstep < p.prof_cap)                     \
       p.prof[(size_t)pstep * PROF_SLOTS + (slot)] = wall_clock64();                                 \
   } while (0)
+// ... and the latest over every active tile workgroup: 43 record seen, 44 iteration 1 done, 45
+// iteration 2 done, 46 arg-max partial (layer 0) / layer-1 rows (layer 1) out
+// ... and per tile workgroup (rows 128 + 4 pstep + k of the profile, slot tb % 64, k = tb / 64
+// for the iteration-2 start, 2 + tb / 64 for the end of the prebuild)
+#define DF_STAMP_TILE(k)                                                                            \
+  do {                                                                                              \
+    if (p.prof != nullptr && threadIdx.x == 0 && 128 + 4 * pstep + 4 < p.prof_cap)                  \
+      p.prof[(size_t)(128 + 4 * pstep + (k) + (tb >> 6)) * PROF_SLOTS + (tb & 63)] = wall_clock64();  \
+  } while (0)
+#define DF_STAMP_MAX(slot)                                                                          \
+  do {                                                                                              \
+    if (p.prof != nullptr && threadIdx.x == 0 && pstep < p.prof_cap)                                \
+      atomicMax(p.prof + (size_t)pstep * PROF_SLOTS + (slot), wall_clock64());                      \
+  } while (0)
 // Tile workgroup (tile j, layer L) of the layer split.
 __device__ __noinline__ void df_tiles(KParams&) {
   KParams& p = kp();
@@ -4123,20 +4222,44 @@ __device__ __noinline__ void df_tiles(KParams&) {
   const GraphInfo gi = p.ginfo[g];
   const int tb = (int)blockIdx.x - 2 * p.n_env, j = tb >> 1, L = tb & 1;
   unsigned long long* const seen = (unsigned long long*)(lds + L_MISC + 42);
-  if (threadIdx.x == 0) *seen = 0ull;
+  unsigned long long* const tried0 = (unsigned long long*)(lds + L_MISC + 38);
+  if (threadIdx.x == 0) *seen = *tried0 = 0ull;
   for (int pstep = 0;; ++pstep) {
     if (threadIdx.x == 0) misc[60] = pstep;
     __syncthreads();
-    // the step record; meanwhile the iteration-1 prebuild from phase A's early word
+    // the step record; meanwhile the iteration-1 prebuild, first from speculative workgroup 0's
+    // result (the likeliest pick, ready before phase A has picked), then, if phase A's early word
+    // names another result, from that one (rows and sums are tagged with the result's slot)
+    // A prebuild from workgroup 0's result keeps its iteration-1 outputs in LDS until phase A's
+    // early word names that result (another result's prebuild then rebuilds the rows): its rows
+    // belong to that result's tile assignment, so storing them for a result phase A does not
+    // take could overwrite rows that other tiles own in the actual state.  A prebuild from the
+    // early word stores at once (the early word is the applied result unless the rollout ends).
     int pre_state = 0, r;
     unsigned long long pre_used = 0ull;
-    while ((r = df_wait_rec(p, (unsigned)(pstep + 1), true)) == 2) {
-      const unsigned long long ew = *seen;
-      if (pre_state == 0 && ew != 0ull) {
+    bool deferred = false;
+    while ((r = df_wait_rec(p, (unsigned)(pstep + 1), true, false, p.df_r0 ? pstep - 1 : -1)) >= 2) {
+      const unsigned long long ew = r == 2 ? *seen : *tried0;
+      if (ew != 0ull && ew != pre_used) {
+        DF_STAMP_MAX(54);
+        pre_used = 0ull;
+        deferred = false;
         pre_state = prebuild_lists(p, gi, j, L, ew);
+        DF_STAMP_MAX(55);
         if (pre_state) pre_used = ew;
-        // the whole of iteration 1 too (MD_VARIANT bit 128: lists only), tagged as prebuilt
-        if (pre_state == 1 && !(p.variant & 128) && spec_iteration1(p, gi, j, L, ew, df_tag(pstep) | 1u)) pre_state = 3;
+        // the whole of iteration 1 too (MD_VARIANT bit 128: lists only)
+        if (pre_state == 1 && !(p.variant & 128) &&
+            spec_iteration1(p, gi, j, L, ew, df_ptag(df_tag(pstep), ew), r == 3)) {
+          pre_state = 3;
+          deferred = r == 3;
+        }
+        DF_STAMP_MAX(56);
+        DF_STAMP_TILE(2);
+      } else if (r == 2 && ew == pre_used && deferred) {
+        // phase A took workgroup 0's result: its prebuilt outputs go out now
+        df_store_tile(p, j, L, 1, df_ptag(df_tag(pstep), ew));
+        __syncthreads();
+        deferred = false;
       }
     }
     if (r != 1 || misc[50] != ST_RUN) break;
@@ -4148,7 +4271,14 @@ __device__ __noinline__ void df_tiles(KParams&) {
     if (threadIdx.x == 0) *seen = ((unsigned long long)(unsigned)misc[55] << 32) | (unsigned)misc[54];
     if (j >= (nl + TILE - 1) / TILE) continue;
     const int pre_ok = pre_state != 0 && cw == pre_used ? pre_state : 0;
-    const unsigned tn = df_tag(pstep), tp = cw != 0ull ? tn | 1u : tn;
+    if (pre_ok == 3 && deferred) {  // (the early word was not seen before the record)
+      df_store_tile(p, j, L, 1, df_ptag(df_tag(pstep), cw));
+      __syncthreads();
+    }
+    // a tile without the confirmed prebuild reads phase A's outputs: the whole of phase A first
+    if (pre_ok != 3 && df_wait_rec(p, (unsigned)(pstep + 1), false, true) != 1) break;
+    DF_STAMP_MAX(43);
+    const unsigned tn = df_tag(pstep), tp = cw != 0ull ? df_ptag(tn, cw) : tn;
     bool nb_ok = true;
     // iteration 1 (skipped when the confirmed prebuild ran it)
     if (pre_ok != 3) {
@@ -4185,6 +4315,8 @@ __device__ __noinline__ void df_tiles(KParams&) {
       __syncthreads();
     }
     DF_STAMP(5);
+    DF_STAMP_MAX(44);
+    DF_STAMP_TILE(0);
     // iteration 2: the neighbours' iteration-1 rows (a confirmed prebuild's are valid too)
     gather_df(p, gi, 2, L, tn, tp);
     __syncthreads();
@@ -4196,6 +4328,7 @@ __device__ __noinline__ void df_tiles(KParams&) {
     df_store_tile(p, j, L, 2, tn);
     __syncthreads();
     DF_STAMP(6);
+    DF_STAMP_MAX(45);
     // iteration 3, then the layer-1 rows to the layer-0 workgroup, which runs the attention and
     // the Q head and publishes the arg-max partial
     gather_df(p, gi, 3, L, tn, tn);
@@ -4208,6 +4341,7 @@ __device__ __noinline__ void df_tiles(KParams&) {
     DF_STAMP(30);
     if (L == 1) {
       split_publish(p, scr, j, (unsigned long long)(pstep + 1));
+      DF_STAMP_MAX(47);
     } else {
       split_receive(p, scr, j, (unsigned long long)(pstep + 1));
       DF_STAMP(8);
@@ -4215,10 +4349,13 @@ __device__ __noinline__ void df_tiles(KParams&) {
                        nullptr);
       DF_STAMP(9);
       DF_STAMP(10);
+      DF_STAMP_MAX(46);
     }
   }
 }
 #undef DF_STAMP
+#undef DF_STAMP_MAX
+#undef DF_STAMP_TILE
 
 __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict__ wimg) {
   extern __shared__ __attribute__((aligned(16))) float lds[];

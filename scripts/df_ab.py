@@ -12,7 +12,8 @@ for name in names:
     z = np.load(os.path.join(ROOT, f"tests/golden/rollout_{name}.npz"))
     g = (int(z["n_nodes"]), z["edges0"], z["edges1"])
     res = {}
-    for df in ("0", "1", "0", "1"):
+    modes = os.environ.get("DF_MODES", "0,1").split(",")
+    for df in modes + modes:
         os.environ["MD_DF"] = df
         e = _lib.Engine(W)
         e.load_graphs([g])
@@ -26,8 +27,7 @@ for name in names:
             assert list(o2[0][0]) == list(out[0][0]), "rollout differs between repeats"
         e.close()
         res.setdefault(df, []).append((float(np.median(ts)), float(np.min(ts)), out))
-    seq0, seq1 = res["0"][0][2][0], res["1"][0][2][0]
-    same = list(seq0[0]) == list(seq1[0]) and list(seq0[1]) == list(seq1[1])
-    print("%s: %d removals; MD_DF=0 %s ms, MD_DF=1 %s ms (median / min per pass); identical rollouts: %s" % (
-        name, len(seq0[0]), ["%.3f/%.3f" % r[:2] for r in res["0"]], ["%.3f/%.3f" % r[:2] for r in res["1"]], same),
-        flush=True)
+    seq0 = res[modes[0]][0][2][0]
+    same = all(list(res[m][0][2][0][0]) == list(seq0[0]) and list(res[m][0][2][0][1]) == list(seq0[1]) for m in modes)
+    print("%s: %d removals; " % (name, len(seq0[0])) + "; ".join("MD_DF=%s %s ms" % (m, ["%.3f/%.3f" % r[:2] for r in res[m]]) for m in modes) +
+          " (median / min per pass); identical rollouts: %s" % same, flush=True)

@@ -29,6 +29,61 @@ print("  median us: " + "  ".join(f"{s}={np.median(d(a, b)):.1f}" for s, a, b in
 print("  mean us:   " + "  ".join(f"{s}={np.mean(d(a, b)):.1f}" for s, a, b in segs) +
       f"  tile end->next phaseA={np.mean((nxt[ok] - full[ok, 9]) / 100.0):.1f}  step={np.mean((nxt[ok] - full[ok, 0]) / 100.0):.1f}", flush=True)
 h = lambda a, b: np.median((full[:, b] - full[:, a]) / 100.0)
+# critical path from the step record (slot 3): the latest tile at each point, phase A's side
+R = P[:-1]
+nx3 = P[1:, 3]
+m = (R[:, 3] > 0) & (R[:, 46] > 0) & (nx3 > 0) & (R[:, 11] > 0)
+rel = lambda col: np.median((R[m, col] - R[m, 3]) / 100.0)
+print("  from the record (latest tile): seen %.1f  it1 %.1f  it2 %.1f  L1 rows out %.1f  arg-max out %.1f | phase A: "
+      "partials in %.1f  spec check %.1f-%.1f  next record %.1f us (%d steps)" % (
+          rel(43), rel(44), rel(45), rel(47), rel(46), rel(11), rel(69) if np.all(R[m, 69] > 0) else float("nan"),
+          rel(71) if np.all(R[m, 71] > 0) else float("nan"), np.median((nx3[m] - R[m, 3]) / 100.0), int(m.sum())), flush=True)
+Rn = P[1:]
+print("  phase A tail (from the spec check end): apply %.1f  features %.1f  write-back %.1f  request+h0 %.1f  record %.1f us" % (
+    np.median((Rn[m, 2] - R[m, 71]) / 100.0), np.median((Rn[m, 34] - Rn[m, 2]) / 100.0), np.median((Rn[m, 14] - Rn[m, 34]) / 100.0),
+    np.median((Rn[m, 15] - Rn[m, 14]) / 100.0), np.median((Rn[m, 3] - Rn[m, 15]) / 100.0)), flush=True)
+mm = m & (Rn[:, 56] > 0)
+print("  prebuild of step t+1 (latest tile, from the record of t): early word seen %.1f  lists %.1f  iteration 1 %.1f us" % (
+    np.median((Rn[mm, 54] - R[mm, 3]) / 100.0) if mm.any() else float("nan"), np.median((Rn[mm, 55] - R[mm, 3]) / 100.0) if mm.any() else float("nan"),
+    np.median((Rn[mm, 56] - R[mm, 3]) / 100.0) if mm.any() else float("nan")), flush=True)
+print("  request -> next record: spec wg0 done %.1f features %.1f" % (
+    np.median((R[m, 68] - R[m, 64]) / 100.0), np.median((R[m, 74] - R[m, 64]) / 100.0)), flush=True)
 print("  head it3 from record: start %.1f graph_sum(S2) done %.1f vrow %.1f head %.1f published %.1f us" % (
     h(3, 49), h(3, 50), h(3, 51), h(3, 52), h(3, 53)), flush=True)
+e.close()
+# per-step table (us from the record of step t): next record, latest tile seeing the next record,
+# spec wg0 done / features (from the request), phase A's spec check end, prebuild stamps of t+1
+print("  step: next_rec seen_next | req->done req->feat | check_end | pre: ew lists it1 | hit_slot", flush=True)
+for t in range(min(len(P) - 2, 40)):
+    a, b, c = P[t], P[t + 1], P[t + 2] if t + 2 < len(P) else P[t + 1]
+    if a[3] == 0 or b[3] == 0:
+        continue
+    f = lambda x: "%.1f" % ((x - a[3]) / 100.0) if x > 0 else "-"
+    print("  %3d: %s %s | %s %s | %s | %s %s %s | %d" % (t, f(b[3]), "%.1f" % ((b[43] - b[3]) / 100.0) if b[43] > 0 else "-",
+          "%.1f" % ((a[68] - a[64]) / 100.0) if a[68] > 0 else "-", "%.1f" % ((a[74] - a[64]) / 100.0) if a[74] > 0 else "-",
+          f(a[71]), f(b[54]), f(b[55]), f(b[56]), int(a[70])), flush=True)
+# per-tile distribution (rows 128 + 4 t + k): iteration-2 start and prebuild end, from the record
+# of step t (prebuild of step t+1 from the record of t)
+e = _lib.Engine(W)
+e.load_graphs([(int(z["n_nodes"]), z["edges0"], z["edges1"])])
+e.reset(); e.rollout()
+e.reset(); e.profile(512); e.rollout()
+P2 = e.profile_read().astype(np.int64); e.profile(0)
+st_rel, pb_rel = [], []
+for t in range(1, min(60, (len(P2) - 132) // 4)):
+    rec = P2[t, 3]
+    if rec == 0:
+        continue
+    s = np.concatenate([P2[128 + 4 * t, :64], P2[129 + 4 * t, :64]])
+    b = np.concatenate([P2[130 + 4 * t, :64], P2[131 + 4 * t, :64]])
+    s = s[s > 0]; b = b[b > 0]
+    if len(s):
+        st_rel.append(np.percentile((s - rec) / 100.0, [10, 50, 90, 100]))
+    if len(b):
+        pb_rel.append(np.percentile((b - rec) / 100.0, [10, 50, 90, 100]))
+if st_rel:
+    print("  per tile, iteration-2 start after the record (median over steps of the p10/p50/p90/max over tiles):",
+          np.round(np.median(np.array(st_rel), axis=0), 1).tolist(), flush=True)
+if pb_rel:
+    print("  per tile, prebuild end after the record:", np.round(np.median(np.array(pb_rel), axis=0), 1).tolist(), flush=True)
 e.close()

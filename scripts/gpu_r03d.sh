@@ -10,6 +10,6 @@ step() {  # name seconds cmd...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
   return 0
 }
-step df_ab 300 python -u scripts/df_ab.py gmm1000_s0,gmm1000_s1,er1000,gmm200_s7 15
+DF_MODES=0,2,1 step df_ab 400 python -u scripts/df_ab.py gmm1000_s0,gmm1000_s1,er1000,gmm200_s7 15
 step df_prof 240 python -u scripts/df_prof.py gmm1000_s0
 step pytest_parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_degree.py -q --timeout 120 --timeout-method thread -p no:cacheprovider

@@ -445,3 +445,41 @@ def test_paired_tiles_match_single_tiles(monkeypatch, cost):
     assert len(out["1"]) == len(batch)
     for i, (a, b) in enumerate(zip(out["0"], out["1"])):
         assert a == b, i
+
+
+@pytest.mark.parametrize("cost", ["unit", "degree"])
+def test_dataflow_mode_same_rollouts(monkeypatch, cost):
+    """The barrier-free dataflow mode of single-graph rollouts (MD_DF=1: tagged granules for the
+    step record, rows and partials; MD_DF=2: plus the iteration-1 prebuild from speculative
+    workgroup 0's result before phase A picks) gives the removal sequences and LMCC traces of
+    the grid-barrier protocol (MD_DF=0), over repeated rollouts (timing-dependent paths), for
+    graphs of 100 to 1000 nodes, with and without the K2 end-game shortcut."""
+    if cost == "unit":
+        names, w = ["gmm200_s7", "er100", "gmm1000_s0", "er300_dense", "gmm1000_s1"], engine.load_weights(engine.DEFAULT_UNIT)
+    else:
+        names, w = ["deg_gmm200_s7", "deg_er100"], engine.load_weights(engine.DEFAULT_DEGREE)
+    for name in names:
+        z = load_golden(name)
+        n = int(z["n_nodes"])
+        out = {}
+        for df in ("0", "2", "1"):
+            for variant in (("0", "2048") if cost == "unit" else ("0",)):
+                monkeypatch.setenv("MD_DF", df)
+                monkeypatch.setenv("MD_VARIANT", variant)
+                if cost == "unit":
+                    e = _lib.Engine(w)
+                    e.load_graphs([(n, z["edges0"], z["edges1"])])
+                else:
+                    from mdcommunity_amd import graph as mgraph
+                    g = mgraph.Graph_test.from_edges(n, z["edges0"], z["edges1"])
+                    mgraph.ensure_degree_weights(g)
+                    e = _lib.Engine(w, cost_mode=_lib.MD_COST_DEGREE)
+                    e.load_graphs([(n, z["edges0"], z["edges1"])], node_w=mgraph.node_weight_array([g]))
+                for rep in range(3):
+                    e.reset()
+                    seq, ranks = e.rollout()[0]
+                    out.setdefault(variant, []).append((df, seq.tolist(), ranks.tolist()))
+                e.close()
+        for variant, runs in out.items():
+            for df, seq, ranks in runs:
+                assert (seq, ranks) == (runs[0][1], runs[0][2]), (name, variant, df)
