@@ -1464,8 +1464,10 @@ __device__ __noinline__ void gather_df(KParams&, const GraphInfo gi, int it, int
   float* const scr = lds_base() + L_SCR;
 
   KParams& p = kp();
-  constexpr int SROWS = 128, NLD = SROWS * 32 / NTHREADS;
-  static_assert(SROWS * 64 <= S_HID - S_M, "dataflow staging fits [S_M, S_HID)");
+  // 80 rows per batch: five 16-byte loads per thread and buffer (two buffers in flight) keep the
+  // function clear of the callee-saved registers (no spill at its entry and exit)
+  constexpr int SROWS = 80, NLD = SROWS * 32 / NTHREADS;
+  static_assert(SROWS * 64 <= S_HID - S_M && SROWS * 32 % NTHREADS == 0, "dataflow staging fits [S_M, S_HID)");
   const int w = wave_id(), lane = lane_id(), t = threadIdx.x;
   const int q = lane & 31;
   const int r = 2 * w + (lane >> 5);
