@@ -142,6 +142,9 @@ struct md_ctx {
   // dataflow mode (single-graph rollouts without grid barriers, md_kernels.hip df_*): tagged
   // granule buffer sized for the largest graph that qualifies (df_graph); MD_DF=0 turns it off
   bool df_on = true;
+  // speculative workgroups build the next step's state from the result phase A takes, before
+  // its write-back (spec_loop early requests); MD_EARLY=0 turns it off
+  bool early_on = true;
   bool df_r0 = false;  // measured: no gain over the early-word prebuild alone
   DevBuf<unsigned long long> dfbuf;
   int df_mt = 0, df_n = 0;
@@ -524,6 +527,7 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
     if (!(c->variant & 1)) {  // MD_VARIANT bit 1: no iteration-1 prebuild
       p.pre_ew = (unsigned long long*)(c->ctl.p + CTL_PRE);
       p.pre_cw = (unsigned long long*)(c->ctl.p + CTL_PRE + 2);
+      p.spec_early = c->early_on ? 1 : 0;
     }
   }
   if (df) {
@@ -722,6 +726,7 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_HOST_HANDSHAKE")) c->host_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_POLL_US")) c->poll_us = std::atoi(v);
   if (const char* v = std::getenv("MD_H0G")) c->h0g_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MD_EARLY")) c->early_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_DF")) {
     c->df_on = std::atoi(v) != 0;
     c->df_r0 = std::atoi(v) == 2;  // MD_DF=2: with the prebuild from speculative workgroup 0's result

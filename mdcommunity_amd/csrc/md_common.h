@@ -172,6 +172,7 @@ struct Params {
   // the result while phase A runs and keep them when the confirmation matches
   unsigned long long* pre_ew;
   unsigned long long* pre_cw;
+  int spec_early;                  // 1: speculative workgroups serve the next request from pre_ew (spec_loop)
   int qspec_n;                     // total nodes of the loaded batch
   // dataflow mode (single-graph rollouts in dedicated mode with the layer split, md_kernels.hip
   // df_*): no grid barrier; the step record, the H rows, the virtual-node and arg-max partials

@@ -984,18 +984,24 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
               break;
             __builtin_amdgcn_s_sleep(1);
           }
+          if (sts != nullptr) {  // diagnostics: longest poll (slot 58), polling lanes (slot 57)
+            atomicMax(sts + 58, wall_clock64() - t0);
+            atomicAdd(sts + 57, 1ull);
+          }
         }
         if (done) {
           E.tmp[A_TMP_WORDS - 1] = spec_slot_index(threadIdx.x, ps);  // the slot, parity included
           E.tmp[A_TMP_WORDS - 2] = (int)(v >> 48);  // killed edges
-          if (sts != nullptr) {
-            sts[70] = threadIdx.x + 1;
-            sts[72] = __hip_atomic_load(tp + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
+          if (sts != nullptr) sts[70] = threadIdx.x + 1;
         }
       }
       __syncthreads();
-      if (sts != nullptr && threadIdx.x == 0) sts[71] = wall_clock64();
+      if (sts != nullptr && threadIdx.x == 0) {
+        sts[71] = wall_clock64();
+        if (E.tmp[A_TMP_WORDS - 1] >= 0)
+          sts[72] = __hip_atomic_load((const g_u64*)(p.sres + (size_t)E.tmp[A_TMP_WORDS - 1] * p.sres_stride) + 5,
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       spec_slot = E.tmp[A_TMP_WORDS - 1];
       spec_nd = E.tmp[A_TMP_WORDS - 2];
       if (p.pre_ew != nullptr && threadIdx.x == 0) {

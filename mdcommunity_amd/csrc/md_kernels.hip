@@ -3823,15 +3823,32 @@ __device__ __noinline__ void spec_loop(KParams&) {
   float* gmx = qv + ((n + 15) & ~15);
   int* cl = (int*)(gmx + G);
   env_stage_static(E, n);  // endpoints and row pointers: once per launch
-  unsigned long long last = 0ull;
+  unsigned long long last = 0ull, last_ew = 0ull;
+  // Early requests: phase A publishes the result it takes (pre_ew: {request tag << 32 | node <<
+  // 16 | slot}) right after its slot check, about 12 us before its write-back and its request.
+  // A workgroup whose LDS still holds the state of that request (own candidate's kills undoable:
+  // `mine` >= -1) builds the next state itself -- undo its own kills, apply the taken result's
+  // kill list -- and serves the next request (same step and tag as phase A's, which it then
+  // ignores) without waiting for the write-back or restaging.  The state is the same bytes
+  // phase A reaches: its step applies exactly that result's kill list (env_apply_spec).
+  int mine = -2;  // -2: no state to build on; -1: state of request `last`, unmodified; else own candidate
   while (true) {
     if (threadIdx.x == 0) {
       const unsigned long long t0 = wall_clock64();
-      unsigned long long v;
-      int stop = 0;
+      unsigned long long v, ew = 0ull;
+      int stop = 0, early = 0;
       while (true) {
         v = __hip_atomic_load((const g_u64*)p.spec_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (v == SPEC_EXIT) { stop = 1; break; }
+        if (p.pre_ew != nullptr && mine >= -1 && p.spec_early) {
+          ew = __hip_atomic_load((const g_u64*)p.pre_ew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (ew != last_ew && (unsigned)(ew >> 32) == (unsigned)last) {
+            v = ((unsigned long long)((unsigned)(last >> 32) + 1u) << 32) |
+                spec_tag(p.launch_seq, (int)((unsigned)last & 0xffffu) + 1);
+            early = 1;
+            break;
+          }
+        }
         if (v != 0ull && v != last && ((unsigned)v >> 16) == (p.launch_seq & 0xffffu)) break;
         if (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR) { stop = 1; break; }
         if (wall_clock64() - t0 > HOST_TIMEOUT_TICKS) { stop = 1; break; }
@@ -3843,6 +3860,11 @@ __device__ __noinline__ void spec_loop(KParams&) {
       misc[3] = -1;
       misc[4] = __float_as_int(NEG_INF);
       misc[5] = 0;
+      misc[6] = early;
+      misc[7] = (int)(ew & 0xffffu);          // the taken result's slot (parity included)
+      misc[8] = (int)((ew >> 16) & 0xffffu);  // and node
+      misc[9] = (int)(unsigned)ew;
+      misc[10] = (int)(unsigned)(ew >> 32);
     }
     __syncthreads();
     if (misc[0]) return;
@@ -3850,9 +3872,58 @@ __device__ __noinline__ void spec_loop(KParams&) {
     const int qb = (misc[2] - 1) & 1;  // buffer of the previous prediction
     int* const slot = p.sres + (size_t)spec_slot_index(k, misc[2]) * p.sres_stride;  // this request's parity
     last = ((unsigned long long)(unsigned)misc[2] << 32) | tag;
+    const bool early = misc[6] != 0;
+    if (early) last_ew = ((unsigned long long)(unsigned)misc[10] << 32) | (unsigned)misc[9];
     // diagnostics (md_profile): workgroup 0's timeline in the request step's slots 65-68
     unsigned long long* ts = p.prof != nullptr && k == 0 && misc[2] < p.prof_cap ? p.prof + (size_t)misc[2] * PROF_SLOTS : nullptr;
     TSTAMP(65);
+    if (ts != nullptr && threadIdx.x == 0) ts[59] = early ? 1 : 0;  // diagnostics: early request
+    if (early) {
+      // the next state from this LDS state: undo the own candidate's kills (its fixed point
+      // killed only alive edges, listed in the dead list), apply the taken result's kill list
+      const int a = misc[8];
+      const int* const ts_ = p.sres + (size_t)misc[7] * p.sres_stride;
+      if (mine != a) {
+        const int nd_s = ldc(ts_ + 7);
+        if (mine >= 0) {
+          const int nd = E.hdr[1];
+          for (int i = threadIdx.x; i < nd; i += NTHREADS) E.st[E.dl[i]] = E_ALIVE;
+          if (threadIdx.x == 0) E.cov8[mine] = 0;
+          __syncthreads();
+        }
+        for (int i = threadIdx.x; i < nd_s; i += NTHREADS) {
+          const int w = ldc(ts_ + SRES_HDR + 3 * i);
+          const int e = w & 0xffff;
+          if (MD_BOK(e < et, 11)) E.st[e] = (uint8_t)(w >> 16);
+        }
+        if (threadIdx.x == 0) E.cov8[a] = 1;
+      }
+      __syncthreads();
+      build_alive<false>(E);
+      // live nodes (residual layer-0 degree > 0, as phase A's degrees say) and Q(t-1)
+      for (int x = threadIdx.x; x < n; x += NTHREADS) uf_store(E.deg0, x, 0);
+      __syncthreads();
+      for_each_alive<false>(E, [&](int e, int u, int v) {
+        if (e < E.e0) {
+          uf_store(E.deg0, u, 1);
+          uf_store(E.deg0, v, 1);
+        }
+      });
+      __syncthreads();
+      for (int b = 0; b < n; b += 4 * NTHREADS) {
+        float qq[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = b + u * NTHREADS + threadIdx.x;
+          if (i < n) qq[u] = ldc(p.qspec + (size_t)qb * p.qspec_n + gi.node_off + i);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = b + u * NTHREADS + threadIdx.x;
+          if (i < n) qv[i] = uf_load(E.deg0, i) > 0 ? qq[u] : NEG_INF;
+        }
+      }
+    } else {
     // step t's state and the previous prediction Q(t-1), loads batched; nodes live now were
     // live then, so their entries are that prediction's
     {
@@ -3894,6 +3965,9 @@ __device__ __noinline__ void spec_loop(KParams&) {
     }
     __syncthreads();
     build_alive<false>(E);
+    }
+    mine = -1;
+    __syncthreads();
     TSTAMP(73);
     // candidate: the live node of rank k (descending Q, ties by ascending id).  Rank 0 (the
     // workgroup whose result phase A takes most often) is the arg-max, one block reduction;
@@ -3982,6 +4056,7 @@ __device__ __noinline__ void spec_loop(KParams&) {
     const int c = misc[3];
     __syncthreads();
     if (c < 0) continue;
+    mine = c;
     TSTAMP(66);
     // taken: phase A of the next step waits for this result instead of recomputing it
     if (threadIdx.x == 0) {
@@ -4273,6 +4348,11 @@ __device__ __noinline__ void df_tiles(KParams&) {
     if (threadIdx.x == 0) *seen = ((unsigned long long)(unsigned)misc[55] << 32) | (unsigned)misc[54];
     if (j >= (nl + TILE - 1) / TILE) continue;
     const int pre_ok = pre_state != 0 && cw == pre_used ? pre_state : 0;
+    if (p.prof != nullptr && threadIdx.x == 0 && pstep < p.prof_cap) {  // diagnostics
+      unsigned long long* const ps = p.prof + (size_t)pstep * PROF_SLOTS;
+      atomicMax(ps + (pre_ok == 3 ? 77 : 76), wall_clock64());  // latest record seen, with / without prebuild
+      if (pre_ok != 3) atomicAdd(ps + 79, 1ull);                 // tiles without the confirmed prebuild
+    }
     if (pre_ok == 3 && deferred) {  // (the early word was not seen before the record)
       df_store_tile(p, j, L, 1, df_ptag(df_tag(pstep), cw));
       __syncthreads();

@@ -46,22 +46,34 @@ mm = m & (Rn[:, 56] > 0)
 print("  prebuild of step t+1 (latest tile, from the record of t): early word seen %.1f  lists %.1f  iteration 1 %.1f us" % (
     np.median((Rn[mm, 54] - R[mm, 3]) / 100.0) if mm.any() else float("nan"), np.median((Rn[mm, 55] - R[mm, 3]) / 100.0) if mm.any() else float("nan"),
     np.median((Rn[mm, 56] - R[mm, 3]) / 100.0) if mm.any() else float("nan")), flush=True)
+print("  tiles seeing the record, latest (from the record): with prebuild %.1f  without %.1f us; tiles without the confirmed prebuild per step: median %.0f mean %.1f max %d" % (
+    np.median((R[m & (R[:, 77] > 0), 77] - R[m & (R[:, 77] > 0), 3]) / 100.0) if (m & (R[:, 77] > 0)).any() else float("nan"),
+    np.median((R[m & (R[:, 76] > 0), 76] - R[m & (R[:, 76] > 0), 3]) / 100.0) if (m & (R[:, 76] > 0)).any() else float("nan"),
+    np.median(R[m, 79]), np.mean(R[m, 79]), int(R[m, 79].max())), flush=True)
+print("  phase A check (from the record): start %.1f end %.1f; steps whose check polled a running slot: %d of %d, longest poll median %.1f us" % (
+    np.median((R[m, 69] - R[m, 3]) / 100.0), np.median((R[m, 71] - R[m, 3]) / 100.0), int((R[m, 57] > 0).sum()), int(m.sum()),
+    np.median(R[m & (R[:, 57] > 0), 58] / 100.0) if (m & (R[:, 57] > 0)).any() else 0.0), flush=True)
 print("  request -> next record: spec wg0 done %.1f features %.1f" % (
     np.median((R[m, 68] - R[m, 64]) / 100.0), np.median((R[m, 74] - R[m, 64]) / 100.0)), flush=True)
+mq = m & (R[:, 65] > 0) & (R[:, 73] > 0) & (R[:, 66] > 0) & (R[:, 67] > 0) & (R[:, 68] > 0) & (R[:, 74] > 0)
+if mq.any():
+    dd = lambda a, b: np.median((R[mq, b] - R[mq, a]) / 100.0)
+    print("  spec wg0 (from the request): seen %.1f  staged %.1f  ranked %.1f  taken %.1f  fixed point %.1f  features %.1f us; request at %.1f from the record" % (
+        dd(64, 65), dd(64, 73), dd(64, 66), dd(64, 67), dd(64, 68), dd(64, 74), np.median((R[mq, 64] - R[mq, 3]) / 100.0)), flush=True)
 print("  head it3 from record: start %.1f graph_sum(S2) done %.1f vrow %.1f head %.1f published %.1f us" % (
     h(3, 49), h(3, 50), h(3, 51), h(3, 52), h(3, 53)), flush=True)
 e.close()
 # per-step table (us from the record of step t): next record, latest tile seeing the next record,
 # spec wg0 done / features (from the request), phase A's spec check end, prebuild stamps of t+1
-print("  step: next_rec seen_next | req->done req->feat | check_end | pre: ew lists it1 | hit_slot", flush=True)
+print("  step: next_rec seen_next | req->done req->feat | check_end | pre: ew lists it1 | hit_slot | no-prebuild tiles", flush=True)
 for t in range(min(len(P) - 2, 40)):
     a, b, c = P[t], P[t + 1], P[t + 2] if t + 2 < len(P) else P[t + 1]
     if a[3] == 0 or b[3] == 0:
         continue
     f = lambda x: "%.1f" % ((x - a[3]) / 100.0) if x > 0 else "-"
-    print("  %3d: %s %s | %s %s | %s | %s %s %s | %d" % (t, f(b[3]), "%.1f" % ((b[43] - b[3]) / 100.0) if b[43] > 0 else "-",
+    print("  %3d: %s %s | %s %s | %s | %s %s %s | %d | %d" % (t, f(b[3]), "%.1f" % ((b[43] - b[3]) / 100.0) if b[43] > 0 else "-",
           "%.1f" % ((a[68] - a[64]) / 100.0) if a[68] > 0 else "-", "%.1f" % ((a[74] - a[64]) / 100.0) if a[74] > 0 else "-",
-          f(a[71]), f(b[54]), f(b[55]), f(b[56]), int(a[70])), flush=True)
+          f(a[71]), f(b[54]), f(b[55]), f(b[56]), int(a[70]), int(b[79])), flush=True)
 # per-tile distribution (rows 128 + 4 t + k): iteration-2 start and prebuild end, from the record
 # of step t (prebuild of step t+1 from the record of t)
 e = _lib.Engine(W)
