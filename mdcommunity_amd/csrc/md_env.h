@@ -82,6 +82,7 @@ __device__ __forceinline__ void uf_add(int* a, int i, int v) {
 __device__ __forceinline__ void uf_add(lds_i32* a, int i, int v) {
   __hip_atomic_fetch_add(a + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+
 template <class P>
 __device__ __forceinline__ int uf_find(P par, int v) {
   int cur = uf_load(par, v);
@@ -933,6 +934,28 @@ __device__ __forceinline__ void h0_update(KParams& p, const GraphInfo& gi, Graph
   }
 }
 
+// Dataflow mode, early step record (thread 0): with the taken result's features published,
+// the state after this step is known before phase A has applied it (live count, and whether it
+// stays running: alive edges in both layers, no K2 end-game, no live-set mismatch -- the
+// result's aggregates in E.tmp[A_TMP_WORDS - 16, -11)); tile workgroups whose iteration-1
+// prebuild used this result start their step on it while this phase A finishes (the others,
+// and the graph head, wait for the record's "full" granule; the tiles' Q stores come after the
+// graph head, so after phase A's reset of Q).
+template <bool GL>
+__device__ __forceinline__ void df_early_record(KParams& p, const EnvView<GL>& E, int n) {
+  const int nl = E.tmp[A_TMP_WORDS - 16], dm0 = E.tmp[A_TMP_WORDS - 15], dm1 = E.tmp[A_TMP_WORDS - 14];
+  const int sd0 = E.tmp[A_TMP_WORDS - 13], sd1 = E.tmp[A_TMP_WORDS - 12], bad = E.tmp[A_TMP_WORDS - 11];
+  const bool eg = p.endgame && p.node_w == nullptr && n < 32768 && nl > 0 && dm0 == 1 && dm1 == 1;
+  volatile int* misc = (volatile int*)(md::lds_base() + L_MISC);
+  if (!bad && sd0 > 0 && sd1 > 0 && !eg && misc[56] != 0) {
+    const unsigned tag = (unsigned)(misc[60] + 1);
+    const int v[6] = {ST_RUN, nl, misc[56], misc[57], misc[56], misc[57]};
+#pragma unroll
+    for (int i = 0; i < 6; ++i) df_st(p.df + DF_REC + i, __int_as_float(v[i]), tag);
+    misc[48] = 1;
+  }
+}
+
 template <bool GL>
 __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, float*, int pend_n,
                         int pend_first, const float*, bool staged) {
@@ -962,7 +985,10 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
       const int ps = ((volatile int*)(lds_base + L_MISC))[60] - 1;  // the request's step
       unsigned long long* sts = p.prof != nullptr && ps >= 0 && ps < p.prof_cap ? p.prof + (size_t)ps * PROF_SLOTS : nullptr;
       if (sts != nullptr && threadIdx.x == 0) sts[69] = wall_clock64();
-      if (threadIdx.x == 0) E.tmp[A_TMP_WORDS - 1] = -1;
+      if (threadIdx.x == 0) {
+        E.tmp[A_TMP_WORDS - 1] = -1;
+        E.tmp[A_TMP_WORDS - 10] = 0;  // the taken result's features were published at the pre-read
+      }
       __syncthreads();
       if ((int)threadIdx.x < p.n_spec) {
         // done, or taken and still running: a taken fixed point started earlier than this one
@@ -984,33 +1010,45 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
               break;
             __builtin_amdgcn_s_sleep(1);
           }
-          if (sts != nullptr) {  // diagnostics: longest poll (slot 58), polling lanes (slot 57)
-            atomicMax(sts + 58, wall_clock64() - t0);
-            atomicAdd(sts + 57, 1ull);
+          if (sts != nullptr) {  // diagnostics: longest poll (slot 32), polling lanes (slot 31)
+            atomicMax(sts + 32, wall_clock64() - t0);
+            atomicAdd(sts + 31, 1ull);
           }
         }
         if (done) {
           E.tmp[A_TMP_WORDS - 1] = spec_slot_index(threadIdx.x, ps);  // the slot, parity included
           E.tmp[A_TMP_WORDS - 2] = (int)(v >> 48);  // killed edges
           if (sts != nullptr) sts[70] = threadIdx.x + 1;
+          if (p.df != nullptr) {
+            const int* pf = (const int*)(lds_base + L_PREF) + PREF_FEAT + 8 * threadIdx.x;
+            if ((unsigned)pf[0] == want && pf[1] == a) {
+#pragma unroll
+              for (int i = 0; i < 6; ++i) E.tmp[A_TMP_WORDS - 16 + i] = pf[2 + i];
+              E.tmp[A_TMP_WORDS - 10] = 1;
+            }
+          }
         }
       }
       __syncthreads();
-      if (sts != nullptr && threadIdx.x == 0) {
-        sts[71] = wall_clock64();
-        if (E.tmp[A_TMP_WORDS - 1] >= 0)
-          sts[72] = __hip_atomic_load((const g_u64*)(p.sres + (size_t)E.tmp[A_TMP_WORDS - 1] * p.sres_stride) + 5,
-                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      if (sts != nullptr && threadIdx.x == 0) sts[71] = wall_clock64();
       spec_slot = E.tmp[A_TMP_WORDS - 1];
       spec_nd = E.tmp[A_TMP_WORDS - 2];
       if (p.pre_ew != nullptr && threadIdx.x == 0) {
-        // the tile workgroups may build their iteration-1 lists from this result meanwhile
+        // the tile workgroups may build their iteration-1 lists from this result meanwhile (and
+        // the speculative workgroups the next state: spec_loop's early requests)
         const unsigned long long ew = spec_slot >= 0 ? ((unsigned long long)want << 32) | ((unsigned)a << 16) | (unsigned)spec_slot : 0ull;
         ((volatile unsigned*)(lds_base + L_MISC))[56] = (unsigned)ew;
         ((volatile unsigned*)(lds_base + L_MISC))[57] = (unsigned)(ew >> 32);
         if (ew != 0ull) __hip_atomic_store((g_u64*)p.pre_ew, ew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // dataflow mode: with the taken result's features already published, the state after
+        // this step is known now; the step record goes out before the result is applied (see
+        // the early record below; the same conditions, from the pre-read aggregates)
+        if (ew != 0ull && p.df != nullptr && pend_n == 1 && p.run_mode == RUN_ROLLOUT && E.tmp[A_TMP_WORDS - 10])
+          df_early_record(p, E, n);
       }
+      if (sts != nullptr && threadIdx.x == 0 && spec_slot >= 0)
+        sts[72] = __hip_atomic_load((const g_u64*)(p.sres + (size_t)spec_slot * p.sres_stride) + 5, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
     }
   }
@@ -1044,24 +1082,9 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
       if (k == 0 && spec_slot >= 0) {
         lm = env_apply_spec(E, p.sres + (size_t)spec_slot * p.sres_stride, spec_nd, pr, c);
         if (threadIdx.x == 0) gv.spec_hits += 1;
-        if (p.df != nullptr && pend_n == 1 && p.run_mode == RUN_ROLLOUT && E.tmp[A_TMP_WORDS - 3] && threadIdx.x == 0) {
-          // dataflow mode, early step record: with the result's features published, the state
-          // after this step is known now (live count, and whether it stays running: alive edges
-          // in both layers, no K2 end-game, no live-set mismatch); tile workgroups whose
-          // iteration-1 prebuild used this result start their step on it while this phase A
-          // finishes (the others, and the graph head, wait for the record's "full" granule)
-          const int nl = E.tmp[A_TMP_WORDS - 16], dm0 = E.tmp[A_TMP_WORDS - 15], dm1 = E.tmp[A_TMP_WORDS - 14];
-          const int sd0 = E.tmp[A_TMP_WORDS - 13], sd1 = E.tmp[A_TMP_WORDS - 12], bad = E.tmp[A_TMP_WORDS - 11];
-          const bool eg = p.endgame && p.node_w == nullptr && n < 32768 && nl > 0 && dm0 == 1 && dm1 == 1;
-          volatile int* misc = (volatile int*)(lds_base + L_MISC);
-          if (!bad && sd0 > 0 && sd1 > 0 && !eg && misc[56] != 0) {
-            const unsigned tag = (unsigned)(misc[60] + 1);
-            const int v[6] = {ST_RUN, nl, misc[56], misc[57], misc[56], misc[57]};
-#pragma unroll
-            for (int i = 0; i < 6; ++i) df_st(p.df + DF_REC + i, __int_as_float(v[i]), tag);
-            misc[48] = 1;
-          }
-        }
+        if (p.df != nullptr && pend_n == 1 && p.run_mode == RUN_ROLLOUT && E.tmp[A_TMP_WORDS - 3] && threadIdx.x == 0 &&
+            ((volatile int*)(lds_base + L_MISC))[48] == 0)
+          df_early_record(p, E, n);
       } else {
         lm = mcc_fixed_point<GL>(E, pr, acc, a, c);
       }

@@ -55,6 +55,10 @@ constexpr int W_IEND = W_IWL2 + 128;
 // ------------------------------------------------------------------ LDS layout (floats)
 constexpr int L_PREF = 0;                        // int [G_CAP + 4] tile prefix of this step
 constexpr int L_MISC = L_PREF + G_CAP + 4;       // 64 words of broadcast scalars
+// dataflow mode, phase A: per speculative slot {features tag (2 words), aggregates (6)} read
+// beside the slot tags (L_PREF words [0, 4 SPEC_MAX) hold the tags)
+constexpr int PREF_FEAT = 4 * 32;
+static_assert(PREF_FEAT + 8 * 32 <= G_CAP + 4, "speculative slot words must fit L_PREF");
 constexpr int L_GV = L_MISC + 64;                // 32 words: phase-A copy of a GraphVar
 constexpr int L_Y0 = L_GV + 32;                  // [64] virtual-node input embedding (constant)
 constexpr int L_YW = L_Y0 + 64;                  // [2][64] virtual-node embedding being iterated
@@ -721,8 +725,19 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
       if (threadIdx.x >= 64 && (int)threadIdx.x < 64 + p.n_spec) {
         const g_u64* tp = (const g_u64*)(p.sres + (size_t)spec_slot_index(threadIdx.x - 64, misc[60] - 1) * p.sres_stride);
         unsigned long long* pre = (unsigned long long*)(lds + L_PREF) + 2 * (threadIdx.x - 64);
+        // (and the features tag and aggregates: a result taken with its features published
+        // lets env_step publish the step record at its slot check)
+        int* pf = (int*)(lds + L_PREF) + PREF_FEAT + 8 * (threadIdx.x - 64);
+        const unsigned long long ft = __hip_atomic_load(tp + SRES_FEAT / 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int fa[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) fa[i] = ldc((const int*)tp + 12 + i);
         pre[0] = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         pre[1] = __hip_atomic_load(tp + SRES_STARTED / 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pf[0] = (int)(unsigned)ft;
+        pf[1] = (int)(unsigned)(ft >> 32);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) pf[2 + i] = fa[i];
       }
     }
     if (threadIdx.x == 0) {
@@ -1187,6 +1202,14 @@ __device__ __noinline__ int prebuild_lists(KParams&, const GraphInfo gi, int j, 
   if (threadIdx.x == 0) {
     const unsigned long long dt2 = __hip_atomic_load((const g_u64*)sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     misc[47] = ((int)(dt2 >> 48) == nd && (unsigned)dt2 == want && ldc(sl + 12) == nl && nl <= n);
+    // in the same round trip: layer L's dmax of the result (spec_iteration1's first-layer
+    // table) and the early word as it stands now (a prebuild phase A has already overtaken
+    // stops after its lists)
+    misc[40] = ldc(sl + 13 + L);
+    const unsigned long long now = p.pre_ew != nullptr ? __hip_atomic_load((const g_u64*)p.pre_ew, __ATOMIC_RELAXED,
+                                                                            __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    misc[36] = (int)(unsigned)now;
+    misc[37] = (int)(unsigned)(now >> 32);
   }
   __syncthreads();
   if (!misc[47]) return 0;  // (else not built: the tile builds after the record)
@@ -1689,7 +1712,7 @@ __device__ __noinline__ bool spec_iteration1(KParams&, const GraphInfo gi, int j
   const float* hp = nullptr;
   int dm = 0x7fffffff;
   if (p.node_w == nullptr) {  // unit cost: rows by degree, from the precomputed table of the result's dmax
-    dm = ldc(sl + 13 + L);
+    dm = ((const int*)(lds + L_MISC))[40];  // (read by prebuild_lists, which runs just before)
     if (p.h0g == nullptr || (p.variant & 4) || dm < 1 || dm > p.h0g_dm) return false;
     hp = p.h0g + (h0g_row(dm, 1) - 1) * EMB;
   }
@@ -3833,27 +3856,36 @@ __device__ __noinline__ void spec_loop(KParams&) {
   // phase A reaches: its step applies exactly that result's kill list (env_apply_spec).
   int mine = -2;  // -2: no state to build on; -1: state of request `last`, unmodified; else own candidate
   while (true) {
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 64) {
+      // one round trip per poll: lane 0 the request word, lane 1 the early word, lane 2 the
+      // error word
+      const int lane = threadIdx.x;
+      const bool we = p.pre_ew != nullptr && mine >= -1 && p.spec_early;
       const unsigned long long t0 = wall_clock64();
       unsigned long long v, ew = 0ull;
       int stop = 0, early = 0;
       while (true) {
-        v = __hip_atomic_load((const g_u64*)p.spec_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long g = 0ull;
+        if (lane == 0) g = __hip_atomic_load((const g_u64*)p.spec_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else if (lane == 1 && we) g = __hip_atomic_load((const g_u64*)p.pre_ew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else if (lane == 2) g = __hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned lo = (unsigned)g, hi = (unsigned)(g >> 32);
+        v = ((unsigned long long)(unsigned)__shfl((int)hi, 0, 64) << 32) | (unsigned)__shfl((int)lo, 0, 64);
+        ew = ((unsigned long long)(unsigned)__shfl((int)hi, 1, 64) << 32) | (unsigned)__shfl((int)lo, 1, 64);
+        const unsigned bw = (unsigned)__shfl((int)lo, 2, 64);
         if (v == SPEC_EXIT) { stop = 1; break; }
-        if (p.pre_ew != nullptr && mine >= -1 && p.spec_early) {
-          ew = __hip_atomic_load((const g_u64*)p.pre_ew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (ew != last_ew && (unsigned)(ew >> 32) == (unsigned)last) {
-            v = ((unsigned long long)((unsigned)(last >> 32) + 1u) << 32) |
-                spec_tag(p.launch_seq, (int)((unsigned)last & 0xffffu) + 1);
-            early = 1;
-            break;
-          }
+        if (we && ew != last_ew && (unsigned)(ew >> 32) == (unsigned)last) {
+          v = ((unsigned long long)((unsigned)(last >> 32) + 1u) << 32) |
+              spec_tag(p.launch_seq, (int)((unsigned)last & 0xffffu) + 1);
+          early = 1;
+          break;
         }
         if (v != 0ull && v != last && ((unsigned)v >> 16) == (p.launch_seq & 0xffffu)) break;
-        if (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR) { stop = 1; break; }
+        if (bw & BAR_ERR) { stop = 1; break; }
         if (wall_clock64() - t0 > HOST_TIMEOUT_TICKS) { stop = 1; break; }
         __builtin_amdgcn_s_sleep(2);
       }
+      if (lane == 0) {
       misc[0] = stop;
       misc[1] = (int)(unsigned)v;
       misc[2] = (int)(unsigned)(v >> 32);
@@ -3865,6 +3897,7 @@ __device__ __noinline__ void spec_loop(KParams&) {
       misc[8] = (int)((ew >> 16) & 0xffffu);  // and node
       misc[9] = (int)(unsigned)ew;
       misc[10] = (int)(unsigned)(ew >> 32);
+      }
     }
     __syncthreads();
     if (misc[0]) return;
@@ -3877,14 +3910,24 @@ __device__ __noinline__ void spec_loop(KParams&) {
     // diagnostics (md_profile): workgroup 0's timeline in the request step's slots 65-68
     unsigned long long* ts = p.prof != nullptr && k == 0 && misc[2] < p.prof_cap ? p.prof + (size_t)misc[2] * PROF_SLOTS : nullptr;
     TSTAMP(65);
-    if (ts != nullptr && threadIdx.x == 0) ts[59] = early ? 1 : 0;  // diagnostics: early request
+    if (ts != nullptr && threadIdx.x == 0) ts[33] = early ? 1 : 0;  // diagnostics: early request
     if (early) {
       // the next state from this LDS state: undo the own candidate's kills (its fixed point
       // killed only alive edges, listed in the dead list), apply the taken result's kill list
       const int a = misc[8];
       const int* const ts_ = p.sres + (size_t)misc[7] * p.sres_stride;
+      // one round trip for Q(t-1) (first 4 x 512 nodes), the kill count and the first 512
+      // kill entries (read before the count is known: entries past it are ignored)
+      constexpr int QU = 4;
+      float qq[QU];
+#pragma unroll
+      for (int u = 0; u < QU; ++u) {
+        const int i = u * NTHREADS + threadIdx.x;
+        if (i < n) qq[u] = ldc(p.qspec + (size_t)qb * p.qspec_n + gi.node_off + i);
+      }
       if (mine != a) {
         const int nd_s = ldc(ts_ + 7);
+        const int w0 = (int)threadIdx.x < et ? ldc(ts_ + SRES_HDR + 3 * threadIdx.x) : 0;
         if (mine >= 0) {
           const int nd = E.hdr[1];
           for (int i = threadIdx.x; i < nd; i += NTHREADS) E.st[E.dl[i]] = E_ALIVE;
@@ -3892,7 +3935,7 @@ __device__ __noinline__ void spec_loop(KParams&) {
           __syncthreads();
         }
         for (int i = threadIdx.x; i < nd_s; i += NTHREADS) {
-          const int w = ldc(ts_ + SRES_HDR + 3 * i);
+          const int w = i < NTHREADS ? w0 : ldc(ts_ + SRES_HDR + 3 * i);
           const int e = w & 0xffff;
           if (MD_BOK(e < et, 11)) E.st[e] = (uint8_t)(w >> 16);
         }
@@ -3910,19 +3953,13 @@ __device__ __noinline__ void spec_loop(KParams&) {
         }
       });
       __syncthreads();
-      for (int b = 0; b < n; b += 4 * NTHREADS) {
-        float qq[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int i = b + u * NTHREADS + threadIdx.x;
-          if (i < n) qq[u] = ldc(p.qspec + (size_t)qb * p.qspec_n + gi.node_off + i);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int i = b + u * NTHREADS + threadIdx.x;
-          if (i < n) qv[i] = uf_load(E.deg0, i) > 0 ? qq[u] : NEG_INF;
-        }
+      for (int u = 0; u < QU; ++u) {
+        const int i = u * NTHREADS + threadIdx.x;
+        if (i < n) qv[i] = uf_load(E.deg0, i) > 0 ? qq[u] : NEG_INF;
       }
+      for (int i = QU * NTHREADS + threadIdx.x; i < n; i += NTHREADS)
+        qv[i] = uf_load(E.deg0, i) > 0 ? ldc(p.qspec + (size_t)qb * p.qspec_n + gi.node_off + i) : NEG_INF;
     } else {
     // step t's state and the previous prediction Q(t-1), loads batched; nodes live now were
     // live then, so their entries are that prediction's
@@ -4157,11 +4194,8 @@ __device__ __noinline__ int df_wait_rec(KParams&, unsigned tag, bool watch, bool
         g = __hip_atomic_load((const g_u64*)(p.sres + (size_t)spec_slot_index(0, req_step) * p.sres_stride + SRES_FEAT),
                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (__ballot(lane == 8 && (g & BAR_ERR))) break;
-      if (!__ballot((lane < 6 || (lane == 6 && full)) && (unsigned)(g >> 32) != tag)) {
-        if (lane < 6) misc[50 + lane] = (int)(unsigned)g;
-        res = 1;
-        break;
-      }
+      // a new early word first (phase A publishes it with, or just before, an early record: the
+      // prebuild from it is the tile's fastest start)
       if (w) {
         const unsigned lo = __shfl((unsigned)g, 7, 64), hi = __shfl((unsigned)(g >> 32), 7, 64);
         const unsigned long long ew = ((unsigned long long)hi << 32) | lo;
@@ -4170,6 +4204,11 @@ __device__ __noinline__ int df_wait_rec(KParams&, unsigned tag, bool watch, bool
           res = 2;
           break;
         }
+      }
+      if (!__ballot((lane < 6 || (lane == 6 && full)) && (unsigned)(g >> 32) != tag)) {
+        if (lane < 6) misc[50 + lane] = (int)(unsigned)g;
+        res = 1;
+        break;
       }
       if (w0) {
         const unsigned rlo = __shfl((unsigned)g, 9, 64), rhi = __shfl((unsigned)(g >> 32), 9, 64);
@@ -4324,6 +4363,13 @@ __device__ __noinline__ void df_tiles(KParams&) {
         pre_state = prebuild_lists(p, gi, j, L, ew);
         DF_STAMP_MAX(55);
         if (pre_state) pre_used = ew;
+        // a prebuild from workgroup 0's result that phase A's early word has already overtaken
+        // (it names another result) stops after its lists
+        const unsigned long long now = ((unsigned long long)(unsigned)misc[37] << 32) | (unsigned)misc[36];
+        if (r == 3 && pre_state == 1 && now != 0ull && now != *seen && now != ew) {
+          pre_state = 0;
+          pre_used = 0ull;
+        }
         // the whole of iteration 1 too (MD_VARIANT bit 128: lists only)
         if (pre_state == 1 && !(p.variant & 128) &&
             spec_iteration1(p, gi, j, L, ew, df_ptag(df_tag(pstep), ew), r == 3)) {

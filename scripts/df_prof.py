@@ -51,8 +51,8 @@ print("  tiles seeing the record, latest (from the record): with prebuild %.1f  
     np.median((R[m & (R[:, 76] > 0), 76] - R[m & (R[:, 76] > 0), 3]) / 100.0) if (m & (R[:, 76] > 0)).any() else float("nan"),
     np.median(R[m, 79]), np.mean(R[m, 79]), int(R[m, 79].max())), flush=True)
 print("  phase A check (from the record): start %.1f end %.1f; steps whose check polled a running slot: %d of %d, longest poll median %.1f us" % (
-    np.median((R[m, 69] - R[m, 3]) / 100.0), np.median((R[m, 71] - R[m, 3]) / 100.0), int((R[m, 57] > 0).sum()), int(m.sum()),
-    np.median(R[m & (R[:, 57] > 0), 58] / 100.0) if (m & (R[:, 57] > 0)).any() else 0.0), flush=True)
+    np.median((R[m, 69] - R[m, 3]) / 100.0), np.median((R[m, 71] - R[m, 3]) / 100.0), int((R[m, 31] > 0).sum()), int(m.sum()),
+    np.median(R[m & (R[:, 31] > 0), 32] / 100.0) if (m & (R[:, 31] > 0)).any() else 0.0), flush=True)
 print("  request -> next record: spec wg0 done %.1f features %.1f" % (
     np.median((R[m, 68] - R[m, 64]) / 100.0), np.median((R[m, 74] - R[m, 64]) / 100.0)), flush=True)
 mq = m & (R[:, 65] > 0) & (R[:, 73] > 0) & (R[:, 66] > 0) & (R[:, 67] > 0) & (R[:, 68] > 0) & (R[:, 74] > 0)
@@ -60,6 +60,11 @@ if mq.any():
     dd = lambda a, b: np.median((R[mq, b] - R[mq, a]) / 100.0)
     print("  spec wg0 (from the request): seen %.1f  staged %.1f  ranked %.1f  taken %.1f  fixed point %.1f  features %.1f us; request at %.1f from the record" % (
         dd(64, 65), dd(64, 73), dd(64, 66), dd(64, 67), dd(64, 68), dd(64, 74), np.median((R[mq, 64] - R[mq, 3]) / 100.0)), flush=True)
+me = (P[1:, 33] == 1) & (P[:-1, 71] > 0) & (P[1:, 65] > 0)
+if me.any():
+    print("  early requests (wg0): %d of %d; phase A's early word -> wg0 sees it %.1f  staged %.1f  fixed point done %.1f  features %.1f us" % (
+        int(me.sum()), len(me), np.median((P[1:, 65][me] - P[:-1, 71][me]) / 100.0), np.median((P[1:, 73][me] - P[:-1, 71][me]) / 100.0),
+        np.median((P[1:, 68][me] - P[:-1, 71][me]) / 100.0), np.median((P[1:, 74][me] - P[:-1, 71][me]) / 100.0)), flush=True)
 print("  head it3 from record: start %.1f graph_sum(S2) done %.1f vrow %.1f head %.1f published %.1f us" % (
     h(3, 49), h(3, 50), h(3, 51), h(3, 52), h(3, 53)), flush=True)
 e.close()
