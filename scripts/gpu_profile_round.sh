@@ -8,7 +8,8 @@
 #  3. scripts/rocprof_summary.py -> summary.txt + traffic.json (tagged with the kernel source
 #     hash), copied to profiles/traffic.json where bench.py reads it;
 #  4. the default bench line.
-# Usage: bash scripts/gpu_profile_round.sh r03
+# Usage: bash scripts/gpu_profile_round.sh r03 [nobench]  (then bench.py on its own, reading the
+# profiles/traffic.json copied from gpurun_out/prof_<tag>/traffic.json)
 TAG=${1:-r03}
 R=$(pwd)
 OUT=$R/gpurun_out/prof_$TAG
@@ -42,5 +43,7 @@ for W in single batch; do
 done
 cd $R
 python scripts/rocprof_summary.py $OUT > /dev/null && cp $OUT/traffic.json profiles/traffic.json && echo "summary done"
-timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
-echo "bench rc=$?"
+if [ "${2:-}" != "nobench" ]; then
+  timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
+  echo "bench rc=$?"
+fi
