@@ -117,13 +117,15 @@ struct md_ctx {
   int max_tiles = 0;  // tiles of the largest loaded graph
   DevBuf<unsigned long long> qslot;  // queue-mode work items
   DevBuf<int> qg;                    // queue-mode per-graph stage counters
-  // speculative environment steps (single-graph rollouts): result slots, Q of the last two
-  // predictions; spec_n workgroups per launch when the CUs are free (MD_SPEC, default 16, 0 = off)
   DevBuf<unsigned> bars;  // grid-barrier counter shards
+  // speculative environment steps (single-graph rollouts): result slots, Q of the last two
+  // predictions; spec_n workgroups per launch when the CUs are free (MD_SPEC, 0 = off).
+  // Default 32 (= SPEC_MAX): on gmm1000_s0 the pick is the previous prediction's rank 16-31 in
+  // 2 of 65 steps (a miss costs ~45 us): 16 -> 32 gave 4.19 -> 4.11 ms, er1000 8.10 -> 7.73 ms
   DevBuf<int> sres;
   DevBuf<float> qspec;
   int sres_stride = 0;
-  int spec_n = 16;  // layer-split hand-off of iteration-3 embeddings
+  int spec_n = 32;
   unsigned launch_seq = 0;
   // host selection hand-shake
   int host_mode = 1;

@@ -79,6 +79,20 @@ for t in range(min(len(P) - 2, 40)):
     print("  %3d: %s %s | %s %s | %s | %s %s %s | %d | %d" % (t, f(b[3]), "%.1f" % ((b[43] - b[3]) / 100.0) if b[43] > 0 else "-",
           "%.1f" % ((a[68] - a[64]) / 100.0) if a[68] > 0 else "-", "%.1f" % ((a[74] - a[64]) / 100.0) if a[74] > 0 else "-",
           f(a[71]), f(b[54]), f(b[55]), f(b[56]), int(a[70]), int(b[79])), flush=True)
+# where the long steps come from: misses (no speculative result taken), cascade steps (the
+# taken result's fixed point ran > 60 us), the rest
+rows = []
+for t in range(len(P) - 1):
+    a, b = P[t], P[t + 1]
+    if a[3] == 0 or b[3] == 0:
+        continue
+    rows.append(((b[3] - a[3]) / 100.0, int(a[70]), (a[68] - a[64]) / 100.0 if a[68] > 0 and a[64] > 0 else -1.0))
+if rows:
+    st = np.array([r[0] for r in rows]); hit = np.array([r[1] for r in rows]); fp = np.array([r[2] for r in rows])
+    miss = hit == 0; casc = (~miss) & (fp > 60); rest = ~miss & ~casc
+    print("  step classes: misses %d (%.0f us total, median %.1f), cascade %d (%.0f us, median %.1f), others %d (%.0f us, median %.1f); slot hits by rank: %s" % (
+        miss.sum(), st[miss].sum(), np.median(st[miss]) if miss.any() else 0, casc.sum(), st[casc].sum(), np.median(st[casc]) if casc.any() else 0,
+        rest.sum(), st[rest].sum(), np.median(st[rest]) if rest.any() else 0, np.bincount(hit).tolist()), flush=True)
 # per-tile distribution (rows 128 + 4 t + k): iteration-2 start and prebuild end, from the record
 # of step t (prebuild of step t+1 from the record of t)
 e = _lib.Engine(W)
