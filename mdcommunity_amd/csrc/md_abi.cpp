@@ -654,10 +654,17 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
   if (c->prof_cap > 0) {
     std::vector<unsigned long long> tmp((size_t)c->prof_cap * PROF_SLOTS);
     HIPCHK(c, hipMemcpy(tmp.data(), c->prof.p, sizeof(unsigned long long) * tmp.size(), hipMemcpyDeviceToHost));
+    // the step records up to the first empty one (MD_PROF_ALL=1: every row up to the last
+    // non-empty one -- the dataflow mode's per-tile rows 128.. follow the step records)
+    const bool all = std::getenv("MD_PROF_ALL") != nullptr && std::atoi(std::getenv("MD_PROF_ALL")) != 0;
+    int rows = 0;
     for (int s = 0; s < c->prof_cap; ++s) {
-      if (tmp[(size_t)s * PROF_SLOTS] == 0) break;
-      c->prof_host.insert(c->prof_host.end(), tmp.begin() + (size_t)s * PROF_SLOTS, tmp.begin() + (size_t)s * PROF_SLOTS + PROF_SLOTS);
+      bool any = tmp[(size_t)s * PROF_SLOTS] != 0;
+      for (int k = 1; all && !any && k < PROF_SLOTS; ++k) any = tmp[(size_t)s * PROF_SLOTS + k] != 0;
+      if (any) rows = s + 1;
+      else if (!all) break;
     }
+    c->prof_host.insert(c->prof_host.end(), tmp.begin(), tmp.begin() + (size_t)rows * PROF_SLOTS);
     HIPCHK(c, hipMemset(c->prof.p, 0, sizeof(unsigned long long) * tmp.size()));
   }
   return MD_OK;

@@ -1138,7 +1138,8 @@ __device__ __noinline__ bool build_nb_lists(KParams&, const GraphInfo gi, const 
 // result (pre_cw).  Returns 1 (rows and lists ready), 2 (rows ready, lists over NB_CAP: the
 // per-row gather), 0 (not built: the result's features not published in time, or too many
 // killed edges for the LDS set).
-__device__ __noinline__ int prebuild_lists(KParams&, const GraphInfo gi, int j, int L, unsigned long long ew) {
+__device__ __noinline__ int prebuild_lists(KParams&, const GraphInfo gi, int j, int L, unsigned long long ew,
+                                           unsigned long long* ts = nullptr, unsigned long long sv = 0ull) {
   KParams& p = kp();
   float* const lds = lds_base();
   float* const scr = lds + L_SCR;
@@ -1150,6 +1151,7 @@ __device__ __noinline__ int prebuild_lists(KParams&, const GraphInfo gi, int j, 
   const int* sl = p.sres + (size_t)slot * p.sres_stride;
   const int n = gi.n, et = gi.e[0] + gi.e[1];
   lds_i32* kh = (lds_i32*)(int*)(scr + S_M);
+  TSTAMP(28);  // diagnostics: prebuild start
   for (int i = threadIdx.x; i < KH_SIZE; i += NTHREADS) kh[i] = -1;
   if (threadIdx.x == 0) {
     // the features tag, the done tag and the live count polled together (one round trip when
@@ -1163,6 +1165,12 @@ __device__ __noinline__ int prebuild_lists(KParams&, const GraphInfo gi, int j, 
       const unsigned long long ft = __hip_atomic_load((const g_u64*)(sl + SRES_FEAT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       dt = __hip_atomic_load((const g_u64*)sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       nl = ldc(sl + 12);
+      // sv != 0 (a prebuild ahead of phase A's pick): stop once phase A's early word (same
+      // round trip) names another result
+      const unsigned long long now = sv != 0ull && p.pre_ew != nullptr
+                                         ? __hip_atomic_load((const g_u64*)p.pre_ew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                         : 0ull;
+      if (now != 0ull && now != sv && now != ew) break;
       if (ft == ft_want) {
         ok = 1;
         break;
@@ -1182,6 +1190,7 @@ __device__ __noinline__ int prebuild_lists(KParams&, const GraphInfo gi, int j, 
     misc[46] = nl;
   }
   __syncthreads();
+  TSTAMP(24);  // diagnostics (one tile's prebuild): slot polled
   if (!misc[44]) return 0;
   const int nd = misc[45], nl = misc[46];
   // the tile's rows from the result's live list (entries as in phase A's list) and every killed
@@ -1212,6 +1221,7 @@ __device__ __noinline__ int prebuild_lists(KParams&, const GraphInfo gi, int j, 
     misc[37] = (int)(unsigned)(now >> 32);
   }
   __syncthreads();
+  TSTAMP(25);  // rows and kill list in
   if (!misc[47]) return 0;  // (else not built: the tile builds after the record)
   if (threadIdx.x < TILE) {
     // entries validated whatever the slot holds: a workgroup that lags may read a slot being
@@ -1237,7 +1247,7 @@ __device__ __noinline__ int prebuild_lists(KParams&, const GraphInfo gi, int j, 
     }
   }
   __syncthreads();
-  return build_nb_lists(p, gi, rows, scr, nullptr, L, true) ? 1 : 2;
+  return build_nb_lists(p, gi, rows, scr, ts, L, true) ? 1 : 2;
 }
 
 // Gather for one tile from the alive neighbour lists: per batch the layer's 256 threads stage
@@ -1702,7 +1712,7 @@ __device__ __noinline__ void df_store_tile(KParams&, int j, int L, int it, unsig
 // dft != 0 (dataflow mode): the outputs go out as granules tagged dft (df_store_tile); defer:
 // none at all -- they stay in LDS (E, X) for df_store_tile once the result is confirmed.
 __device__ __noinline__ bool spec_iteration1(KParams&, const GraphInfo gi, int j, int L, unsigned long long ew,
-                                             unsigned dft = 0, bool defer = false) {
+                                             unsigned dft = 0, bool defer = false, unsigned long long* ts = nullptr) {
   KParams& p = kp();
   float* const lds = lds_base();
   float* const scr = lds + L_SCR;
@@ -1718,14 +1728,17 @@ __device__ __noinline__ bool spec_iteration1(KParams&, const GraphInfo gi, int j
   }
   gather_tile2s(p, gi, 1, rows, scr, L, sl + sres_deg(et) + L * n, hp, dm);
   __syncthreads();
+  TSTAMP(26);  // diagnostics: gathered
   update_tile_split(lds + L_W, scr, L);
   __syncthreads();
   normalize_tile_split(scr + S_E, scr, L);
   __syncthreads();
+  TSTAMP(27);  // updated, normalised
   if (defer) return true;
   if (dft != 0) {
     df_store_tile(p, j, L, 1, dft);
     __syncthreads();
+    TSTAMP(35);  // stored
     return true;
   }
   if (threadIdx.x < 64) {
@@ -4360,7 +4373,9 @@ __device__ __noinline__ void df_tiles(KParams&) {
         DF_STAMP_MAX(54);
         pre_used = 0ull;
         deferred = false;
-        pre_state = prebuild_lists(p, gi, j, L, ew);
+        // diagnostics: tile 0's layer-0 workgroup stamps the pieces of its prebuild
+        unsigned long long* const pts = p.prof != nullptr && tb == 0 && pstep < p.prof_cap ? p.prof + (size_t)pstep * PROF_SLOTS : nullptr;
+        pre_state = prebuild_lists(p, gi, j, L, ew, pts, r == 3 ? *seen : 0ull);
         DF_STAMP_MAX(55);
         if (pre_state) pre_used = ew;
         // a prebuild from workgroup 0's result that phase A's early word has already overtaken
@@ -4372,7 +4387,7 @@ __device__ __noinline__ void df_tiles(KParams&) {
         }
         // the whole of iteration 1 too (MD_VARIANT bit 128: lists only)
         if (pre_state == 1 && !(p.variant & 128) &&
-            spec_iteration1(p, gi, j, L, ew, df_ptag(df_tag(pstep), ew), r == 3)) {
+            spec_iteration1(p, gi, j, L, ew, df_ptag(df_tag(pstep), ew), r == 3, pts)) {
           pre_state = 3;
           deferred = r == 3;
         }

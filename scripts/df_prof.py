@@ -16,6 +16,7 @@ for _ in range(10):
     e.reset(); e.rollout(); ks.append(e.last_timing()[0])
 e.reset(); e.profile(512); e.rollout(); ms, _ = e.last_timing()
 P = e.profile_read().astype(np.int64); e.profile(0)
+TR = e.trace(0)
 S = len(P)
 full = P[(P[:, 10] > 0) & (P[:, 0] > 0)]
 nxt = np.append(P[1:, 0], 0)[(P[:, 10] > 0) & (P[:, 0] > 0)]
@@ -53,6 +54,11 @@ print("  tiles seeing the record, latest (from the record): with prebuild %.1f  
 print("  phase A check (from the record): start %.1f end %.1f; steps whose check polled a running slot: %d of %d, longest poll median %.1f us" % (
     np.median((R[m, 69] - R[m, 3]) / 100.0), np.median((R[m, 71] - R[m, 3]) / 100.0), int((R[m, 31] > 0).sum()), int(m.sum()),
     np.median(R[m & (R[:, 31] > 0), 32] / 100.0) if (m & (R[:, 31] > 0)).any() else 0.0), flush=True)
+mp = (P[:, 28] > 0) & (P[:, 24] > 0) & (P[:, 25] > 0) & (P[:, 63] > 0) & (P[:, 26] > 0) & (P[:, 27] > 0) & (P[:, 35] > 0)
+if mp.any():
+    q = lambda a, b: np.median((P[mp, b] - P[mp, a]) / 100.0)
+    print("  tile 0 / layer 0 prebuild pieces (us, %d steps): poll %.1f  rows+kills %.1f  lists: prefix %.1f scan %.1f write %.1f  gather %.1f  update+norm %.1f  store %.1f  | total %.1f" % (
+        int(mp.sum()), q(28, 24), q(24, 25), q(25, 61), q(61, 62), q(62, 63), q(63, 26), q(26, 27), q(27, 35), q(28, 35)), flush=True)
 print("  request -> next record: spec wg0 done %.1f features %.1f" % (
     np.median((R[m, 68] - R[m, 64]) / 100.0), np.median((R[m, 74] - R[m, 64]) / 100.0)), flush=True)
 mq = m & (R[:, 65] > 0) & (R[:, 73] > 0) & (R[:, 66] > 0) & (R[:, 67] > 0) & (R[:, 68] > 0) & (R[:, 74] > 0)
@@ -93,13 +99,19 @@ if rows:
     print("  step classes: misses %d (%.0f us total, median %.1f), cascade %d (%.0f us, median %.1f), others %d (%.0f us, median %.1f); slot hits by rank: %s" % (
         miss.sum(), st[miss].sum(), np.median(st[miss]) if miss.any() else 0, casc.sum(), st[casc].sum(), np.median(st[casc]) if casc.any() else 0,
         rest.sum(), st[rest].sum(), np.median(st[rest]) if rest.any() else 0, np.bincount(hit).tolist()), flush=True)
+    nt, gp = TR["n_tie"], TR["gap"]
+    print("  misses (row: step us, ties / top-2 gap of predictions row-1..row+1): " + "; ".join(
+        "%d: %.0f us, %s" % (t, st[t], [(int(nt[k]), float(gp[k])) for k in range(max(0, t - 1), min(len(nt), t + 2))])
+        for t in np.nonzero(miss)[0]), flush=True)
 # per-tile distribution (rows 128 + 4 t + k): iteration-2 start and prebuild end, from the record
 # of step t (prebuild of step t+1 from the record of t)
+os.environ["MD_PROF_ALL"] = "1"
 e = _lib.Engine(W)
 e.load_graphs([(int(z["n_nodes"]), z["edges0"], z["edges1"])])
 e.reset(); e.rollout()
 e.reset(); e.profile(512); e.rollout()
 P2 = e.profile_read().astype(np.int64); e.profile(0)
+del os.environ["MD_PROF_ALL"]
 st_rel, pb_rel = [], []
 for t in range(1, min(60, (len(P2) - 132) // 4)):
     rec = P2[t, 3]
@@ -112,6 +124,20 @@ for t in range(1, min(60, (len(P2) - 132) // 4)):
         st_rel.append(np.percentile((s - rec) / 100.0, [10, 50, 90, 100]))
     if len(b):
         pb_rel.append(np.percentile((b - rec) / 100.0, [10, 50, 90, 100]))
+late = []
+for t in range(1, min(60, (len(P2) - 132) // 4)):
+    rec = P2[t, 3]
+    if rec == 0:
+        continue
+    s = np.concatenate([P2[128 + 4 * t, :64], P2[129 + 4 * t, :64]]).astype(np.float64)
+    s[s <= 0] = np.nan
+    if np.isfinite(s).any():
+        late.append(int(np.nanargmax(s)))
+if late:
+    lt = np.bincount(np.array(late), minlength=128)
+    top = np.argsort(-lt)[:8]
+    print("  latest tile workgroup to start iteration 2 (tile workgroup tb = 2 j + layer: steps): " +
+          ", ".join("%d: %d" % (int(k), int(lt[k])) for k in top if lt[k] > 0), flush=True)
 if st_rel:
     print("  per tile, iteration-2 start after the record (median over steps of the p10/p50/p90/max over tiles):",
           np.round(np.median(np.array(st_rel), axis=0), 1).tolist(), flush=True)
