@@ -92,7 +92,10 @@ def test_c3_256_graphs_one_queue_launch_and_tail(graphs, weights, single):
     """configs[2]: 256 graphs in one queue-mode launch (its last <= 8 running graphs continue
     in one lock-step launch, MD_QPARK) == 256 single-graph rollouts."""
     mr, outs, launches = batch_rollout(weights, graphs[:256])
-    assert launches == 2
+    # the queue launch, then the lock-step launch of the graphs it parked -- none when the last
+    # running graphs all end (typically by a K2 end-game) at the environment step that would
+    # park them, which depends on the order the workgroups reach them
+    assert launches in (1, 2)
     assert sum(len(s) for s, _ in outs) > 256 * 20
     check_against_single(mr, outs, single, 0)
     check_goldens(mr, outs)
@@ -103,7 +106,7 @@ def test_c5_slice_512_graphs_one_queue_launch_and_tail(graphs, weights, single):
     """configs[4]'s per-GPU slice: 512 graphs (G_CAP) in one queue launch and its lock-step
     tail launch == single-graph rollouts."""
     mr, outs, launches = batch_rollout(weights, graphs)
-    assert launches == 2
+    assert launches in (1, 2)  # (see the C3 test)
     check_against_single(mr, outs, single, 0)
     check_goldens(mr, outs)
 
