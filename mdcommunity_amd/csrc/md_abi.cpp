@@ -274,6 +274,7 @@ const char* err_name(int e) {
     case 6: return "kernel argument layout differs from the compiled assumption";
     case 7: return "dataflow mode: a tile's alive-neighbour list exceeded NB_CAP";
     case 8: return "dataflow mode: phase A's state differs from its early step record";
+    case 9: return "a speculative result's kill list is out of range";
     default: return e >= 1000 ? "bounds check failed (debug build; site = code - 1000)" : "unknown device error";
   }
 }

@@ -827,6 +827,7 @@ __device__ __forceinline__ int env_apply_spec(const EnvView<false>& E, const int
     ft = __hip_atomic_load((const g_u64*)(slot + SRES_FEAT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     dt = __hip_atomic_load((const g_u64*)slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  int bad_slot = 0;
   for (int i0 = threadIdx.x; i0 < nd; i0 += 4 * NTHREADS) {
     int v[4], c0[4], c1[4];
 #pragma unroll
@@ -843,12 +844,20 @@ __device__ __forceinline__ int env_apply_spec(const EnvView<false>& E, const int
       if (i0 + u * NTHREADS >= nd) continue;
       const int e = v[u] & 0xffff, l = e < E.e0 ? 0 : 1;
       const uint8_t s = (uint8_t)(v[u] >> 16);
+      // indices from another workgroup's result: checked before any write (a result that is
+      // not consistent raises ERR_SPEC_SLOT instead of writing out of range)
+      const int csr = 2 * (l ? E.et - E.e0 : E.e0);
+      if (!(e < E.et && c0[u] >= 0 && c0[u] < csr && c1[u] >= 0 && c1[u] < csr)) {
+        bad_slot = 1;
+        continue;
+      }
       E.st[e] = s;
       stc(E.gst[l] + (e < E.e0 ? e : e - E.e0), s);
       stc(E.calive[l] + c0[u], (uint8_t)0);
       stc(E.calive[l] + c1[u], (uint8_t)0);
     }
   }
+  if (__syncthreads_or(bad_slot) && threadIdx.x == 0) raise_err(kp(), ERR_SPEC_SLOT);
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int i = 0; i < 5; ++i) E.tmp[A_TMP_WORDS - 8 + i] = h[i];

@@ -125,7 +125,7 @@ static_assert(2 * STG_ROWS * 64 <= S_HID - S_M, "neighbour staging fits [S_M, S_
 constexpr float NEG_INF = -__builtin_huge_valf();
 constexpr unsigned long long BARRIER_TIMEOUT_TICKS = 400000000ull;  // 4 s at 100 MHz
 enum : int { ERR_TIMEOUT = 1, ERR_COVERED = 2, ERR_LIVE_MISMATCH = 3, ERR_BADNODE = 4, ERR_HOST = 5, ERR_ABI = 6,
-             ERR_DF_LISTS = 7, ERR_DF_EARLY = 8 };
+             ERR_DF_LISTS = 7, ERR_DF_EARLY = 8, ERR_SPEC_SLOT = 9 };
 
 // Kernel arguments of md_rollout_kernel / md_env_kernel, (Params, const float*), read in every
 // device function through the implicit-argument pointer (SGPRs s[8:9] in callees) at a fixed
@@ -4121,6 +4121,7 @@ __device__ __noinline__ void spec_loop(KParams&) {
     const int nd = E.hdr[1];
     for (int i = threadIdx.x; i < nd; i += NTHREADS) {
       const int e = E.dl[i];
+      if (!(e < et)) continue;  // (cannot happen: dead-list entries are edge ids)
       const int l = e < E.e0 ? 0 : 1, kk = e < E.e0 ? e : e - E.e0;
       stc(slot + SRES_HDR + 3 * i, e | ((int)E.st[e] << 16));
       stc(slot + SRES_HDR + 3 * i + 1, E.epos[l][2 * kk]);
