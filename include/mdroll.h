@@ -127,7 +127,7 @@ md_status md_rollout_trace(md_ctx* ctx, int graph, int32_t* n_live, int32_t* m0,
 
 /* Speculative environment steps of the last md_rollout for graph g: removals whose mutual-LMCC
  * fixed point was taken from a speculative workgroup (hits) out of all removals.  A
- * single-graph rollout runs up to MD_SPEC (default 16) extra workgroups on CUs it leaves
+ * single-graph rollout runs up to MD_SPEC (default 32) extra workgroups on CUs it leaves
  * free; each runs the next step's fixed point for one likely next removal while the tiles
  * compute Q.  Results never depend on it (diagnostics). */
 md_status md_spec_stats(md_ctx* ctx, int graph, int32_t* hits, int32_t* removals);
@@ -238,7 +238,14 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *                     precomputed per-dmax tables
  *   MD_HOST_STATS     set: print hand-shake timing statistics to stderr
  *   MD_SPEC           speculative environment workgroups of a single-graph rollout (0..32,
- *                     default 16, 0 = off; md_spec_stats)
+ *                     default 32, 0 = off; md_spec_stats)
+ *   MD_EARLY          0: speculative workgroups wait for phase A's write-back and restage the
+ *                     state instead of building the next state from the result phase A takes
+ *   MD_DF             single-graph rollouts in dedicated mode with the layer split: 1 (default)
+ *                     dataflow mode (no grid barrier, tagged hand-offs), 2 also prebuilds from
+ *                     speculative workgroup 0's result before phase A picks, 0 grid barriers
+ *   MD_PROF_ALL       md_profile_read returns every non-empty record row (the dataflow mode's
+ *                     per-tile rows after the step records), not only the step records
  *   MD_MAX_CUS        use at most this many CUs (>= 8; default: all), e.g. for several ranks
  *                     sharing one GPU, whose persistent grids must be co-resident
  */
