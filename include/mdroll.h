@@ -241,6 +241,8 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *                     default 32, 0 = off; md_spec_stats)
  *   MD_EARLY          0: speculative workgroups wait for phase A's write-back and restage the
  *                     state instead of building the next state from the result phase A takes
+ *   MD_SPEC_ABORT     0: a speculative fixed point runs to the end even when phase A has taken
+ *                     another result of its request (default 1: it stops after the round)
  *   MD_DF             single-graph rollouts in dedicated mode with the layer split: 1 (default)
  *                     dataflow mode (no grid barrier, tagged hand-offs), 2 also prebuilds from
  *                     speculative workgroup 0's result before phase A picks, 0 grid barriers

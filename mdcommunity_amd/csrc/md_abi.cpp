@@ -147,6 +147,9 @@ struct md_ctx {
   // speculative workgroups build the next step's state from the result phase A takes, before
   // its write-back (spec_loop early requests); MD_EARLY=0 turns it off
   bool early_on = true;
+  // a speculative fixed point stops once phase A has taken another result of its request or a
+  // later request is out (MD_SPEC_ABORT=0: always runs to the end)
+  bool abort_on = true;
   bool df_r0 = false;  // measured: no gain over the early-word prebuild alone
   DevBuf<unsigned long long> dfbuf;
   int df_mt = 0, df_n = 0;
@@ -531,6 +534,7 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
       p.pre_ew = (unsigned long long*)(c->ctl.p + CTL_PRE);
       p.pre_cw = (unsigned long long*)(c->ctl.p + CTL_PRE + 2);
       p.spec_early = c->early_on ? 1 : 0;
+      p.spec_abort = c->abort_on ? 1 : 0;
     }
   }
   if (df) {
@@ -737,6 +741,7 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_POLL_US")) c->poll_us = std::atoi(v);
   if (const char* v = std::getenv("MD_H0G")) c->h0g_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_EARLY")) c->early_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MD_SPEC_ABORT")) c->abort_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_DF")) {
     c->df_on = std::atoi(v) != 0;
     c->df_r0 = std::atoi(v) == 2;  // MD_DF=2: with the prebuild from speculative workgroup 0's result

@@ -173,6 +173,7 @@ struct Params {
   unsigned long long* pre_ew;
   unsigned long long* pre_cw;
   int spec_early;                  // 1: speculative workgroups serve the next request from pre_ew (spec_loop)
+  int spec_abort;                  // 1: a speculative fixed point stops once its result cannot be used
   int qspec_n;                     // total nodes of the loaded batch
   // dataflow mode (single-graph rollouts in dedicated mode with the layer split, md_kernels.hip
   // df_*): no grid barrier; the step record, the H rows, the virtual-node and arg-max partials

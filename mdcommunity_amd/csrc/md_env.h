@@ -407,21 +407,44 @@ __device__ void compact_alive(const EnvView<GL>& E) {
 // `cover` >= 0: first cover that node (U/mvc_env.py:74-85) inside the first union pass -- its
 // alive edges become covered instead of being united -- and return the covered edge counts
 // per layer in cc[2].
+// Speculative workgroups (spec_loop): the fixed point of a request's candidate stops after a
+// round once the result cannot be used -- phase A's early word names another result of the same
+// request, or a later request is out -- so a workgroup stuck in a long cascade is free for the
+// next request sooner.  Returns -1 then (the LDS state is partial).
+struct SpecAbort {
+  const unsigned long long* ew;   // phase A's early word
+  const unsigned long long* req;  // the request word
+  unsigned tag;                   // this request's tag
+  int slot;                       // this workgroup's result slot (parity included)
+  int step;                       // this request's step
+};
 template <bool GL>
-__device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long long* acc, int cover, int* cc) {
+__device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long long* acc, int cover, int* cc,
+                               const SpecAbort* ab = nullptr) {
   const EnvView<GL> E = Ein;  // fields in registers
   const int n = E.gi->n;
   int pruned0 = 0, pruned1 = 0;
   if (acc != nullptr && threadIdx.x == 0) acc[PA_CALLS] += 1;
   bool first = true, dirty = cover >= 0;  // dead entries in the alive list
+  unsigned long long ab_ew = 0ull, ab_req = 0ull;  // thread 0: loaded during the previous round's prune
   while (true) {
     unsigned long long tp = wall_clock64();
     if (acc != nullptr && threadIdx.x == 0) acc[PA_ROUNDS] += 1;
+    if constexpr (!GL) {
+      if (ab != nullptr && !first && threadIdx.x == 0) {
+        const bool taken_elsewhere = (unsigned)(ab_ew >> 32) == ab->tag && (int)(ab_ew & 0xffffu) != ab->slot;
+        const bool newer = ab_req != 0ull && ab_req != SPEC_EXIT && (int)(unsigned)(ab_req >> 32) > ab->step;
+        E.hdr[3] = (taken_elsewhere || newer) ? 1 : 0;
+      }
+    }
     for (int x = threadIdx.x; x < n; x += NTHREADS) {
       uf_store(E.par0, x, x);
       uf_store(E.par1, x, x);
     }
     __syncthreads();
+    if constexpr (!GL) {
+      if (ab != nullptr && !first && E.hdr[3] != 0) return -1;
+    }
     PACC(acc, PA_INIT, tp);
     int k0 = 0, k1 = 0;
     if (first && cover >= 0) {
@@ -486,6 +509,12 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
       break;
     }
     int c0 = 0, c1 = 0;
+    if constexpr (!GL) {
+      if (ab != nullptr && threadIdx.x == 0) {  // (used at the next round's start)
+        ab_ew = __hip_atomic_load((const g_u64*)ab->ew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ab_req = __hip_atomic_load((const g_u64*)ab->req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
     for_each_alive<GL>(E, [&](int e, int u, int v) {
       auto other = e < E.e0 ? E.deg1 : E.deg0;  // layer-0 edges are pruned by layer-1 components
       if (uf_load(other, u) != uf_load(other, v)) {

@@ -4117,7 +4117,18 @@ __device__ __noinline__ void spec_loop(KParams&) {
     __syncthreads();
     TSTAMP(67);
     int pr[2], cc[2];
-    const int lm = mcc_fixed_point<false>(E, pr, nullptr, c, cc);
+    SpecAbort ab;
+    ab.ew = p.pre_ew;
+    ab.req = p.spec_req;
+    ab.tag = tag;
+    ab.slot = spec_slot_index(k, misc[2]);
+    ab.step = misc[2];
+    const int lm = mcc_fixed_point<false>(E, pr, nullptr, c, cc, p.pre_ew != nullptr && p.spec_abort ? &ab : nullptr);
+    if (lm < 0) {  // the result can no longer be used: the LDS state is partial, restage next
+      mine = -2;
+      if (ts != nullptr && threadIdx.x == 0) ts[36] = 1;  // diagnostics: aborted
+      continue;
+    }
     const int nd = E.hdr[1];
     for (int i = threadIdx.x; i < nd; i += NTHREADS) {
       const int e = E.dl[i];

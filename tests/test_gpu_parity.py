@@ -323,24 +323,26 @@ def test_speculative_steps_match_plain(monkeypatch, name):
     the same removal sequence and LMCC trace as without them, with most removals served by a
     speculative result, for the per-step protocol and the K2 end-game alike; 16 and 32 of
     them, with early requests (the next state built from the result phase A takes) and
-    without (MD_EARLY=0: restaged from HBM after phase A's write-back)."""
+    without (MD_EARLY=0: restaged from HBM after phase A's write-back), and with the fixed
+    points of unusable results stopped early or run to the end (MD_SPEC_ABORT=0)."""
     z = load_golden(name)
     n = int(z["n_nodes"])
     w = engine.load_weights(engine.DEFAULT_UNIT)
     out = {}
-    for spec, early in (("0", "1"), ("16", "1"), ("32", "1"), ("32", "0")):
+    for spec, early, abort in (("0", "1", "1"), ("16", "1", "1"), ("32", "1", "1"), ("32", "0", "1"), ("32", "1", "0")):
         for variant in ("0", "2048"):
             monkeypatch.setenv("MD_SPEC", spec)
             monkeypatch.setenv("MD_EARLY", early)
+            monkeypatch.setenv("MD_SPEC_ABORT", abort)
             monkeypatch.setenv("MD_VARIANT", variant)
             e = _lib.Engine(w)
             e.load_graphs([(n, z["edges0"], z["edges1"])])
             for rep in range(2):
                 e.reset()
                 seq, ranks = e.rollout()[0]
-                out.setdefault((spec, early, variant), []).append((seq.tolist(), ranks.tolist(), e.spec_stats(0)))
+                out.setdefault((spec, early, abort, variant), []).append((seq.tolist(), ranks.tolist(), e.spec_stats(0)))
             e.close()
-    base = out[("0", "1", "0")][0]
+    base = out[("0", "1", "1", "0")][0]
     for key, runs in out.items():
         for seq, ranks, (hits, rem) in runs:
             assert seq == base[0] and ranks == base[1], key
