@@ -243,9 +243,11 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *                     state instead of building the next state from the result phase A takes
  *   MD_SPEC_ABORT     0: a speculative fixed point runs to the end even when phase A has taken
  *                     another result of its request (default 1: it stops after the round)
- *   MD_DF             single-graph rollouts in dedicated mode with the layer split: 1 (default)
- *                     dataflow mode (no grid barrier, tagged hand-offs), 2 also prebuilds from
- *                     speculative workgroup 0's result before phase A picks, 0 grid barriers
+ *   MD_DF             single-graph rollouts in dedicated mode with the layer split: 3 (default)
+ *                     dataflow mode (no grid barrier, tagged hand-offs) whose tiles derive
+ *                     phase A's pick from the arg-max partials and prebuild from it; 1 without
+ *                     that (the prebuild waits for phase A's early word); 2 prebuilds from
+ *                     speculative workgroup 0's result before phase A picks; 0 grid barriers
  *   MD_PROF_ALL       md_profile_read returns every non-empty record row (the dataflow mode's
  *                     per-tile rows after the step records), not only the step records
  *   MD_MAX_CUS        use at most this many CUs (>= 8; default: all), e.g. for several ranks

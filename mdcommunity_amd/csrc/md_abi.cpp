@@ -151,6 +151,8 @@ struct md_ctx {
   // later request is out (MD_SPEC_ABORT=0: always runs to the end)
   bool abort_on = true;
   bool df_r0 = false;  // measured: no gain over the early-word prebuild alone
+  bool df_self = true;  // MD_DF=3 (default): tiles derive phase A's pick (df_wait_rec)
+  bool self_spec = true;  // ... and publish it to the speculative workgroups (MD_SELF_SPEC=0: off)
   DevBuf<unsigned long long> dfbuf;
   int df_mt = 0, df_n = 0;
   std::vector<char> df_graph;
@@ -209,7 +211,7 @@ md_status fail(md_ctx* c, md_status s, const char* fmt, ...) {
   } while (0)
 
 // Control block layout (ints): [0] barrier counter, [1] error word (zeroed before each launch).
-constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_Q = 2, CTL_SPEC = 8, CTL_TEAM = 12, CTL_EXIT = 14, CTL_PRE = 64,
+constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_Q = 2, CTL_SPEC = 8, CTL_TEAM = 12, CTL_EXIT = 14, CTL_SELF = 32, CTL_PRE = 64,
               CTL_RING = 96, CTL_WORDS = 96 + 32 * 8;  // CTL_PRE and each ring's tickets on lines of their own
 constexpr int SPEC_MAX = 32;  // speculative workgroups per launch at most  // CTL_SPEC: u64 request word
 
@@ -542,6 +544,8 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
     p.df_mt = c->df_mt;
     p.df_n = c->df_n;
     p.df_r0 = c->df_r0 ? 1 : 0;
+    p.df_self = c->df_self ? 1 : 0;
+    if (c->df_self && p.pre_ew != nullptr && c->self_spec) p.self_ew = (unsigned long long*)(c->ctl.p + CTL_SELF);
   }
   p.qmode = qmode ? 1 : 0;
   p.qpair = c->pair_on ? 1 : 0;
@@ -742,9 +746,11 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_H0G")) c->h0g_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_EARLY")) c->early_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_SPEC_ABORT")) c->abort_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MD_SELF_SPEC")) c->self_spec = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_DF")) {
     c->df_on = std::atoi(v) != 0;
     c->df_r0 = std::atoi(v) == 2;  // MD_DF=2: with the prebuild from speculative workgroup 0's result
+    c->df_self = std::atoi(v) == 3;
   }
   if (const char* v = std::getenv("MD_SPEC")) c->spec_n = std::max(0, std::min(SPEC_MAX, std::atoi(v)));
   md_status st = MD_OK;

@@ -172,6 +172,9 @@ struct Params {
   // the result while phase A runs and keep them when the confirmation matches
   unsigned long long* pre_ew;
   unsigned long long* pre_cw;
+  // dataflow mode with the self-pick: tile 0's derivation of phase A's early word, published when
+  // the result it names is finished (speculative workgroups start the next state from it)
+  unsigned long long* self_ew;
   int spec_early;                  // 1: speculative workgroups serve the next request from pre_ew (spec_loop)
   int spec_abort;                  // 1: a speculative fixed point stops once its result cannot be used
   int qspec_n;                     // total nodes of the loaded batch
@@ -184,6 +187,7 @@ struct Params {
   int df_mt;                       // tiles of the largest graph the buffer is sized for
   int df_n;                        // nodes of that graph
   int df_r0;                       // 1: tiles prebuild from speculative workgroup 0's result before phase A picks
+  int df_self;                     // 1: tiles derive phase A's pick from the arg-max partials (df_wait_rec)
 };
 // dataflow buffer size (granules) for graphs of at most n nodes / mt tiles
 inline long long df_granules(int n, int mt) { return 64 + 772LL * mt + 8LL * 64 * n; }

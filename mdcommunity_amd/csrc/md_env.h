@@ -413,6 +413,7 @@ __device__ void compact_alive(const EnvView<GL>& E) {
 // next request sooner.  Returns -1 then (the LDS state is partial).
 struct SpecAbort {
   const unsigned long long* ew;   // phase A's early word
+  const unsigned long long* ew2;  // tile 0's derivation of it (nullptr: none)
   const unsigned long long* req;  // the request word
   unsigned tag;                   // this request's tag
   int slot;                       // this workgroup's result slot (parity included)
@@ -426,13 +427,14 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
   int pruned0 = 0, pruned1 = 0;
   if (acc != nullptr && threadIdx.x == 0) acc[PA_CALLS] += 1;
   bool first = true, dirty = cover >= 0;  // dead entries in the alive list
-  unsigned long long ab_ew = 0ull, ab_req = 0ull;  // thread 0: loaded during the previous round's prune
+  unsigned long long ab_ew = 0ull, ab_ew2 = 0ull, ab_req = 0ull;  // thread 0: loaded during the previous round's prune
   while (true) {
     unsigned long long tp = wall_clock64();
     if (acc != nullptr && threadIdx.x == 0) acc[PA_ROUNDS] += 1;
     if constexpr (!GL) {
       if (ab != nullptr && !first && threadIdx.x == 0) {
-        const bool taken_elsewhere = (unsigned)(ab_ew >> 32) == ab->tag && (int)(ab_ew & 0xffffu) != ab->slot;
+        const bool taken_elsewhere = ((unsigned)(ab_ew >> 32) == ab->tag && (int)(ab_ew & 0xffffu) != ab->slot) ||
+                                     ((unsigned)(ab_ew2 >> 32) == ab->tag && (int)(ab_ew2 & 0xffffu) != ab->slot);
         const bool newer = ab_req != 0ull && ab_req != SPEC_EXIT && (int)(unsigned)(ab_req >> 32) > ab->step;
         E.hdr[3] = (taken_elsewhere || newer) ? 1 : 0;
       }
@@ -513,6 +515,7 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
       if (ab != nullptr && threadIdx.x == 0) {  // (used at the next round's start)
         ab_ew = __hip_atomic_load((const g_u64*)ab->ew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ab_req = __hip_atomic_load((const g_u64*)ab->req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ab->ew2 != nullptr) ab_ew2 = __hip_atomic_load((const g_u64*)ab->ew2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     for_each_alive<GL>(E, [&](int e, int u, int v) {

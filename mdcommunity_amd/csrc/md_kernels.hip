@@ -1492,7 +1492,7 @@ __device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it,
 // read as tagged granules (df_hb) -- 32 lanes per row, each loading its two features and their
 // tags in one 16-byte load -- polled until every tag is ta or tb, so the gather itself waits for
 // exactly the rows it needs instead of a grid barrier.  Same staging, same adds in CSR order.
-__device__ __noinline__ void gather_df(KParams&, const GraphInfo gi, int it, int L, unsigned ta, unsigned tb) {
+__device__ __forceinline__ void gather_df(KParams&, const GraphInfo gi, int it, int L, unsigned ta, unsigned tb) {
   const int* const rows = (const int*)(lds_base() + L_SCR + S_ROW);
   float* const scr = lds_base() + L_SCR;
 
@@ -1682,7 +1682,7 @@ __device__ __noinline__ void normalize_tile_split(float*, float*, int L) {
 // path's values) and the new embedding rows, thread t storing row t / 32's features 2 (t % 32)
 // and 2 (t % 32) + 1 as one 16-byte pair of granules.  Reads E / X in LDS: the caller syncs
 // before overwriting them.
-__device__ __noinline__ void df_store_tile(KParams&, int j, int L, int it, unsigned tag) {
+__device__ __forceinline__ void df_store_tile(KParams&, int j, int L, int it, unsigned tag) {
   KParams& p = kp();
   float* const scr = lds_base() + L_SCR;
   const int* rows = (const int*)(scr + S_ROW);
@@ -1711,7 +1711,7 @@ __device__ __noinline__ void df_store_tile(KParams&, int j, int L, int it, unsig
 
 // dft != 0 (dataflow mode): the outputs go out as granules tagged dft (df_store_tile); defer:
 // none at all -- they stay in LDS (E, X) for df_store_tile once the result is confirmed.
-__device__ __noinline__ bool spec_iteration1(KParams&, const GraphInfo gi, int j, int L, unsigned long long ew,
+__device__ __forceinline__ bool spec_iteration1(KParams&, const GraphInfo gi, int j, int L, unsigned long long ew,
                                              unsigned dft = 0, bool defer = false, unsigned long long* ts = nullptr) {
   KParams& p = kp();
   float* const lds = lds_base();
@@ -3874,6 +3874,7 @@ __device__ __noinline__ void spec_loop(KParams&) {
       // error word
       const int lane = threadIdx.x;
       const bool we = p.pre_ew != nullptr && mine >= -1 && p.spec_early;
+      const bool ws = we && p.self_ew != nullptr;
       const unsigned long long t0 = wall_clock64();
       unsigned long long v, ew = 0ull;
       int stop = 0, early = 0;
@@ -3882,10 +3883,15 @@ __device__ __noinline__ void spec_loop(KParams&) {
         if (lane == 0) g = __hip_atomic_load((const g_u64*)p.spec_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else if (lane == 1 && we) g = __hip_atomic_load((const g_u64*)p.pre_ew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else if (lane == 2) g = __hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else if (lane == 3 && ws) g = __hip_atomic_load((const g_u64*)p.self_ew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned lo = (unsigned)g, hi = (unsigned)(g >> 32);
         v = ((unsigned long long)(unsigned)__shfl((int)hi, 0, 64) << 32) | (unsigned)__shfl((int)lo, 0, 64);
         ew = ((unsigned long long)(unsigned)__shfl((int)hi, 1, 64) << 32) | (unsigned)__shfl((int)lo, 1, 64);
         const unsigned bw = (unsigned)__shfl((int)lo, 2, 64);
+        if (ws && !(ew != last_ew && (unsigned)(ew >> 32) == (unsigned)last)) {
+          // tile 0's self-pick: the word phase A's early word will be (its result finished)
+          ew = ((unsigned long long)(unsigned)__shfl((int)hi, 3, 64) << 32) | (unsigned)__shfl((int)lo, 3, 64);
+        }
         if (v == SPEC_EXIT) { stop = 1; break; }
         if (we && ew != last_ew && (unsigned)(ew >> 32) == (unsigned)last) {
           v = ((unsigned long long)((unsigned)(last >> 32) + 1u) << 32) |
@@ -4119,6 +4125,7 @@ __device__ __noinline__ void spec_loop(KParams&) {
     int pr[2], cc[2];
     SpecAbort ab;
     ab.ew = p.pre_ew;
+    ab.ew2 = p.self_ew;
     ab.req = p.spec_req;
     ab.tag = tag;
     ab.slot = spec_slot_index(k, misc[2]);
@@ -4195,8 +4202,19 @@ __device__ __noinline__ void spec_loop(KParams&) {
 // L_MISC + 42), 0 on an error anywhere.  Uniform.
 // With `watch`, also 3 when speculative workgroup 0's result for this step's request (spec_req of
 // step req_step) has its features published and differs from the LDS word at L_MISC + 38 (then
-// updated): the likeliest next state, prebuilt before phase A has picked.
-__device__ __noinline__ int df_wait_rec(KParams&, unsigned tag, bool watch, bool full = false, int req_step = -1) {
+// updated): the likeliest next state, prebuilt before phase A has picked (p.df_r0).
+// Self-pick (p.df_self, nt_self = the previous step's tile count, <= 64): the wave also polls the
+// previous step's arg-max partials (phase A's inputs) and, once all are in, combines them exactly
+// as phase A does; a unique maximum whose node is the candidate of a started or finished result
+// of request req_step gives the early word phase A will publish, returned as 4 (L_MISC + 38) --
+// the prebuild then starts before phase A's slot check, and stores at once: phase A takes the
+// same node, so the same state and tile assignment, whether it then takes this result (the same
+// early word, absorbed here without a return) or computes the state itself (a result that
+// started after its slot pre-read: the confirmation does not match and the tile rebuilds the
+// same rows untagged).  misc[30] = 1 once this step's self-pick is decided (or phase A's early
+// word came first).
+__device__ __forceinline__ int df_wait_rec(KParams&, unsigned tag, bool watch, bool full = false, int req_step = -1,
+                                        int nt_self = 0) {
   KParams& p = kp();
   int* const misc = (int*)(lds_base() + L_MISC);
   unsigned long long* const seen = (unsigned long long*)(lds_base() + L_MISC + 42);
@@ -4204,8 +4222,13 @@ __device__ __noinline__ int df_wait_rec(KParams&, unsigned tag, bool watch, bool
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     const bool w = watch && p.pre_ew != nullptr;
-    const bool w0 = w && req_step >= 0 && p.sres != nullptr && p.spec_req != nullptr;
-    const unsigned long long sv = *seen, s0 = *tried0;
+    const bool wr = w && req_step >= 0 && p.sres != nullptr && p.spec_req != nullptr;
+    const bool w0 = wr && p.df_r0;
+    bool ws = wr && nt_self > 0 && nt_self <= 64 && !p.host_select && misc[30] == 0;
+    const unsigned ptag = (unsigned)(req_step + 1) << 1;  // the partials of step req_step (df_tag)
+    const float* const apb = (const float*)df_ap(p);
+    unsigned long long sv = *seen;
+    const unsigned long long s0 = *tried0;
     const unsigned long long t0 = wall_clock64();
     int res = 0;
     while (true) {
@@ -4214,10 +4237,15 @@ __device__ __noinline__ int df_wait_rec(KParams&, unsigned tag, bool watch, bool
       if (lane < 7) g = __hip_atomic_load((const g_u64*)(p.df + DF_REC + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else if (lane == 8) g = __hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else if (lane == 7 && w) g = __hip_atomic_load((const g_u64*)p.pre_ew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else if (lane == 9 && w0) g = __hip_atomic_load((const g_u64*)p.spec_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else if (lane == 9 && (w0 || ws)) g = __hip_atomic_load((const g_u64*)p.spec_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else if (lane == 10 && w0)
         g = __hip_atomic_load((const g_u64*)(p.sres + (size_t)spec_slot_index(0, req_step) * p.sres_stride + SRES_FEAT),
                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pc = pa;
+      if (ws && lane < nt_self) {
+        pa = ldc4(apb, lane * 32);
+        pc = ldc4(apb, lane * 32 + 16);
+      }
       if (__ballot(lane == 8 && (g & BAR_ERR))) break;
       // a new early word first (phase A publishes it with, or just before, an early record: the
       // prebuild from it is the tile's fastest start)
@@ -4225,15 +4253,65 @@ __device__ __noinline__ int df_wait_rec(KParams&, unsigned tag, bool watch, bool
         const unsigned lo = __shfl((unsigned)g, 7, 64), hi = __shfl((unsigned)(g >> 32), 7, 64);
         const unsigned long long ew = ((unsigned long long)hi << 32) | lo;
         if (ew != sv) {
-          if (lane == 0) *seen = ew;
-          res = 2;
-          break;
+          if (lane == 0) {
+            *seen = ew;
+            misc[30] = 1;
+          }
+          sv = ew;
+          // (phase A's early word equal to this step's self-pick: that prebuild is the one)
+          if (!(p.df_self && ew == s0 && (unsigned)(ew >> 32) != 0u)) {
+            res = 2;
+            break;
+          }
         }
       }
       if (!__ballot((lane < 6 || (lane == 6 && full)) && (unsigned)(g >> 32) != tag)) {
         if (lane < 6) misc[50 + lane] = (int)(unsigned)g;
         res = 1;
         break;
+      }
+      if (ws && !__ballot(lane < nt_self && !(df_ok4(pa, ptag, ptag) && df_ok4(pc, ptag, ptag)))) {
+        // every partial of the step is in: phase A's combine (max / min / sum steps, so the
+        // result does not depend on the order)
+        float bm = NEG_INF, bs = NEG_INF;
+        int bi = 0x7fffffff, bc = 0;
+        const int c = lane < nt_self ? __float_as_int(pc.z) : 0;
+        if (c != 0) argmax_combine(bm, bs, bi, bc, pa.x, pa.z, __float_as_int(pc.x), c);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const float m2 = __shfl_xor(bm, o, 64), s2 = __shfl_xor(bs, o, 64);
+          const int i2 = __shfl_xor(bi, o, 64), c2 = __shfl_xor(bc, o, 64);
+          if (c2 != 0) argmax_combine(bm, bs, bi, bc, m2, s2, i2, c2);
+        }
+        const unsigned rlo = __shfl((unsigned)g, 9, 64), rhi = __shfl((unsigned)(g >> 32), 9, 64);
+        ws = false;
+        if (lane == 0) misc[30] = 1;
+        if (bc == 1 && (int)rhi == req_step && rlo != 0u) {
+          // the result of the request whose candidate is the pick (started or finished): the
+          // one phase A's slot check takes
+          unsigned long long sd = 0ull, ss = 0ull;
+          if (lane < p.n_spec) {
+            const g_u64* tp = (const g_u64*)(p.sres + (size_t)spec_slot_index(lane, req_step) * p.sres_stride);
+            sd = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ss = __hip_atomic_load(tp + SRES_STARTED / 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          const bool fin = lane < p.n_spec && (unsigned)sd == rlo && (int)((sd >> 32) & 0xffffu) == bi;
+          const bool hit = fin || (lane < p.n_spec && (unsigned)ss == rlo && (int)(ss >> 32) == bi);
+          const unsigned long long m = __ballot(hit);
+          if (m != 0ull) {
+            const int k = __builtin_ctzll(m);
+            const unsigned long long e0 = ((unsigned long long)rlo << 32) | ((unsigned long long)(unsigned)bi << 16) |
+                                          (unsigned)spec_slot_index(k, req_step);
+            // tile 0 (layer 0) hands a finished result's word to the speculative workgroups
+            if (p.self_ew != nullptr && (int)blockIdx.x == 2 * p.n_env && lane == k && fin)
+              __hip_atomic_store((g_u64*)p.self_ew, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (e0 != s0) {
+              if (lane == 0) *tried0 = e0;
+              res = 4;
+              break;
+            }
+          }
+        }
       }
       if (w0) {
         const unsigned rlo = __shfl((unsigned)g, 9, 64), rhi = __shfl((unsigned)(g >> 32), 9, 64);
@@ -4365,8 +4443,12 @@ __device__ __noinline__ void df_tiles(KParams&) {
   unsigned long long* const seen = (unsigned long long*)(lds + L_MISC + 42);
   unsigned long long* const tried0 = (unsigned long long*)(lds + L_MISC + 38);
   if (threadIdx.x == 0) *seen = *tried0 = 0ull;
+  int nl_prev = 0;  // live nodes of the previous step (its tile count: the self-pick's partials)
   for (int pstep = 0;; ++pstep) {
-    if (threadIdx.x == 0) misc[60] = pstep;
+    if (threadIdx.x == 0) {
+      misc[60] = pstep;
+      misc[30] = 0;  // this step's self-pick not decided yet (df_wait_rec)
+    }
     __syncthreads();
     // the step record; meanwhile the iteration-1 prebuild, first from speculative workgroup 0's
     // result (the likeliest pick, ready before phase A has picked), then, if phase A's early word
@@ -4379,21 +4461,22 @@ __device__ __noinline__ void df_tiles(KParams&) {
     int pre_state = 0, r;
     unsigned long long pre_used = 0ull;
     bool deferred = false;
-    while ((r = df_wait_rec(p, (unsigned)(pstep + 1), true, false, p.df_r0 ? pstep - 1 : -1)) >= 2) {
-      const unsigned long long ew = r == 2 ? *seen : *tried0;
+    while ((r = df_wait_rec(p, (unsigned)(pstep + 1), true, false, p.df_r0 || p.df_self ? pstep - 1 : -1,
+                            p.df_self && pstep >= 1 ? (nl_prev + TILE - 1) / TILE : 0)) >= 2) {
+      const unsigned long long ew = r == 2 ? *seen : *tried0;  // (3: workgroup 0's result, 4: the self-pick)
       if (ew != 0ull && ew != pre_used) {
         DF_STAMP_MAX(54);
         pre_used = 0ull;
         deferred = false;
         // diagnostics: tile 0's layer-0 workgroup stamps the pieces of its prebuild
         unsigned long long* const pts = p.prof != nullptr && tb == 0 && pstep < p.prof_cap ? p.prof + (size_t)pstep * PROF_SLOTS : nullptr;
-        pre_state = prebuild_lists(p, gi, j, L, ew, pts, r == 3 ? *seen : 0ull);
+        pre_state = prebuild_lists(p, gi, j, L, ew, pts, r >= 3 ? *seen : 0ull);
         DF_STAMP_MAX(55);
         if (pre_state) pre_used = ew;
         // a prebuild from workgroup 0's result that phase A's early word has already overtaken
         // (it names another result) stops after its lists
         const unsigned long long now = ((unsigned long long)(unsigned)misc[37] << 32) | (unsigned)misc[36];
-        if (r == 3 && pre_state == 1 && now != 0ull && now != *seen && now != ew) {
+        if (r >= 3 && pre_state == 1 && now != 0ull && now != *seen && now != ew) {
           pre_state = 0;
           pre_used = 0ull;
         }
@@ -4415,6 +4498,7 @@ __device__ __noinline__ void df_tiles(KParams&) {
     if (r != 1 || misc[50] != ST_RUN) break;
     DF_STAMP(4);
     const int nl = misc[51];
+    nl_prev = nl;
     const unsigned long long cw = ((unsigned long long)(unsigned)misc[53] << 32) | (unsigned)misc[52];
     __syncthreads();
     // the next step's wait starts from this step's early word: a change is the next phase A's
