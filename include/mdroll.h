@@ -248,6 +248,8 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *                     phase A's pick from the arg-max partials and prebuild from it; 1 without
  *                     that (the prebuild waits for phase A's early word); 2 prebuilds from
  *                     speculative workgroup 0's result before phase A picks; 0 grid barriers
+ *   MD_SELF_SPEC      0: the speculative workgroups wait for phase A's early word instead of
+ *                     tile 0's derivation of it (MD_DF=3)
  *   MD_PROF_ALL       md_profile_read returns every non-empty record row (the dataflow mode's
  *                     per-tile rows after the step records), not only the step records
  *   MD_MAX_CUS        use at most this many CUs (>= 8; default: all), e.g. for several ranks

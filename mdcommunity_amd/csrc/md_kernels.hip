@@ -1975,8 +1975,10 @@ __device__ __forceinline__ void graph_aux(float* gs, const GraphInfo& gi, const 
 
 // Graph rows: y_l from the final virtual-node embeddings E_l = Y3_l (in L_YW), the layer-mix
 // weights softmax(relu(y_l.WL1).WL2) and the aux features (U/PrepareBatchGraph.py:92-101).
+__device__ __forceinline__ void head_publish_part(KParams& p, const float* lds, int g, unsigned long long htag, bool mix);
 __device__ __noinline__ void graph_head(KParams&, float*, float*, const GraphInfo gi,
-                                        const GraphVar&, bool wl1_resident, bool aux_ready) {
+                                        const GraphVar&, bool wl1_resident, bool aux_ready,
+                                        unsigned long long pub_tag = 0ull, int pub_g = -1) {
   float* const lds = lds_base();
   float* const scr = lds + L_SCR;
   const GraphVar& gv = *(const GraphVar*)(lds + L_GV);
@@ -2013,6 +2015,9 @@ __device__ __noinline__ void graph_head(KParams&, float*, float*, const GraphInf
     ys[l * 64 + lane] = m / fmaxf(nr, 1e-12f);
   }
   __syncthreads();
+  // (dedicated mode: y and the aux features go to the tiles now, the layer-mix weights below
+  // when they are done -- the tiles' attention needs them only for the final combine)
+  if (pub_tag != 0ull) head_publish_part(p, lds, pub_g, pub_tag, false);
   if (threadIdx.x < 256) {
     const int ll = threadIdx.x >> 7, j = threadIdx.x & 127;
     const float a = fma_chain<64>(0.f, 0, [&](int k) { return ys[ll * 64 + k]; },
@@ -2046,6 +2051,7 @@ __device__ __noinline__ void graph_head(KParams&, float*, float*, const GraphInf
 // each of 144 tile threads polls its own granule until the tag matches: one memory round trip
 // for the hand-off, no separate flag (MI355X_MICROARCH.md, handoff-1to1 row: 8-byte granules).
 constexpr int HB_FLOATS = 144;
+constexpr int HB_MIX = 128;  // granules 128, 129: the layer-mix weights (L_GS[0..1])
 __device__ __forceinline__ void head_publish(KParams& p, const float* lds, int g, unsigned long long htag) {
   if (threadIdx.x < HB_FLOATS) {
     const unsigned long long gr = (htag << 32) | (unsigned)__float_as_uint(lds[L_YS + threadIdx.x]);
@@ -2053,8 +2059,18 @@ __device__ __forceinline__ void head_publish(KParams& p, const float* lds, int g
                        __HIP_MEMORY_SCOPE_AGENT);
   }
 }
-__device__ __forceinline__ void head_receive(KParams& p, float* lds, int g, unsigned long long htag) {
-  if (threadIdx.x < HB_FLOATS) {
+// the granules of head_publish without the layer-mix weights (mix = false), or those two alone
+__device__ __forceinline__ void head_publish_part(KParams& p, const float* lds, int g, unsigned long long htag, bool mix) {
+  const int t = threadIdx.x;
+  if (t < HB_FLOATS && ((t == HB_MIX || t == HB_MIX + 1) == mix)) {
+    const unsigned long long gr = (htag << 32) | (unsigned)__float_as_uint(lds[L_YS + t]);
+    __hip_atomic_store((g_u64*)(p.hbuf + 2 * ((size_t)g * HB_FLOATS + t)), gr, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// skip_mix: every granule but the layer-mix weights (head_mix_weights polls those)
+__device__ __forceinline__ void head_receive(KParams& p, float* lds, int g, unsigned long long htag, bool skip_mix = false) {
+  if (threadIdx.x < HB_FLOATS && !(skip_mix && (threadIdx.x == HB_MIX || threadIdx.x == HB_MIX + 1))) {
     const g_u64* src = (const g_u64*)(p.hbuf + 2 * ((size_t)g * HB_FLOATS + threadIdx.x));
     const unsigned long long t0 = wall_clock64();
     unsigned long long gr;
@@ -2070,6 +2086,27 @@ __device__ __forceinline__ void head_receive(KParams& p, float* lds, int g, unsi
     lds[L_YS + threadIdx.x] = __uint_as_float((unsigned)gr);
   }
   __syncthreads();
+}
+// The layer-mix weights (w0, w1) of the head hand-off, polled by lanes 0 and 1 of the calling
+// wave and broadcast to it.
+__device__ __forceinline__ float2 head_mix_weights(KParams& p, int g, unsigned long long htag) {
+  const int lane = lane_id();
+  unsigned long long gr = 0ull;
+  if (lane < 2) {
+    const g_u64* src = (const g_u64*)(p.hbuf + 2 * ((size_t)g * HB_FLOATS + HB_MIX + lane));
+    const unsigned long long t0 = wall_clock64();
+    while (((gr = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != htag) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > BARRIER_TIMEOUT_TICKS ||
+          (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR)) {
+        raise_err(p, ERR_TIMEOUT);
+        gr = 0;
+        break;
+      }
+    }
+  }
+  return make_float2(__uint_as_float((unsigned)__shfl((int)(unsigned)gr, 0, 64)),
+                     __uint_as_float((unsigned)__shfl((int)(unsigned)gr, 1, 64)));
 }
 
 // Layer split, iteration 3: workgroup (tile, 1) hands its normalised layer-1 rows (S_E layer 1,
@@ -2157,9 +2194,9 @@ __device__ __noinline__ void head_iteration(KParams&, float*, float*, int g, int
     HSTAMP(50);
     vrow_update(lds + L_W, scr, sbuf, yw);  // Y3 from S2
     HSTAMP(51);
-    graph_head(p, lds, scr, gi, gv, true, true);
+    graph_head(p, lds, scr, gi, gv, true, true, htag, g);  // (y and the aux features published inside)
     HSTAMP(52);
-    head_publish(p, lds, g, htag);
+    head_publish_part(p, lds, g, htag, true);
     HSTAMP(53);
   }
 }
@@ -2281,7 +2318,7 @@ __device__ __noinline__ void attention_q_tile(KParams&, float*, float*, const Gr
   __syncthreads();
   TSTAMP(39);
   QATS(2);
-  if (htag != 0ull) head_receive(p, lds, g, htag);
+  if (htag != 0ull) head_receive(p, lds, g, htag, true);  // (the layer-mix weights at the combine below)
   TSTAMP(40);
   QATS(3);
   {
@@ -2362,10 +2399,11 @@ __device__ __noinline__ void attention_q_tile(KParams&, float*, float*, const Gr
     const int lane = threadIdx.x;
     float bm = NEG_INF, bs = NEG_INF;
     int bi = 0x7fffffff, bc = 0;
+    const float2 mw = htag != 0ull ? head_mix_weights(p, g, htag) : make_float2(gs[0], gs[1]);
     if (lane < 16) {
       const int v = rows[lane];
       if (v >= 0) {
-        const float qq = gs[0] * ql[lane] + gs[1] * ql[16 + lane];
+        const float qq = mw.x * ql[lane] + mw.y * ql[16 + lane];
         stc(p.q + gi.node_off + v, qq);
         if (p.qspec != nullptr)  // this step's Q for the speculative workgroups (buffer = step & 1)
           stc(p.qspec + (size_t)(((const int*)(lds + L_MISC))[60] & 1) * p.qspec_n + gi.node_off + v, qq);
