@@ -250,6 +250,8 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *                     speculative workgroup 0's result before phase A picks; 0 grid barriers
  *   MD_SELF_SPEC      0: the speculative workgroups wait for phase A's early word instead of
  *                     tile 0's derivation of it (MD_DF=3)
+ *   MD_FP_SHORTCUT    0: every mutual-LMCC fixed point runs its confirmation round (default 1:
+ *                     a pruned partition certified by its spanning forests ends the fixed point)
  *   MD_PROF_ALL       md_profile_read returns every non-empty record row (the dataflow mode's
  *                     per-tile rows after the step records), not only the step records
  *   MD_MAX_CUS        use at most this many CUs (>= 8; default: all), e.g. for several ranks

@@ -152,7 +152,8 @@ struct md_ctx {
   bool abort_on = true;
   bool df_r0 = false;  // measured: no gain over the early-word prebuild alone
   bool df_self = true;  // MD_DF=3 (default): tiles derive phase A's pick (df_wait_rec)
-  bool self_spec = true;  // ... and publish it to the speculative workgroups (MD_SELF_SPEC=0: off)
+  bool self_spec = true;
+  bool fp_short = true;  // MD_FP_SHORTCUT=0: every fixed point runs its confirmation round  // ... and publish it to the speculative workgroups (MD_SELF_SPEC=0: off)
   DevBuf<unsigned long long> dfbuf;
   int df_mt = 0, df_n = 0;
   std::vector<char> df_graph;
@@ -217,6 +218,7 @@ constexpr int SPEC_MAX = 32;  // speculative workgroups per launch at most  // C
 
 Params make_params(md_ctx* c) {
   Params p{};
+  p.fp_short = c->fp_short ? 1 : 0;
   p.w = c->w.p;
   p.ginfo = c->ginfo.p;
   p.gvar = c->gvar.p;
@@ -747,6 +749,7 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_EARLY")) c->early_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_SPEC_ABORT")) c->abort_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_SELF_SPEC")) c->self_spec = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MD_FP_SHORTCUT")) c->fp_short = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_DF")) {
     c->df_on = std::atoi(v) != 0;
     c->df_r0 = std::atoi(v) == 2;  // MD_DF=2: with the prebuild from speculative workgroup 0's result

@@ -107,6 +107,18 @@ __device__ __forceinline__ void uf_unite(P par, int a, int b) {
   }
 }
 
+// uf_unite that reports whether it linked two trees (the edge is then a spanning-forest edge)
+template <class P>
+__device__ __forceinline__ bool uf_link(P par, int a, int b) {
+  while (true) {
+    a = uf_find(par, a);
+    b = uf_find(par, b);
+    if (a == b) return false;
+    if (a > b) { const int t = a; a = b; b = t; }
+    if (uf_cas(par, b, b, a) == b) return true;
+  }
+}
+
 // Union of the trees holding a and b, climbing both paths in lockstep (two independent LDS
 // loads per hop instead of two dependent find loops), path splitting on the way; stops when
 // the paths meet or after hooking root hi -> lo (a failed compare-and-swap re-reads).
@@ -304,6 +316,35 @@ __device__ __forceinline__ int2 block_sum2(int a, int b, int* tmp) {
   return r;
 }
 
+// Sums of four ints over the block (leading barrier only, as block_sum2).
+__device__ __forceinline__ int4 block_sum4(int a, int b, int c, int d, int* tmp) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+    c += __shfl_xor(c, o, 64);
+    d += __shfl_xor(d, o, 64);
+  }
+  __syncthreads();
+  lds_i32* t = (lds_i32*)tmp;
+  if (lane_id() == 0) {
+    t[4 * wave_id()] = a;
+    t[4 * wave_id() + 1] = b;
+    t[4 * wave_id() + 2] = c;
+    t[4 * wave_id() + 3] = d;
+  }
+  __syncthreads();
+  int4 r = make_int4(0, 0, 0, 0);
+#pragma unroll
+  for (int w = 0; w < NTHREADS / 64; ++w) {
+    r.x += t[4 * w];
+    r.y += t[4 * w + 1];
+    r.z += t[4 * w + 2];
+    r.w += t[4 * w + 3];
+  }
+  return r;
+}
+
 // ------------------------------------------------------------------ alive-edge list
 // LDS mode keeps the ids of the alive edges in a compact list (edges only die during a
 // rollout), so the per-step passes -- cover, unions, prune, degrees -- touch the alive edges
@@ -407,6 +448,16 @@ __device__ void compact_alive(const EnvView<GL>& E) {
 // `cover` >= 0: first cover that node (U/mvc_env.py:74-85) inside the first union pass -- its
 // alive edges become covered instead of being united -- and return the covered edge counts
 // per layer in cc[2].
+// Confirmation shortcut (LDS mode; MD_FP_SHORTCUT=0: off): a round whose partitions differ is
+// normally followed by one more union round, often only to confirm that the pruned partition
+// P = C0 ^ C1 is connected in both layers.  The union pass records which alive edges linked two
+// trees (a spanning forest F_l of each layer: |F_l| = n - #C_l); after the prune, F_l minus its
+// t_l pruned edges is a forest whose n - |F_l| + t_l pieces each lie inside one class of P, so
+// when #C_l + t_l == #P for both layers every class of P is connected in both layers by
+// surviving edges: P is the fixed point and no edge crosses it unpruned -- the same result the
+// next round would confirm.  #P counts the distinct (C0, C1) label pairs through an LDS hash
+// table in the parent arrays (free between the label pass and the next round), whose slots
+// then label P for the LMCC count.
 // Speculative workgroups (spec_loop): the fixed point of a request's candidate stops after a
 // round once the result cannot be used -- phase A's early word names another result of the same
 // request, or a later request is out -- so a workgroup stuck in a long cascade is free for the
@@ -427,6 +478,8 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
   int pruned0 = 0, pruned1 = 0;
   if (acc != nullptr && threadIdx.x == 0) acc[PA_CALLS] += 1;
   bool first = true, dirty = cover >= 0;  // dead entries in the alive list
+  bool skipped = false;                   // ended by the confirmation shortcut (labels: table slots in deg1)
+  const bool shortcut = !GL && kp().fp_short;
   unsigned long long ab_ew = 0ull, ab_ew2 = 0ull, ab_req = 0ull;  // thread 0: loaded during the previous round's prune
   while (true) {
     unsigned long long tp = wall_clock64();
@@ -449,7 +502,29 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
     }
     PACC(acc, PA_INIT, tp);
     int k0 = 0, k1 = 0;
-    if (first && cover >= 0) {
+    const bool cv = first && cover >= 0;
+    if constexpr (!GL) {
+      // the union pass over contiguous runs of the alive list (for_each_alive_runs), recording
+      // per list position whether the edge linked two trees (the other alive-list buffer is free
+      // until the final compaction)
+      const int na = E.hdr[0];
+      const lds_u16* al = E.hdr[2] ? E.al_other : E.al;
+      lds_u8* tf = (lds_u8*)(E.hdr[2] ? E.al : E.al_other);
+      const int chunk = (na + NTHREADS - 1) / NTHREADS;
+      const int i0 = min(na, (int)threadIdx.x * chunk), i1 = min(na, i0 + chunk);
+      for (int i = i0; i < i1; ++i) {
+        const int e = al[i];
+        if (E.st[e] != E_ALIVE) continue;
+        const int u = (int)E.u16[e], v = (int)E.v16[e];
+        if (cv && (u == cover || v == cover)) {
+          E.kill(e, E_COVERED);
+          if (e < E.e0) k0++; else k1++;
+        } else {
+          const bool lk = uf_link(e < E.e0 ? E.par0 : E.par1, u, v);
+          if (shortcut) tf[i] = lk ? 1 : 0;
+        }
+      }
+    } else if (cv) {
       for_each_alive_runs<GL>(E, [&](int e, int u, int v) {
         if (u == cover || v == cover) {
           E.kill(e, E_COVERED);
@@ -484,19 +559,30 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
       }
     }
     tp = wall_clock64();
-    int diff = 0;
+    int diff = 0, nr0 = 0, nr1 = 0;
     for (int x = threadIdx.x; x < n; x += NTHREADS) {
       const int r0 = uf_find(E.par0, x), r1 = uf_find(E.par1, x);
       uf_store(E.deg0, x, r0);
       uf_store(E.deg1, x, r1);
       diff |= (r0 != r1);
+      nr0 += r0 == x;  // components per layer (their roots)
+      nr1 += r1 == x;
     }
-    if (first && cover >= 0) {
-      // covered-edge counts and the partition test in one block exchange
-      // (per layer at most n - 1 < 2^16 covered edges; at most 512 threads with diff set)
-      const int2 c = block_sum2(k0, k1 + (diff ? 1 << 16 : 0), E.tmp);
+    int nc0 = 0, nc1 = 0;
+    if (cv) {
+      // covered-edge counts, the component counts and the partition test in one block exchange
+      // (per layer at most n - 1 < 2^16 covered edges and n < 2^16 roots; at most 512 threads
+      // with diff set)
+      const int4 c = block_sum4(k0, k1, nr0, nr1 + (diff ? 1 << 16 : 0), E.tmp);
       cc[0] = c.x;
-      cc[1] = c.y & 0xffff;
+      cc[1] = c.y;
+      nc0 = c.z;
+      nc1 = c.w & 0xffff;
+      diff = (c.w >> 16) != 0;
+    } else if (shortcut) {
+      const int2 c = block_sum2(nr0, nr1 + (diff ? 1 << 16 : 0), E.tmp);
+      nc0 = c.x;
+      nc1 = c.y & 0xffff;
       diff = (c.y >> 16) != 0;
     } else {
       diff = __syncthreads_or(diff);
@@ -510,37 +596,93 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
       if (dirty) compact_alive<GL>(E);
       break;
     }
-    int c0 = 0, c1 = 0;
+    int c0 = 0, c1 = 0, t0 = 0, t1 = 0;
     if constexpr (!GL) {
       if (ab != nullptr && threadIdx.x == 0) {  // (used at the next round's start)
         ab_ew = __hip_atomic_load((const g_u64*)ab->ew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ab_req = __hip_atomic_load((const g_u64*)ab->req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (ab->ew2 != nullptr) ab_ew2 = __hip_atomic_load((const g_u64*)ab->ew2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-    }
-    for_each_alive<GL>(E, [&](int e, int u, int v) {
-      auto other = e < E.e0 ? E.deg1 : E.deg0;  // layer-0 edges are pruned by layer-1 components
-      if (uf_load(other, u) != uf_load(other, v)) {
-        E.kill(e, E_PRUNED);
-        if (e < E.e0) c0++; else c1++;
+      // the prune pass (for_each_alive's order), counting the pruned spanning-forest edges
+      const int na = E.hdr[0];
+      const lds_u16* al = E.hdr[2] ? E.al_other : E.al;
+      const lds_u8* tf = (const lds_u8*)(E.hdr[2] ? E.al : E.al_other);
+      for (int i = threadIdx.x; i < na; i += NTHREADS) {
+        const int e = al[i];
+        if (E.st[e] != E_ALIVE) continue;
+        const int u = (int)E.u16[e], v = (int)E.v16[e];
+        auto other = e < E.e0 ? E.deg1 : E.deg0;  // layer-0 edges are pruned by layer-1 components
+        if (uf_load(other, u) != uf_load(other, v)) {
+          E.kill(e, E_PRUNED);
+          const int f = shortcut ? (int)tf[i] : 0;
+          if (e < E.e0) { c0++; t0 += f; } else { c1++; t1 += f; }
+        }
       }
-    });
-    const int2 c = block_sum2(c0, c1, E.tmp);
+    } else {
+      for_each_alive<GL>(E, [&](int e, int u, int v) {
+        auto other = e < E.e0 ? E.deg1 : E.deg0;
+        if (uf_load(other, u) != uf_load(other, v)) {
+          E.kill(e, E_PRUNED);
+          if (e < E.e0) c0++; else c1++;
+        }
+      });
+    }
+    const int4 c = block_sum4(c0, c1, t0, t1, E.tmp);
     pruned0 += c.x;
     pruned1 += c.y;
     dirty = true;
     PACC(acc, PA_PRUNE, tp);
+    if constexpr (!GL) {
+      // confirmation shortcut (see above): #C0 + t0 == #C1 + t1 is necessary; then count the
+      // classes of P = C0 ^ C1 (distinct label pairs) in a hash table over both parent arrays
+      if (shortcut && nc0 + c.z == nc1 + c.w) {
+        auto ht = E.par0;  // par0, par1: 2n words, contiguous (env_layout)
+        const unsigned hs = 2u * (unsigned)n;
+        for (int x = threadIdx.x; x < 2 * n; x += NTHREADS) uf_store(ht, x, -1);
+        __syncthreads();
+        int np = 0;
+        for (int x = threadIdx.x; x < n; x += NTHREADS) {
+          const int key = (int)(((unsigned)uf_load(E.deg0, x) << 16) | (unsigned)uf_load(E.deg1, x));
+          unsigned h = ((unsigned)key * 2654435761u) % hs;
+          while (true) {
+            const int old = uf_cas(ht, (int)h, -1, key);
+            if (old == -1) { np++; break; }
+            if (old == key) break;
+            h = h + 1u == hs ? 0u : h + 1u;
+          }
+          uf_store(E.deg1, x, (int)h);  // x's class of P: its table slot (only this thread reads deg1[x] here)
+        }
+        const int2 q = block_sum2(np, 0, E.tmp);
+        if (nc0 + c.z == q.x && nc1 + c.w == q.x) {
+          skipped = true;
+          compact_alive<GL>(E);
+          break;
+        }
+        __syncthreads();  // (the next round's init overwrites the table)
+      }
+    }
   }
   const unsigned long long tc = wall_clock64();
   pr[0] = pruned0;
   pr[1] = pruned1;
-  for (int x = threadIdx.x; x < n; x += NTHREADS) uf_store(E.par1, x, 0);
-  __syncthreads();
-  for (int x = threadIdx.x; x < n; x += NTHREADS)
-    if (!E.covered(x)) uf_add(E.par1, uf_load(E.deg0, x), 1);
-  __syncthreads();
   int best = 0;
-  for (int x = threadIdx.x; x < n; x += NTHREADS) best = max(best, uf_load(E.par1, x));
+  if (skipped) {
+    // LMCC over the classes of P: sizes by table slot (deg1), in the table's words
+    auto ht = E.par0;
+    for (int x = threadIdx.x; x < 2 * n; x += NTHREADS) uf_store(ht, x, 0);
+    __syncthreads();
+    for (int x = threadIdx.x; x < n; x += NTHREADS)
+      if (!E.covered(x)) uf_add(ht, uf_load(E.deg1, x), 1);
+    __syncthreads();
+    for (int x = threadIdx.x; x < 2 * n; x += NTHREADS) best = max(best, uf_load(ht, x));
+  } else {
+    for (int x = threadIdx.x; x < n; x += NTHREADS) uf_store(E.par1, x, 0);
+    __syncthreads();
+    for (int x = threadIdx.x; x < n; x += NTHREADS)
+      if (!E.covered(x)) uf_add(E.par1, uf_load(E.deg0, x), 1);
+    __syncthreads();
+    for (int x = threadIdx.x; x < n; x += NTHREADS) best = max(best, uf_load(E.par1, x));
+  }
   best = block_max_int(best, E.tmp);
   PACC(acc, PA_COUNT, tc);
   return best;
