@@ -489,3 +489,30 @@ def test_dataflow_mode_same_rollouts(monkeypatch, cost):
         for variant, runs in out.items():
             for df, seq, ranks in runs:
                 assert (seq, ranks) == (runs[0][1], runs[0][2]), (name, variant, df)
+
+
+def test_fixed_point_shortcut_same_rollouts(monkeypatch):
+    """MD_FP_SHORTCUT=0 (every mutual-LMCC fixed point runs its confirmation round) gives the
+    removal sequences and LMCC traces of the default shortcut (tests/test_fixed_point_shortcut.py
+    checks the certificate itself on the CPU): single-graph launches (phase A, speculative
+    workgroups, dataflow mode) and a 24-graph queue-mode launch (environment items)."""
+    from mdcommunity_amd import gmm
+    w = engine.load_weights(engine.DEFAULT_UNIT)
+    singles = [load_golden(k) for k in ("gmm200_s7", "er100", "gmm1000_s0", "er300_dense")]
+    batch = [(1000,) + gmm.gmm_pair(1000, seed=s) for s in range(24)]
+    out = {}
+    for fs in ("0", "1"):
+        monkeypatch.setenv("MD_FP_SHORTCUT", fs)
+        e = _lib.Engine(w)
+        res = []
+        for z in singles:
+            e.load_graphs([(int(z["n_nodes"]), z["edges0"], z["edges1"])])
+            e.reset()
+            seq, ranks = e.rollout()[0]
+            res.append((seq.tolist(), ranks.tolist()))
+        e.load_graphs(batch)
+        e.reset()
+        res += [(s.tolist(), r.tolist()) for s, r in e.rollout()]
+        e.close()
+        out[fs] = res
+    assert out["0"] == out["1"]
