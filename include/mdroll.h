@@ -99,6 +99,16 @@ md_status md_load_graphs(md_ctx* ctx, int n_graphs, const int32_t* n_nodes,
  * LMCC size = Graph_test.max_rank (U/graph.py:80-84). */
 md_status md_reset(md_ctx* ctx, int32_t* max_rank_out);
 
+/* md_reset with MvcEnv.s0's prune deferred: the state is cleared now, and the initial
+ * mutual-LMCC prune runs as the first environment step of the next md_rollout, inside the same
+ * launch (every rollout kernel starts with an environment step; no separate s0 launch and host
+ * round trip).  Only md_rollout may follow; md_max_rank reads max_rank after it. */
+md_status md_reset_deferred(md_ctx* ctx);
+
+/* Graph_test.max_rank of every loaded graph as of the last launch (after md_reset, or after the
+ * md_rollout that followed md_reset_deferred): max_rank_out[g]. */
+md_status md_max_rank(md_ctx* ctx, int32_t* max_rank_out);
+
 /* One Q evaluation of the current state of every graph (Predict, U/MultiDismantler_torch.py:263-302).
  * q_out (may be NULL): sum(n_nodes) floats, graph-major; non-live nodes get -1073741823.5.
  * argmax/n_tie/top_gap (may be NULL): per graph, arg-max node (-1 if terminal), number of
@@ -252,6 +262,8 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *                     tile 0's derivation of it (MD_DF=3)
  *   MD_FP_SHORTCUT    0: every mutual-LMCC fixed point runs its confirmation round (default 1:
  *                     a pruned partition certified by its spanning forests ends the fixed point)
+ *   MD_FIRST_REQ      0: no speculative request at a rollout's first environment step (default
+ *                     1: candidates ranked by residual degree, as no prediction exists yet)
  *   MD_PROF_ALL       md_profile_read returns every non-empty record row (the dataflow mode's
  *                     per-tile rows after the step records), not only the step records
  *   MD_MAX_CUS        use at most this many CUs (>= 8; default: all), e.g. for several ranks

@@ -23,6 +23,7 @@ STATUS_NAMES = {1: "MD_EINVAL", 2: "MD_EHIP", 3: "MD_EOOM", 4: "MD_ESTATE", 5: "
 PROF_SLOTS = 96  # MD_PROF_SLOTS in include/mdroll.h
 
 EXPORTS = ("md_create", "md_destroy", "md_last_error", "md_set_weights", "md_load_graphs", "md_reset",
+           "md_reset_deferred", "md_max_rank",
            "md_predict", "md_step", "md_rollout", "md_rollout_trace", "md_get_state", "md_set_state",
            "md_set_team_size", "md_set_tie_argsort", "md_last_timing", "md_profile", "md_profile_read",
            "md_version", "md_device_count", "md_spec_stats", "md_gmm_last_error", "md_gmm_nodes", "md_gmm_links")
@@ -62,6 +63,8 @@ def load_library(path=LIB_PATH):
         "md_set_weights": (ctypes.c_int, [vp, _f32p, ctypes.c_size_t]),
         "md_load_graphs": (ctypes.c_int, [vp, ctypes.c_int, _i32p, _i64p, _i32p, _i64p, _i32p, _f32p]),
         "md_reset": (ctypes.c_int, [vp, _i32p]),
+        "md_reset_deferred": (ctypes.c_int, [vp]),
+        "md_max_rank": (ctypes.c_int, [vp, _i32p]),
         "md_predict": (ctypes.c_int, [vp, _f32p, _i32p, _i32p, _f32p]),
         "md_step": (ctypes.c_int, [vp, _i32p, _i32p, _u8p]),
         "md_rollout": (ctypes.c_int, [vp, ctypes.c_int, _i32p, _i32p, _i32p, SELECT_CB_ADDR, vp]),
@@ -191,6 +194,16 @@ class Engine:
     def reset(self):
         mr = np.zeros(len(self.n_nodes), np.int32)
         self._check(self.lib.md_reset(self.h, _ptr(mr, _i32p)))
+        return mr
+
+    def reset_deferred(self):
+        """reset() with MvcEnv.s0's prune run as the first environment step of the next
+        rollout() (one launch, no separate s0 launch); max_rank() after that rollout."""
+        self._check(self.lib.md_reset_deferred(self.h))
+
+    def max_rank(self):
+        mr = np.zeros(len(self.n_nodes), np.int32)
+        self._check(self.lib.md_max_rank(self.h, _ptr(mr, _i32p)))
         return mr
 
     def predict(self):

@@ -153,7 +153,8 @@ struct md_ctx {
   bool df_r0 = false;  // measured: no gain over the early-word prebuild alone
   bool df_self = true;  // MD_DF=3 (default): tiles derive phase A's pick (df_wait_rec)
   bool self_spec = true;
-  bool fp_short = true;  // MD_FP_SHORTCUT=0: every fixed point runs its confirmation round  // ... and publish it to the speculative workgroups (MD_SELF_SPEC=0: off)
+  bool fp_short = true;  // MD_FP_SHORTCUT=0: every fixed point runs its confirmation round
+  bool first_req = true;  // MD_FIRST_REQ=0: no speculative request at a rollout's first step  // ... and publish it to the speculative workgroups (MD_SELF_SPEC=0: off)
   DevBuf<unsigned long long> dfbuf;
   int df_mt = 0, df_n = 0;
   std::vector<char> df_graph;
@@ -219,6 +220,7 @@ constexpr int SPEC_MAX = 32;  // speculative workgroups per launch at most  // C
 Params make_params(md_ctx* c) {
   Params p{};
   p.fp_short = c->fp_short ? 1 : 0;
+  p.first_req = c->first_req ? 1 : 0;
   p.w = c->w.p;
   p.ginfo = c->ginfo.p;
   p.gvar = c->gvar.p;
@@ -750,6 +752,7 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_SPEC_ABORT")) c->abort_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_SELF_SPEC")) c->self_spec = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_FP_SHORTCUT")) c->fp_short = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MD_FIRST_REQ")) c->first_req = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_DF")) {
     c->df_on = std::atoi(v) != 0;
     c->df_r0 = std::atoi(v) == 2;  // MD_DF=2: with the prebuild from speculative workgroup 0's result
@@ -1089,6 +1092,38 @@ md_status md_reset(md_ctx* c, int32_t* max_rank_out) {
   if (st != MD_OK) return st;
   if (max_rank_out)
     for (int g = 0; g < c->ng; ++g) max_rank_out[g] = c->hvar[g].max_rank;
+  return MD_OK;
+}
+
+md_status md_reset_deferred(md_ctx* c) {
+  if (!c) return MD_EINVAL;
+  if (c->ng == 0) return fail(c, MD_ESTATE, "no graphs loaded");
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<int> gl(c->ng);
+  for (int g = 0; g < c->ng; ++g) gl[g] = g;
+  HIPCHK(c, hipMemcpyAsync(c->glist.p, gl.data(), sizeof(int) * gl.size(), hipMemcpyHostToDevice, c->stream));
+  Params p = make_params(c);
+  p.nglist = c->ng;
+  HIPCHK(c, launch_reset(p, c->stream));
+  c->last_ms = 0.0;
+  c->last_launches = 0;
+  // the host view md_rollout starts from (it pushes it to the device): as md_reset_kernel left
+  // the GraphVar, with the edge counts as alive counts (a graph with edges in both layers runs;
+  // its first environment step, s0 not done, prunes and recomputes them)
+  for (int g = 0; g < c->ng; ++g) {
+    GraphVar v = {};
+    v.status = ST_RUN;
+    v.argmax = -1;
+    v.alive[0] = c->hinfo[g].e[0];
+    v.alive[1] = c->hinfo[g].e[1];
+    c->hvar[g] = v;
+  }
+  return MD_OK;
+}
+
+md_status md_max_rank(md_ctx* c, int32_t* max_rank_out) {
+  if (!c || !max_rank_out) return MD_EINVAL;
+  for (int g = 0; g < c->ng; ++g) max_rank_out[g] = c->hvar[g].max_rank;
   return MD_OK;
 }
 

@@ -1349,7 +1349,21 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
   }
   MD_PROF_A(14);
   QENV(3);
-  if (p.n_spec > 0 && !err && gv.alive[0] > 0 && gv.alive[1] > 0 && ((const volatile int*)(lds_base + L_MISC))[5]) {
+  // a rollout's first environment step (no action, no prediction yet) asks too, with the
+  // candidates ranked by residual degree (both layers) instead of the previous Q: the first
+  // pick is a hub (rank 1-2 by degree on the GMM seeds), so step 1 needs no fixed point of its
+  // own (MD_FIRST_REQ=0: off)
+  const bool first_req = !GL && p.first_req && p.n_spec > 0 && p.run_mode == RUN_ROLLOUT && pend_n == 0 &&
+                         p.qspec != nullptr && !((const volatile int*)(lds_base + L_MISC))[5];
+  if (p.n_spec > 0 && !err && gv.alive[0] > 0 && gv.alive[1] > 0 &&
+      (((const volatile int*)(lds_base + L_MISC))[5] || first_req)) {
+    if constexpr (!GL) {
+      if (first_req) {  // the ranking keys where the speculative workgroups read Q(t - 1)
+        const int ps = ((const volatile int*)(lds_base + L_MISC))[60];
+        float* qs = p.qspec + (size_t)((ps - 1) & 1) * p.qspec_n + gi.node_off;
+        for (int x = threadIdx.x; x < n; x += NTHREADS) stc(qs + x, (float)(uf_load(E.deg0, x) + uf_load(E.deg1, x)));
+      }
+    }
     // the state after this step is in HBM once every store has drained: ask the speculative
     // workgroups for the next step's fixed point of the likely next removals (before the
     // first-layer table, which they do not read)

@@ -516,3 +516,28 @@ def test_fixed_point_shortcut_same_rollouts(monkeypatch):
         e.close()
         out[fs] = res
     assert out["0"] == out["1"]
+
+
+def test_deferred_reset_same_rollouts():
+    """md_reset_deferred (MvcEnv.s0's prune as the rollout launch's first environment step, the
+    bench's path) gives the removal sequences, LMCC traces and max_rank of md_reset + md_rollout:
+    single-graph launches (dataflow mode) and a 24-graph queue-mode launch, twice each (the
+    deferred reset after a finished rollout)."""
+    from mdcommunity_amd import gmm
+    w = engine.load_weights(engine.DEFAULT_UNIT)
+    singles = [load_golden(k) for k in ("gmm200_s7", "er100", "gmm1000_s0")]
+    sets = [[(int(z["n_nodes"]), z["edges0"], z["edges1"])] for z in singles]
+    sets.append([(1000,) + gmm.gmm_pair(1000, seed=s) for s in range(24)])
+    e = _lib.Engine(w)
+    try:
+        for graphs in sets:
+            e.load_graphs(graphs)
+            mr = e.reset().copy()
+            ref = [(s.tolist(), r.tolist()) for s, r in e.rollout()]
+            for _ in range(2):
+                e.reset_deferred()
+                got = [(s.tolist(), r.tolist()) for s, r in e.rollout()]
+                assert got == ref
+                assert np.array_equal(e.max_rank(), mr)
+    finally:
+        e.close()
