@@ -94,9 +94,10 @@ constexpr int L_TOTAL = L_SCR + S_END;      // floats of dynamic LDS per workgro
 // reads are done, E aliases M, the attention features F the dead X, the hidden layer the
 // dead E, and the gather stages its neighbour rows in P and X before it writes them.  The
 // first tile keeps its lists at S_NBH, the second at P2_NB1.
-constexpr int P2_P = 0;                         // [2][2][64][17] gathered neighbour sums
-constexpr int P2_X = 2 * 2 * 64 * LDT;          // [2][2][64][17] own embedding
-constexpr int P2_M = 0;                         // [2][2][128][17] [P.P1 | X.P2]
+constexpr int P2_LD = 16;                      // P / X / M blocks: K-rows of 16 rows, rotated (p2o)
+constexpr int P2_P = 0;                         // [2][2][64][16] gathered neighbour sums
+constexpr int P2_X = 2 * 2 * 64 * LDT;          // [2][2][64][16] own embedding (F's offset)
+constexpr int P2_M = 0;                         // [2][2][128][16] [P.P1 | X.P2]
 constexpr int P2_E = 0;                         // [2][2][64][17] new embedding / attention output
 constexpr int P2_F = P2_X;                      // [2][2][64][17] tanh features / Q-head input
 constexpr int P2_HID = 0;                       // [2][32][33]
@@ -112,6 +113,25 @@ static_assert(P2_FLAG + 16 == P2_NB1 && 2 * P2_X <= P2_ROW, "paired-tile scratch
 static_assert(2 * STG2_ROWS * 64 <= P2_ROW, "paired gather staging below the row ids");
 static_assert(2 * 32 * 33 <= P2_X, "paired hidden layer inside the E region");
 __device__ __forceinline__ int p2b(int l, int rb, int K) { return (l * 2 + rb) * K * LDT; }
+// The update's operand blocks P, X and M are [K][16] with K-row k holding its 16 rows rotated
+// by 5 * (k >> 1) (p2m block bases, p2o elements): the MFMA A-operand reads (a wave half reads
+// K-rows k, k + 1 for k even, rows 0..15) then cover all 32 banks of ds_read_b32, where [k][17]
+// put row 15 of k + 1 on row 0's bank (2-way on every A read); the gather and MFMA D writes
+// conflict no more than with [k][17].  E and F keep [k][17] (their row-wise and column-wise
+// accesses would pay a rotated offset per element).
+__device__ __forceinline__ int p2m(int l, int rb, int K) { return (l * 2 + rb) * K * P2_LD; }
+__device__ __forceinline__ int p2o(int k, int row) { return k * P2_LD + ((row + 5 * (k >> 1)) & 15); }
+// A-operand offsets of a lane (ak = lane >> 4, ar = lane & 15): p2o(4 * s + ak, ar) is
+// 64 * s + ro[s & 7] (the rotation 5 * (2 * s + (ak >> 1)) repeats every 8 k-steps), so the
+// reads of every k-step take an immediate offset from one of 8 lane registers.
+struct P2Rot {
+  int ro[8];
+  __device__ __forceinline__ P2Rot(int ak, int ar) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ro[q] = ak * P2_LD + ((ar + 10 * q + 5 * (ak >> 1)) & 15);
+  }
+  __device__ __forceinline__ int operator()(int s) const { return 64 * s + ro[s & 7]; }
+};
 // phase A uses [L_W, L_TOTAL) (weights are reloaded afterwards)
 constexpr int A_WORDS = L_TOTAL - L_W;
 constexpr int A_TMP_WORDS = 1024;
@@ -519,6 +539,18 @@ __device__ __forceinline__ float col_sum16(const float* a, int nv) {
   float v[TILE];
 #pragma unroll
   for (int r = 0; r < TILE; ++r) v[r] = a[r];
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < TILE; ++r)
+    if (r < nv) s = s + v[r];
+  return s;
+}
+// col_sum16 of K-row k of a rotated block (rows read at their rotated positions, summed in
+// row order).
+__device__ __forceinline__ float col_sum16_p2(const float* blk, int k, int nv) {
+  float v[TILE];
+#pragma unroll
+  for (int r = 0; r < TILE; ++r) v[r] = blk[p2o(k, r)];
   float s = 0.f;
 #pragma unroll
   for (int r = 0; r < TILE; ++r)
@@ -3045,16 +3077,16 @@ __device__ __noinline__ void gather_pair(KParams&, const GraphInfo gi, int it) {
   const int c = 4 * qd;
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb) {
-    float* atp = scr + P2_P + p2b(l, rb, 64);
-    float* atx = scr + P2_X + p2b(l, rb, 64);
-    atp[(c + 0) * LDT + r] = acc[rb].x;
-    atp[(c + 1) * LDT + r] = acc[rb].y;
-    atp[(c + 2) * LDT + r] = acc[rb].z;
-    atp[(c + 3) * LDT + r] = acc[rb].w;
-    atx[(c + 0) * LDT + r] = own[rb].x;
-    atx[(c + 1) * LDT + r] = own[rb].y;
-    atx[(c + 2) * LDT + r] = own[rb].z;
-    atx[(c + 3) * LDT + r] = own[rb].w;
+    float* atp = scr + P2_P + p2m(l, rb, 64);
+    float* atx = scr + P2_X + p2m(l, rb, 64);
+    atp[p2o(c + 0, r)] = acc[rb].x;
+    atp[p2o(c + 1, r)] = acc[rb].y;
+    atp[p2o(c + 2, r)] = acc[rb].z;
+    atp[p2o(c + 3, r)] = acc[rb].w;
+    atx[p2o(c + 0, r)] = own[rb].x;
+    atx[p2o(c + 1, r)] = own[rb].y;
+    atx[p2o(c + 2, r)] = own[rb].z;
+    atx[p2o(c + 3, r)] = own[rb].w;
   }
 }
 
@@ -3127,17 +3159,17 @@ __device__ __noinline__ void gather_pair_csr(KParams&, const GraphInfo gi, int i
         }
       }
     }
-    float* atp = scr + P2_P + p2b(l, rb, 64);
-    float* atx = scr + P2_X + p2b(l, rb, 64);
+    float* atp = scr + P2_P + p2m(l, rb, 64);
+    float* atx = scr + P2_X + p2m(l, rb, 64);
     const int c = 4 * qd;
-    atp[(c + 0) * LDT + r] = acc.x;
-    atp[(c + 1) * LDT + r] = acc.y;
-    atp[(c + 2) * LDT + r] = acc.z;
-    atp[(c + 3) * LDT + r] = acc.w;
-    atx[(c + 0) * LDT + r] = own.x;
-    atx[(c + 1) * LDT + r] = own.y;
-    atx[(c + 2) * LDT + r] = own.z;
-    atx[(c + 3) * LDT + r] = own.w;
+    atp[p2o(c + 0, r)] = acc.x;
+    atp[p2o(c + 1, r)] = acc.y;
+    atp[p2o(c + 2, r)] = acc.z;
+    atp[p2o(c + 3, r)] = acc.w;
+    atx[p2o(c + 0, r)] = own.x;
+    atx[p2o(c + 1, r)] = own.y;
+    atx[p2o(c + 2, r)] = own.z;
+    atx[p2o(c + 3, r)] = own.w;
   }
 }
 
@@ -3149,6 +3181,7 @@ __device__ __noinline__ void update_pair() {
 
   const int w = wave_id(), l = w >> 2, cb = w & 3, lane = lane_id();
   const int ar = lane & 15, ak = lane >> 4;
+  const P2Rot rot(ak, ar);
   const float* p1 = wi + W_IP1 + cb * 16 * 64;
   const float* p2 = wi + W_IP2 + cb * 16 * 64;
   const float* p3 = wi + W_IP3 + cb * 32 * 64;
@@ -3160,8 +3193,8 @@ __device__ __noinline__ void update_pair() {
     for (int s = 0; s < 16; ++s) {
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) {
-        xa[rb][s] = scr[P2_P + p2b(l, rb, 64) + (4 * s + ak) * LDT + ar];
-        xb[rb][s] = scr[P2_X + p2b(l, rb, 64) + (4 * s + ak) * LDT + ar];
+        xa[rb][s] = scr[P2_P + p2m(l, rb, 64) + rot(s)];
+        xb[rb][s] = scr[P2_X + p2m(l, rb, 64) + rot(s)];
       }
       wa[s] = p1[s * 64 + lane];
       wb[s] = p2[s * 64 + lane];
@@ -3192,11 +3225,11 @@ __device__ __noinline__ void update_pair() {
   __syncthreads();  // every P / X read done: M overwrites them
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb) {
-    float* atm = scr + P2_M + p2b(l, rb, 128);
+    float* atm = scr + P2_M + p2m(l, rb, 128);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      atm[col * LDT + 4 * ak + r] = a1[rb][r];
-      atm[(64 + col) * LDT + 4 * ak + r] = a2[rb][r];
+      atm[p2o(col, 4 * ak + r)] = a1[rb][r];
+      atm[p2o(64 + col, 4 * ak + r)] = a2[rb][r];
     }
   }
   __syncthreads();
@@ -3206,7 +3239,7 @@ __device__ __noinline__ void update_pair() {
 #pragma unroll
     for (int s = 0; s < 32; ++s) {
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb) xm[rb][s] = scr[P2_M + p2b(l, rb, 128) + (4 * s + ak) * LDT + ar];
+      for (int rb = 0; rb < 2; ++rb) xm[rb][s] = scr[P2_M + p2m(l, rb, 128) + rot(s)];
       wc[s] = p3[s * 64 + lane];
     }
 #pragma unroll
@@ -3586,7 +3619,7 @@ __device__ __noinline__ void queue_pair(KParams&, float* lds, int g, int gl, int
   if (it == 1 && t < 256) {
     // S0 (first-layer input) partial sums before the update overwrites X
     const int b = t >> 7, l = (t >> 6) & 1, c = t & 63;
-    const float s_old = col_sum16(scr + P2_X + p2b(l, b, 64) + c * LDT, tile_rows_valid(rows + 16 * b));
+    const float s_old = col_sum16_p2(scr + P2_X + p2m(l, b, 64), c, tile_rows_valid(rows + 16 * b));
     stc(p.spart + (size_t)(gi.tile_off + j + b) * 384 + l * 64 + c, s_old);
   }
   QTS(2);
