@@ -102,7 +102,9 @@ md_status md_reset(md_ctx* ctx, int32_t* max_rank_out);
 /* md_reset with MvcEnv.s0's prune deferred: the state is cleared now, and the initial
  * mutual-LMCC prune runs as the first environment step of the next md_rollout, inside the same
  * launch (every rollout kernel starts with an environment step; no separate s0 launch and host
- * round trip).  Only md_rollout may follow; md_max_rank reads max_rank after it. */
+ * round trip).  Any other call that reads or changes the state (md_predict, md_step,
+ * md_get_state, md_set_state, md_max_rank) first runs that prune exactly as md_reset does, so an
+ * action is never applied before it; md_max_rank after the md_rollout reads max_rank. */
 md_status md_reset_deferred(md_ctx* ctx);
 
 /* Graph_test.max_rank of every loaded graph as of the last launch (after md_reset, or after the

@@ -40,6 +40,13 @@ namespace {
 
 constexpr double QMASK = -(2147483647.0 / 2.0);  // U/MultiDismantler_torch.py:60
 
+// MD_TRACE=1 (diagnostics): every device allocation and every kernel launch to stderr, flushed,
+// so a GPU memory-fault report (its faulting address) can be mapped to a buffer and a launch.
+bool trace_on() {
+  static const bool on = std::getenv("MD_TRACE") != nullptr && std::atoi(std::getenv("MD_TRACE")) != 0;
+  return on;
+}
+
 template <class T>
 struct DevBuf {
   T* p = nullptr;
@@ -48,7 +55,11 @@ struct DevBuf {
     release();
     n = count;
     if (count == 0) return hipSuccess;
-    return hipMalloc((void**)&p, count * sizeof(T));
+    const hipError_t e = hipMalloc((void**)&p, count * sizeof(T));
+    if (trace_on())
+      std::fprintf(stderr, "md trace: alloc %p .. %p (%zu B)\n", (void*)p, (void*)((char*)p + count * sizeof(T)),
+                   count * sizeof(T));
+    return e;
   }
   void release() {
     if (p) (void)hipFree(p);
@@ -68,7 +79,11 @@ struct HostBuf {
     hipError_t e = hipHostMalloc((void**)&h, count * sizeof(T), hipHostMallocMapped | hipHostMallocCoherent);
     if (e != hipSuccess) return e;
     std::memset(h, 0, count * sizeof(T));
-    return hipHostGetDevicePointer((void**)&d, h, 0);
+    e = hipHostGetDevicePointer((void**)&d, h, 0);
+    if (trace_on())
+      std::fprintf(stderr, "md trace: host alloc %p .. %p (%zu B)\n", (void*)d, (void*)((char*)d + count * sizeof(T)),
+                   count * sizeof(T));
+    return e;
   }
   void release() {
     if (h) (void)hipHostFree(h);
@@ -113,7 +128,8 @@ struct md_ctx {
   DevBuf<float> H[2][2], h0tab[2], q, spart, apart, ybuf, hbuf, tr_q, node_w;
   DevBuf<unsigned long long> xbuf;
   DevBuf<int> nbc;  // neighbour-list cache slots (tiles of the largest launch)
-  int nbc_slots = 0, nbc_gstride = 0;
+  int nbc_slots = 0;
+  DevBuf<int> gtoff;  // per launch graph slot: first tile within the launch (queue-mode cache slots)
   int max_tiles = 0;  // tiles of the largest loaded graph
   DevBuf<unsigned long long> qslot;  // queue-mode work items
   DevBuf<int> qg;                    // queue-mode per-graph stage counters
@@ -128,9 +144,9 @@ struct md_ctx {
   int spec_n = 32;
   unsigned launch_seq = 0;
   // host selection hand-shake
-  int host_mode = 1;
+  int host_mode = 1;  // 1: ties / multi-node steps are answered inside the launch (MD_HOST_HANDSHAKE)
   md_argsort_f64 tie_argsort = nullptr;  // numpy's float64 argsort (md_set_tie_argsort), else the callback
-  int poll_us = 0;    // host poll interval while serving (MD_POLL_US)  // 1: ties / multi-node steps are answered inside the launch (MD_HOST_HANDSHAKE)
+  int poll_us = 0;    // host poll interval while serving (MD_POLL_US)
   HostBuf<unsigned> h_req, h_ans;
   HostBuf<int> h_nact, h_act;
   HostBuf<float> h_q;
@@ -138,6 +154,9 @@ struct md_ctx {
   HostBuf<unsigned> h_done;  // launch completion record {tag, error word} (kernel_exit)
   HostBuf<int> h_gvar;       // GraphVars of the last launch, copied by kernel_exit
   bool vars_stale = false;   // a launch ended without its completion record
+  // md_reset_deferred left MvcEnv.s0's prune to the next md_rollout's first environment step;
+  // any other call that reads or changes the state runs that prune first (finish_deferred_s0)
+  bool s0_pending = false;
   bool need_gscr = false;
   DevBuf<unsigned long long> prof;
   int prof_cap = 0;
@@ -152,9 +171,9 @@ struct md_ctx {
   bool abort_on = true;
   bool df_r0 = false;  // measured: no gain over the early-word prebuild alone
   bool df_self = true;  // MD_DF=3 (default): tiles derive phase A's pick (df_wait_rec)
-  bool self_spec = true;
+  bool self_spec = true;  // ... and tile 0 publishes it to the speculative workgroups (MD_SELF_SPEC=0: off)
   bool fp_short = true;  // MD_FP_SHORTCUT=0: every fixed point runs its confirmation round
-  bool first_req = true;  // MD_FIRST_REQ=0: no speculative request at a rollout's first step  // ... and publish it to the speculative workgroups (MD_SELF_SPEC=0: off)
+  bool first_req = true;  // MD_FIRST_REQ=0: no speculative request at a rollout's first step
   DevBuf<unsigned long long> dfbuf;
   int df_mt = 0, df_n = 0;
   std::vector<char> df_graph;
@@ -181,7 +200,7 @@ struct md_ctx {
       H[l][0].release(); H[l][1].release();
     }
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
-    tr_stat.release(); glist.release(); ctl.release(); tpart.release(); q.release(); spart.release();
+    tr_stat.release(); glist.release(); gtoff.release(); ctl.release(); tpart.release(); q.release(); spart.release();
     apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); nbc.release(); qslot.release(); qg.release(); tr_q.release(); node_w.release();
     sres.release(); qspec.release(); bars.release(); dfbuf.release();
     df_graph.clear();
@@ -215,7 +234,7 @@ md_status fail(md_ctx* c, md_status s, const char* fmt, ...) {
 // Control block layout (ints): [0] barrier counter, [1] error word (zeroed before each launch).
 constexpr int CTL_BAR = 0, CTL_ERR = 1, CTL_Q = 2, CTL_SPEC = 8, CTL_TEAM = 12, CTL_EXIT = 14, CTL_SELF = 32, CTL_PRE = 64,
               CTL_RING = 96, CTL_WORDS = 96 + 32 * 8;  // CTL_PRE and each ring's tickets on lines of their own
-constexpr int SPEC_MAX = 32;  // speculative workgroups per launch at most  // CTL_SPEC: u64 request word
+constexpr int SPEC_MAX = 32;  // speculative workgroups per launch at most (CTL_SPEC: the u64 request word)
 
 Params make_params(md_ctx* c) {
   Params p{};
@@ -266,7 +285,7 @@ Params make_params(md_ctx* c) {
   p.qring = (unsigned*)(c->ctl.p + CTL_RING);
   p.qrings = c->qxcd ? 8 : 1;
   p.qg = c->qg.p;
-  p.nbc_gstride = c->nbc_gstride;
+  p.gtoff = c->gtoff.p;
   p.glist = c->glist.p;
   p.prof = c->prof_cap > 0 ? c->prof.p : nullptr;
   p.prof_cap = c->prof_cap;
@@ -502,6 +521,12 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
   const bool df = run_mode == RUN_ROLLOUT && n_env == 1 && ngl == 1 && !team_env && c->dfbuf.p != nullptr &&
                   c->df_graph[gl[0]] && 2 * ((c->hinfo[gl[0]].n + TILE - 1) / TILE) <= grid - 2 && !(c->variant & 16);
   HIPCHK(c, hipMemcpyAsync(c->glist.p, gl, sizeof(int) * ngl, hipMemcpyHostToDevice, c->stream));
+  if (qmode) {
+    // queue-mode neighbour-list cache slots: each graph slot's tiles from its launch prefix
+    std::vector<int> to(ngl + 1, 0);
+    for (int i = 0; i < ngl; ++i) to[i + 1] = to[i] + (c->hinfo[gl[i]].n + TILE - 1) / TILE;
+    HIPCHK(c, hipMemcpyAsync(c->gtoff.p, to.data(), sizeof(int) * (ngl + 1), hipMemcpyHostToDevice, c->stream));
+  }
   {
     // per-launch clears in one dispatch: control words, barrier shards; graph-head hand-off
     // granules carry the step as their tag (stale tags from earlier launches must not match);
@@ -593,6 +618,9 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
     p.h_done = c->h_done.d;
     p.h_gvar = c->h_gvar.d;
   }
+  if (trace_on())
+    std::fprintf(stderr, "md trace: ctx %p launch %u run %d grid %d spec %d env %d df %d qmode %d graphs %d\n", (void*)c,
+                 p.launch_seq, run_mode, grid, n_spec, n_env, df ? 1 : 0, qmode ? 1 : 0, ngl);
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   HIPCHK(c, launch_rollout(p, c->wimg.p, grid + n_spec, c->stream));
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
@@ -648,6 +676,7 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
       std::fprintf(stderr, "md host: %d requests served in %.3f ms of a %.3f ms launch wait\n", n_served, 1e3 * serve_s,
                    1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t_launch).count());
   }
+  if (trace_on()) std::fprintf(stderr, "md trace: ctx %p launch %u done\n", (void*)c, p.launch_seq);
   int dev_err = 0;
   if (rec && __atomic_load_n(c->h_done.h, __ATOMIC_ACQUIRE) == p.launch_seq) {
     dev_err = (int)__atomic_load_n(c->h_done.h + 1, __ATOMIC_RELAXED);
@@ -778,10 +807,16 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
     return st;
   }
   *out = c;
+  if (trace_on())
+    std::fprintf(stderr, "md trace: create ctx %p df %d r0 %d self %d variant %d spec %d\n", (void*)c, c->df_on ? 1 : 0,
+                 c->df_r0 ? 1 : 0, c->df_self ? 1 : 0, c->variant, c->spec_n);
   return MD_OK;
 }
 
-void md_destroy(md_ctx* ctx) { delete ctx; }
+void md_destroy(md_ctx* ctx) {
+  if (trace_on()) std::fprintf(stderr, "md trace: destroy ctx %p\n", (void*)ctx);
+  delete ctx;
+}
 
 // Unit cost: the first-layer tables of every dmax up to the largest loaded graph's n - 1
 // (tables of dmax <= H0G_MAX_DM only: 2048 dmax values are 537 MB; larger dmax values are
@@ -974,16 +1009,18 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->hbuf.alloc((size_t)n_graphs * 144 * 2));
   HIPCHK(c, c->xbuf.alloc((size_t)XB_SLOTS * 2048));
   {
-    // cache slots: one per tile of the loaded graphs (queue mode addresses the graph's own
-    // tiles, tile_off + tile; the lock-step modes the launch's tile prefix index, which is
-    // below the launch's tile count)
-    long maxt = 1;
-    for (int g = 0; g < n_graphs; ++g) maxt = std::max<long>(maxt, (n_nodes[g] + TILE - 1) / TILE);
-    const long slots = (long)tt;
-    c->nbc_slots = (int)slots;
-    c->nbc_gstride = (int)maxt;
-    c->max_tiles = (int)maxt;
-    HIPCHK(c, c->nbc.alloc((size_t)std::max<long>(1, slots) * NBC_INTS));
+    // cache slots: every launch addresses its own tile prefix (the lock-step modes: the launch's
+    // tile index; queue mode: gtoff[graph slot] + tile), so the tiles of the QG_CAP largest
+    // graphs bound every launch -- not the whole loaded set
+    std::vector<long> nt(n_graphs);
+    for (int g = 0; g < n_graphs; ++g) nt[g] = (n_nodes[g] + TILE - 1) / TILE;
+    std::sort(nt.begin(), nt.end(), std::greater<long>());
+    long slots = 0;
+    for (int g = 0; g < std::min(n_graphs, QG_CAP); ++g) slots += nt[g];
+    c->nbc_slots = (int)std::min<long>(slots, INT32_MAX / NBC_INTS);
+    c->max_tiles = (int)std::max<long>(1, nt[0]);
+    HIPCHK(c, c->nbc.alloc((size_t)std::max(1, c->nbc_slots) * NBC_INTS));
+    HIPCHK(c, c->gtoff.alloc(QG_CAP + 1));
   }  // split tiles of a launch <= CUs / 2 <= XB_SLOTS
   HIPCHK(c, c->h_req.alloc((size_t)n_graphs));
   HIPCHK(c, c->h_ans.alloc((size_t)n_graphs));
@@ -1080,6 +1117,7 @@ md_status md_reset(md_ctx* c, int32_t* max_rank_out) {
   if (!c) return MD_EINVAL;
   if (c->ng == 0) return fail(c, MD_ESTATE, "no graphs loaded");
   HIPCHK(c, hipSetDevice(c->device));
+  c->s0_pending = false;
   std::vector<int> gl(c->ng);
   for (int g = 0; g < c->ng; ++g) gl[g] = g;
   HIPCHK(c, hipMemcpyAsync(c->glist.p, gl.data(), sizeof(int) * gl.size(), hipMemcpyHostToDevice, c->stream));
@@ -1118,11 +1156,31 @@ md_status md_reset_deferred(md_ctx* c) {
     v.alive[1] = c->hinfo[g].e[1];
     c->hvar[g] = v;
   }
+  c->s0_pending = true;
   return MD_OK;
 }
 
+namespace {
+// The s0 prune md_reset_deferred left pending, as md_reset runs it (one RUN_STEP launch over
+// every graph from the state md_reset_kernel left on the device): called by every entry point
+// except md_rollout (whose first environment step runs it) before it reads or changes the
+// state, so an action is never applied before the initial prune (U/mvc_env.py:52 then :74-87).
+md_status finish_deferred_s0(md_ctx* c) {
+  if (!c->s0_pending) return MD_OK;
+  c->s0_pending = false;
+  std::vector<int> gl(c->ng);
+  for (int g = 0; g < c->ng; ++g) gl[g] = g;
+  return launch(c, gl, RUN_STEP, 0);
+}
+}  // namespace
+
 md_status md_max_rank(md_ctx* c, int32_t* max_rank_out) {
   if (!c || !max_rank_out) return MD_EINVAL;
+  if (c->ng > 0) {
+    HIPCHK(c, hipSetDevice(c->device));
+    md_status st = finish_deferred_s0(c);
+    if (st != MD_OK) return st;
+  }
   for (int g = 0; g < c->ng; ++g) max_rank_out[g] = c->hvar[g].max_rank;
   return MD_OK;
 }
@@ -1131,6 +1189,10 @@ md_status md_predict(md_ctx* c, float* q_out, int32_t* argmax, int32_t* n_tie, f
   if (!c) return MD_EINVAL;
   if (c->ng == 0) return fail(c, MD_ESTATE, "no graphs loaded");
   HIPCHK(c, hipSetDevice(c->device));
+  {
+    md_status st0 = finish_deferred_s0(c);
+    if (st0 != MD_OK) return st0;
+  }
   std::vector<int> gl;
   for (int g = 0; g < c->ng; ++g) {
     GraphVar& v = c->hvar[g];
@@ -1163,6 +1225,10 @@ md_status md_step(md_ctx* c, const int32_t* actions, int32_t* lmcc_out, uint8_t*
   if (!c || !actions) return MD_EINVAL;
   if (c->ng == 0) return fail(c, MD_ESTATE, "no graphs loaded");
   HIPCHK(c, hipSetDevice(c->device));
+  {
+    md_status st0 = finish_deferred_s0(c);
+    if (st0 != MD_OK) return st0;
+  }
   std::vector<int> gl;
   for (int g = 0; g < c->ng; ++g) {
     const int a = actions[g];
@@ -1195,6 +1261,7 @@ md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, i
   if (!c || step < 1) return MD_EINVAL;
   if (c->ng == 0) return fail(c, MD_ESTATE, "no graphs loaded");
   HIPCHK(c, hipSetDevice(c->device));
+  c->s0_pending = false;  // the first environment step of this rollout runs the deferred s0 prune
   const int host_select = step > 1 ? 1 : 0;
   c->last_ms = 0.0;
   c->last_launches = 0;
@@ -1307,6 +1374,10 @@ md_status md_rollout_trace(md_ctx* c, int graph, int32_t* n_live, int32_t* m0, i
 md_status md_get_state(md_ctx* c, int graph, uint8_t* covered, uint8_t* removed0, uint8_t* removed1, int32_t* counters) {
   if (!c || graph < 0 || graph >= c->ng) return MD_EINVAL;
   HIPCHK(c, hipSetDevice(c->device));
+  {
+    md_status st0 = finish_deferred_s0(c);
+    if (st0 != MD_OK) return st0;
+  }
   const GraphInfo& gi = c->hinfo[graph];
   if (covered) HIPCHK(c, hipMemcpy(covered, c->covered.p + gi.node_off, gi.n, hipMemcpyDeviceToHost));
   uint8_t* outs[2] = {removed0, removed1};
@@ -1330,6 +1401,10 @@ md_status md_get_state(md_ctx* c, int graph, uint8_t* covered, uint8_t* removed0
 md_status md_set_state(md_ctx* c, int graph, const uint8_t* covered, const uint8_t* removed0, const uint8_t* removed1) {
   if (!c || graph < 0 || graph >= c->ng || !covered) return MD_EINVAL;
   HIPCHK(c, hipSetDevice(c->device));
+  {
+    md_status st0 = finish_deferred_s0(c);
+    if (st0 != MD_OK) return st0;
+  }
   const GraphInfo& gi = c->hinfo[graph];
   GraphVar& v = c->hvar[graph];
   std::vector<int> eu, ev;

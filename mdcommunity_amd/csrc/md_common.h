@@ -112,6 +112,8 @@ struct Params {
   int* nbc;                        // per launch tile slot: its alive neighbour lists (NBC_INTS ints), built at
                                    //   iteration 1, reloaded by iterations 2-3 of multi-tile workgroups
   int nbc_slots;
+  const int* gtoff;                // per launch graph slot: its first tile in the launch (prefix of the
+                                   //   slots' tile counts; queue-mode cache slot = gtoff[slot] + tile)
   unsigned long long* xbuf;        // layer split: per launch tile slot [2 layers][1024] E-row granules {tag, value}
   int* pend;                       // per node slot: host-queued actions
   int* tr_action;                  // per node slot: removal order
@@ -146,7 +148,6 @@ struct Params {
   int* err;                        // device error word (nonzero = failure code)
   unsigned long long* prof;        // optional phase timestamps of workgroup 0 (wall clock)
   int prof_cap;                    // steps of 16 timestamp slots available in prof
-  int nbc_gstride;                 // queue mode: cache slot = graph slot * nbc_gstride + tile
   int qmode;                       // 1: batch rollout through the device work queue (queue_loop)
   int qpair;                       // queue mode: a 2-tile item's tiles run jointly (queue_pair; MD_PAIR)
   int qpark;                       // queue mode: graphs left to the lock-step kernel at the tail (MD_QPARK)
@@ -187,8 +188,8 @@ struct Params {
   int df_mt;                       // tiles of the largest graph the buffer is sized for
   int df_n;                        // nodes of that graph
   int df_r0;                       // 1: tiles prebuild from speculative workgroup 0's result before phase A picks
-  int fp_short;
-  int first_req;                   // 1: a rollout's first step requests degree-ranked speculative results (env_step)                    // 1: mutual-LMCC fixed points end by the confirmation shortcut (mcc_fixed_point)
+  int fp_short;                    // 1: mutual-LMCC fixed points end by the confirmation shortcut (mcc_fixed_point)
+  int first_req;                   // 1: a rollout's first step requests degree-ranked speculative results (env_step)
   int df_self;                     // 1: tiles derive phase A's pick from the arg-max partials (df_wait_rec)
 };
 // dataflow buffer size (granules) for graphs of at most n nodes / mt tiles

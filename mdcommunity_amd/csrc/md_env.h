@@ -512,10 +512,26 @@ __device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long lo
       lds_u8* tf = (lds_u8*)(E.hdr[2] ? E.al : E.al_other);
       const int chunk = (na + NTHREADS - 1) / NTHREADS;
       const int i0 = min(na, (int)threadIdx.x * chunk), i1 = min(na, i0 + chunk);
+#ifdef MD_UNION_PIPE
+      // diagnostic variant (timing perturbation only): the next entry's id, state and endpoints
+      // loaded one step ahead
+      int e_n = i0 < i1 ? (int)al[i0] : 0;
+      int s_n = i0 < i1 ? (int)E.st[e_n] : 0, u_n = i0 < i1 ? (int)E.u16[e_n] : 0, v_n = i0 < i1 ? (int)E.v16[e_n] : 0;
+      for (int i = i0; i < i1; ++i) {
+        const int e = e_n, s = s_n, u = u_n, v = v_n;
+        if (i + 1 < i1) {
+          e_n = al[i + 1];
+          s_n = E.st[e_n];
+          u_n = E.u16[e_n];
+          v_n = E.v16[e_n];
+        }
+        if (s != E_ALIVE) continue;
+#else
       for (int i = i0; i < i1; ++i) {
         const int e = al[i];
         if (E.st[e] != E_ALIVE) continue;
         const int u = (int)E.u16[e], v = (int)E.v16[e];
+#endif
         if (cv && (u == cover || v == cover)) {
           E.kill(e, E_COVERED);
           if (e < E.e0) k0++; else k1++;

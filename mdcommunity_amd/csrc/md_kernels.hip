@@ -2665,7 +2665,7 @@ __device__ __noinline__ bool env_build_lists(KParams&, const GraphInfo gi, int g
   const EnvLayout Lo = env_layout(n, et);
   const EnvView<false> E = env_view<false>(p, gi, ia);
   const int nl = ((const GraphVar*)(lds + L_GV))->n_live, nt = (nl + TILE - 1) / TILE;
-  if (Lo.total + 3 * nl + 2 * nt + 8 > A_WORDS || gi.tile_off + nt > p.nbc_slots || nl <= 0) return false;
+  if (Lo.total + 3 * nl + 2 * nt + 8 > A_WORDS || p.gtoff[gl] + nt > p.nbc_slots || nl <= 0) return false;
   // scratch after the environment: node of each live position, per-position prefixes of the
   // CSR extent and of the alive count (nl + 1 each), per-tile alive totals of both layers
   int* pn = ia + Lo.total;
@@ -2673,7 +2673,7 @@ __device__ __noinline__ bool env_build_lists(KParams&, const GraphInfo gi, int g
   int* pd = px + nl + 1;
   int* tt = pd + nl + 1;
   int* tmp = E.tmp;
-  int* base_slot = p.nbc + (size_t)gi.tile_off * NBC_INTS;
+  int* base_slot = p.nbc + (size_t)p.gtoff[gl] * NBC_INTS;
   {
     // live positions (ascending ids, as the live list)
     const int chunk = (n + NTHREADS - 1) / NTHREADS;
@@ -2827,7 +2827,7 @@ __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int
       tqd = now_;                                                 \
     }                                                             \
   } while (0)
-  const int slot = p.ginfo[g].tile_off + j;  // neighbour-list cache slot: the graph's tile
+  const int slot = p.gtoff[gl] + j;  // neighbour-list cache slot: the graph's tile within the launch
   const bool cacheable = slot < p.nbc_slots && !(p.variant & 16);
   // iteration 1: the environment item built this step's lists when its flag says so (read in
   // the same round trip as the speculative reload)
@@ -3543,7 +3543,7 @@ __device__ __noinline__ void queue_pair(KParams&, float* lds, int g, int gl, int
     }                                                             \
   } while (0)
   const int t = threadIdx.x;
-  const int slot0 = p.ginfo[g].tile_off + j;  // neighbour-list cache slots: the graph's tiles
+  const int slot0 = p.gtoff[gl] + j;  // neighbour-list cache slots: the graph's tiles within the launch
   const int nbo[2] = {0, P2_NB1 - S_NBH};
   bool cacheable[2], want[2];
 #pragma unroll

@@ -541,3 +541,44 @@ def test_deferred_reset_same_rollouts():
                 assert np.array_equal(e.max_rank(), mr)
     finally:
         e.close()
+
+
+def test_deferred_reset_then_step_predict_state():
+    """After md_reset_deferred, md_step / md_predict / md_get_state / md_max_rank run the pending
+    s0 prune first (U/mvc_env.py:52 before :74-87): the state, LMCC, max_rank and Q equal those
+    after md_reset, on a single graph and on a 3-graph batch."""
+    w = engine.load_weights(engine.DEFAULT_UNIT)
+    singles = [load_golden(k) for k in ("gmm200_s7", "er100", "gmm1000_s0")]
+    sets = [[(int(z["n_nodes"]), z["edges0"], z["edges1"])] for z in singles[:1]]
+    sets.append([(int(z["n_nodes"]), z["edges0"], z["edges1"]) for z in singles])
+    e = _lib.Engine(w)
+    try:
+        for graphs in sets:
+            e.load_graphs(graphs)
+            ng = len(graphs)
+            mr = e.reset().copy()
+            q_ref = e.predict()[0].copy()
+            acts = np.array([int(np.argmax(q_ref[int(e.node_off[g]):int(e.node_off[g + 1])])) for g in range(ng)], np.int32)
+            lm_ref, term_ref = e.step(acts)
+            st_ref = [e.get_state(g) for g in range(ng)]
+            # md_step straight after the deferred reset
+            e.reset_deferred()
+            lm, term = e.step(acts)
+            assert np.array_equal(lm, lm_ref) and np.array_equal(term, term_ref)
+            for g in range(ng):
+                got = e.get_state(g)
+                for a, b in zip(got, st_ref[g]):
+                    assert np.array_equal(a, b)
+            assert np.array_equal(e.max_rank(), mr)
+            # md_predict / md_get_state / md_max_rank straight after the deferred reset
+            e.reset_deferred()
+            assert np.array_equal(e.predict()[0], q_ref)
+            e.reset_deferred()
+            s0_state = e.get_state(0)
+            e.reset()
+            for a, b in zip(s0_state, e.get_state(0)):
+                assert np.array_equal(a, b)
+            e.reset_deferred()
+            assert np.array_equal(e.max_rank(), mr)
+    finally:
+        e.close()
