@@ -78,6 +78,8 @@ def parse(argv=None):
     ap.add_argument("--batch-steps", type=int, default=2)
     ap.add_argument("--degree-steps", type=int, default=3, help="timed degree-cost rollouts (0: skip)")
     ap.add_argument("--real-steps", type=int, default=1, help="timed rollouts of the testReal-sized object (0: skip)")
+    ap.add_argument("--real-cases", default="degree,unit",
+                    help="cases of the testReal-sized object: degree (step 1), unit (stepRatio 0.01)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-step", action="store_true", help="skip the per-step-protocol comparison rollouts")
     ap.add_argument("--cpu-sample-seconds", type=float, default=12.0)
@@ -88,6 +90,8 @@ def parse(argv=None):
                     help="graphs of the C5 object (BASELINE configs[4]), strong-scaled: the same graphs at every "
                          "world size, split contiguously over the ranks (0: skip)")
     ap.add_argument("--c5-steps", type=int, default=1)
+    ap.add_argument("--c5-shard-graphs", type=int, default=512,
+                    help="world size 1: also time one rank's C5 shard at 8 GPUs (4096 / 8 graphs) alone; 0: skip")
     ap.add_argument("--rccl", action="store_true",
                     help="initialise torch.distributed over RCCL (backend nccl) even at world size 1, so the "
                          "collectives of the multi-GPU path run on the GPU")
@@ -392,6 +396,8 @@ def roofline(F, B, kernel_ms_per_step, launches_per_step, traffic):
     else:
         bound, achieved, peak, unit = "mfma", (Fs / t / 1e12 if t > 0 else 0.0), PEAK_FP32_TFLOPS, "TFLOP/s"
     per = max(1e-9, launches_per_step)
+    # one unit throughout: the bench step (== one launch for single-graph rollouts); the
+    # per-launch averages follow for the rocprof comparison
     return {
         "bound": bound,
         "achieved": achieved,
@@ -407,6 +413,12 @@ def roofline(F, B, kernel_ms_per_step, launches_per_step, traffic):
         "predictions_hbm_bound": int((tb >= tf).sum()),
         "predictions_mfma_bound": int((tf > tb).sum()),
         "roofline_ms_per_step": t_roof * 1e3,
+        "per": "bench step",
+        "algorithmic_flops_per_step": Fs,
+        "algorithmic_bytes_per_step": Bs,
+        "kernel_ms_per_step": kernel_ms_per_step,
+        "traffic_over_algorithmic_bytes": (traffic / Bs) if (traffic is not None and Bs > 0) else None,
+        "launches_per_step": launches_per_step,
         "algorithmic_flops_per_launch": Fs / per,
         "algorithmic_bytes_per_launch": Bs / per,
         "kernel_ms_per_launch": kernel_ms_per_step / per,
@@ -423,6 +435,23 @@ def load_traffic():
     if tj.get("src_hash") != kernel_src_hash():
         return None, f"stale (made from sources {tj.get('src_hash')}, built {kernel_src_hash()})"
     return tj, "measured by " + str(tj.get("source", "rocprofv3 PMC passes"))
+
+
+def apply_traffic(rl, tw, launches_per_step=1.0):
+    """Measured HBM traffic of one workload of traffic.json (`tw`: its main kernel's bytes per
+    launch, and for queue launches the tail launch's) as bytes per bench step, beside the
+    algorithmic bytes of the same step."""
+    if not tw:
+        return rl
+    q, tail = tw.get("hbm_bytes_per_launch"), tw.get("tail_hbm_bytes_per_launch")
+    extra = launches_per_step - 1.0
+    if q is not None and (extra < 0.5 or tail is not None):
+        rl["traffic"] = q + (extra * tail if extra >= 0.5 else 0.0)
+        b = rl.get("algorithmic_bytes_per_step") or 0.0
+        rl["traffic_over_algorithmic_bytes"] = rl["traffic"] / b if b > 0 else None
+    if tw.get("mfma_busy") is not None:
+        rl["mfma_busy"] = tw.get("mfma_busy")
+    return rl
 
 
 def golden_checks(seq_by_seed, audc_by_seed):
@@ -462,6 +491,7 @@ def degree_object(args, edges, make_engine):
     dt = time.perf_counter() - t0
     mr, outs = last
     seq, ranks = outs[0]
+    F, B = trace_work(eng, 1)
     eng.close()
     tw0, tw1 = sum(g.weights[0].values()), sum(g.weights[1].values())
     score = 0.0
@@ -473,6 +503,10 @@ def degree_object(args, edges, make_engine):
            "value": rem / dt, "unit": "removals/s", "steps": args.degree_steps,
            "ms_per_step": dt / args.degree_steps * 1e3, "kernel_ms_per_step": kms / args.degree_steps,
            "removals_per_step": rem / args.degree_steps, "score": score}
+    traffic, tnote = load_traffic()
+    out["roofline"] = apply_traffic(roofline(F, B, kms / args.degree_steps, nl / args.degree_steps, None),
+                                    (traffic or {}).get("degree"), nl / args.degree_steps)
+    out["roofline"]["traffic_note"] = tnote
     cp = os.path.join(ROOT, "tests", "golden", "cert_deg_gmm1000_s%d.npz" % args.seed)
     if z is not None:
         out.update(score_match=score == float(z["score"]),
@@ -500,9 +534,13 @@ def real_scale_object(args, make_engine, tmpdir):
     mgraph.ensure_degree_weights(g)
     out = {"workload": "testReal-shaped 2-layer multiplex N=%d (mdcommunity_amd.synth seed 0: heavy-tailed, "
                        "%d / %d edges, hubs ~1100), HBM environment" % (n, len(e0), len(e1))}
-    for key, cost, ckpt, step in (("degree_step1", _lib.MD_COST_DEGREE, engine.DEFAULT_DEGREE, 1),
-                                  ("unit_step_ratio_0.01", _lib.MD_COST_UNIT, engine.DEFAULT_UNIT_REAL,
-                                   max(int(0.01 * n), 1))):
+    traffic, tnote = load_traffic()
+    cases = [c.strip() for c in args.real_cases.split(",") if c.strip()]
+    for key, cost, ckpt, step, tkey in (("degree_step1", _lib.MD_COST_DEGREE, engine.DEFAULT_DEGREE, 1, "real_degree"),
+                                        ("unit_step_ratio_0.01", _lib.MD_COST_UNIT, engine.DEFAULT_UNIT_REAL,
+                                         max(int(0.01 * n), 1), "real_unit")):
+        if tkey.split("_")[1] not in cases:
+            continue
         eng = make_engine(engine.load_weights(ckpt), cost_mode=cost)
         eng.load_graphs([(n, e0, e1)], node_w=mgraph.node_weight_array([g]) if cost == _lib.MD_COST_DEGREE else None)
         eng.reset()
@@ -510,17 +548,25 @@ def real_scale_object(args, make_engine, tmpdir):
         t0 = time.perf_counter()
         kms = 0.0
         rem = 0
+        nl = 0
         for _ in range(max(1, args.real_steps)):
             mr = eng.reset()
             seq, ranks = eng.rollout(step=step)[0]
             kms += eng.last_timing()[0]
+            nl += eng.last_timing()[1]
             rem += len(seq)
         dt = time.perf_counter() - t0
+        F, B = trace_work(eng, 1)
         eng.close()
         k = max(1, args.real_steps)
         out[key] = {"value": rem / dt, "unit": "removals/s", "removals_per_rollout": rem // k, "step": step,
                     "ms_per_rollout": dt / k * 1e3, "kernel_ms_per_rollout": kms / k, "max_rank": int(mr[0]),
+                    "predictions_per_rollout": int(len(F)),
                     "audc": audc_of(ranks, mr[0], n) if cost == _lib.MD_COST_UNIT else None}
+        # one bench step = one rollout (MvcEnv.s0 by md_reset's own launch, outside the rollout
+        # launch and its roofline)
+        out[key]["roofline"] = apply_traffic(roofline(F, B, kms / k, nl / k, None), (traffic or {}).get(tkey), nl / k)
+        out[key]["roofline"]["traffic_note"] = tnote
     out["reference_note"] = ("the reference's committed homo_genetic_multiplex run (N=18222, unit cost, stepRatio 0): "
                              "2081 removals in 1582.6 s (results/unitcost/MultiDismantler_real/StepRatio_0.0000)")
     return out
@@ -745,6 +791,20 @@ def rank_main(args):
                   **c5)
         c5["scaling"] = "strong"
         c5["gather_complete"] = c5["graphs"] == args.c5_graphs
+        if world == 1 and 0 < args.c5_shard_graphs < args.c5_graphs:
+            # one rank's shard at 8 GPUs (the first 512 seeds) on this GPU alone: 8 x its rate over
+            # the 4096-graph rate predicts the 1 -> 8 strong-scaling ratio of `c5` (the shards'
+            # rollout lengths differ a little: seeds are independent draws of one generator)
+            sh, _, _ = many_graph_object(args, "c5_shard", graphs_of(range(0, args.c5_shard_graphs)), 0,
+                                         max(1, args.c5_steps), rank, world, None, dev, make_engine, weights, sync,
+                                         parallel)
+            c5["rank_shard_at_8"] = {
+                "graphs": args.c5_shard_graphs, "value": sh["value"], "ms_per_step": sh["ms_per_step"],
+                "removals_per_step": sh["removals_per_step"], "launches_per_step": sh["roofline"]["launches_per_step"],
+                "per_gpu_rate_vs_c5": sh["value"] / c5["value"],
+                "predicted_8_gpu_ratio": (args.c5_graphs / args.c5_shard_graphs) * sh["value"] / c5["value"]
+                * (c5["removals_per_step"] / (sh["removals_per_step"] * args.c5_graphs / args.c5_shard_graphs)),
+                "note": "predicted ratio = (4096-graph time on 1 GPU) / (the 512-graph shard's time on 1 GPU)"}
         if rank == 0 and args.cpu_dry_run:
             c5["audc_all"] = caudc
             c5["removals_all"] = crem
@@ -778,13 +838,11 @@ def rank_main(args):
                               prefix=int(c["prefix"]))
         traffic, traffic_note = load_traffic()
         if batch is not None and traffic is not None and args.batch_graphs == 256 and "batch" in traffic:
-            tb = traffic["batch"]
-            q, tail = tb.get("hbm_bytes_per_launch"), tb.get("tail_hbm_bytes_per_launch")
-            extra = batch["roofline"]["launches_per_step"] - 1.0
-            if q is not None and (extra < 0.5 or tail is not None):
-                batch["roofline"]["traffic"] = q + (extra * tail if extra >= 0.5 else 0.0)
-            batch["roofline"]["mfma_busy"] = tb.get("mfma_busy")
+            apply_traffic(batch["roofline"], traffic["batch"], batch["roofline"]["launches_per_step"])
             batch["roofline"]["traffic_note"] = traffic_note
+        if c5 is not None and traffic is not None and args.c5_graphs == 4096 and world == 1 and "c5" in traffic:
+            apply_traffic(c5["roofline"], traffic["c5"], c5["roofline"]["launches_per_step"])
+            c5["roofline"]["traffic_note"] = traffic_note
         have = golden is not None and audc is not None
         k = 0
         if have:

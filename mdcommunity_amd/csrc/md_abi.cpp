@@ -105,7 +105,6 @@ struct md_ctx {
   int variant = 0;   // diagnostics knob (MD_VARIANT)
   int pair_on = 1;   // queue mode: paired tiles (MD_PAIR=0: one tile at a time)
   int qpark = 8;     // queue mode: at most this many graphs left -> the lock-step kernel (MD_QPARK, 0 = off)
-  int qxcd = 0;      // queue mode: 8 XCD-affine work rings (MD_QXCD=1)
   double last_ms = 0.0;
   int last_launches = 0;
 
@@ -283,7 +282,6 @@ Params make_params(md_ctx* c) {
   p.qctl = (unsigned*)(c->ctl.p + CTL_Q);
   p.qslot = c->qslot.p;
   p.qring = (unsigned*)(c->ctl.p + CTL_RING);
-  p.qrings = c->qxcd ? 8 : 1;
   p.qg = c->qg.p;
   p.gtoff = c->gtoff.p;
   p.glist = c->glist.p;
@@ -773,7 +771,6 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_ENV_MODE")) c->env_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_PAIR")) c->pair_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_QPARK")) c->qpark = std::max(0, std::min(16, std::atoi(v)));
-  if (const char* v = std::getenv("MD_QXCD")) c->qxcd = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_HOST_HANDSHAKE")) c->host_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_POLL_US")) c->poll_us = std::atoi(v);
   if (const char* v = std::getenv("MD_H0G")) c->h0g_on = std::atoi(v) != 0;

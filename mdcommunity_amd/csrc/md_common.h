@@ -151,8 +151,7 @@ struct Params {
   int qmode;                       // 1: batch rollout through the device work queue (queue_loop)
   int qpair;                       // queue mode: a 2-tile item's tiles run jointly (queue_pair; MD_PAIR)
   int qpark;                       // queue mode: graphs left to the lock-step kernel at the tail (MD_QPARK)
-  unsigned* qring;                 // queue mode: ring r's {head, tail} tickets at qring + 32 r
-  int qrings;                      // queue mode: 1, or 8 XCD-affine rings (MD_QXCD)
+  unsigned* qring;                 // queue mode: the ring's {head, tail} tickets (a line of their own)
   unsigned* qctl;                  // queue mode: {head ticket, tail ticket, running graphs}
   unsigned long long* qslot;       // queue mode: Q_CAP item slots {ticket + 1, item}
   int* qg;                         // queue mode: per graph slot {tiles done in the stage, tiles}

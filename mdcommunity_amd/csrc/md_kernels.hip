@@ -2569,53 +2569,44 @@ __device__ __forceinline__ int q_tail(KParams& p) {
   const int v = (p.variant >> 13) & 7;
   return v == 0 ? (int)gridDim.x / 8 : (v == 7 ? -1 : 16 * v);
 }
-// Pushes n items f(0..n-1); every thread of the workgroup calls it.
-// Rings: p.qrings (1 or 8) work-queue rings, each with its head / tail tickets on a line of its
-// own (p.qring + 32 r) and Q_CAP / qrings slots.  With 8, a graph's items stay on the ring of
-// the workgroups blockIdx % 8 = r (one XCD: blocks b and b + 8 share an XCD), so its
-// embedding rows are written and re-read through one XCD's L2: every push of a graph's items
-// is made by a workgroup that processed one of its items (same ring), except the launch's
-// first admissions (ring i % 8 for the i-th) and the EXIT items (every ring).
-__device__ __forceinline__ int q_my_ring(KParams& p) { return (int)(blockIdx.x % (unsigned)p.qrings); }
-__device__ __forceinline__ g_u32* q_ctl(KParams& p, int r) { return (g_u32*)(p.qring + 32 * r); }
-__device__ __forceinline__ unsigned long long* q_slot(KParams& p, int r, unsigned tk) {
-  const unsigned per = (unsigned)(Q_CAP / p.qrings);
-  return p.qslot + (size_t)r * per + (tk & (per - 1u));
+// Pushes n items f(0..n-1); every thread of the workgroup calls it.  The ring's head / tail
+// tickets sit on a line of their own (p.qring); Q_CAP slots.
+__device__ __forceinline__ g_u32* q_ctl(KParams& p) { return (g_u32*)p.qring; }
+__device__ __forceinline__ unsigned long long* q_slot(KParams& p, unsigned tk) {
+  return p.qslot + (tk & (unsigned)(Q_CAP - 1));
 }
 template <class F>
-__device__ __forceinline__ void q_push(KParams& p, int n, F&& f, int* bc, int ring = -1) {
+__device__ __forceinline__ void q_push(KParams& p, int n, F&& f, int* bc) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's data stores are done
   __syncthreads();
-  const int r = ring < 0 ? q_my_ring(p) : ring;
   if (threadIdx.x == 0)
-    bc[0] = (int)__hip_atomic_fetch_add(q_ctl(p, r) + QC_TAIL, (unsigned)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bc[0] = (int)__hip_atomic_fetch_add(q_ctl(p) + QC_TAIL, (unsigned)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   const unsigned base = (unsigned)bc[0];
   for (int i = threadIdx.x; i < n; i += NTHREADS) {
     const unsigned tk = base + (unsigned)i;
     const unsigned long long v = ((unsigned long long)(tk + 1u) << 32) | f(i);
-    __hip_atomic_store((g_u64*)q_slot(p, r, tk), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((g_u64*)q_slot(p, tk), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
 }
-// EXIT items on every ring (two per workgroup of the launch on each: a workgroup may hold one
-// ticket it never uses)
+// EXIT items, two per workgroup of the launch (a workgroup may hold one ticket it never uses)
 __device__ __forceinline__ void q_push_exit(KParams& p, int* bc) {
-  for (int r = 0; r < p.qrings; ++r) q_push(p, 2 * gridDim.x, [&](int) { return (unsigned)QK_EXIT; }, bc, r);
+  q_push(p, 2 * gridDim.x, [&](int) { return (unsigned)QK_EXIT; }, bc);
 }
 // Thread 0 takes the next ticket; it is taken one item ahead (the atomic's latency overlaps
 // the current item), so a workgroup may hold one ticket it never uses when it exits: EXIT
 // items are pushed twice per workgroup.
 __device__ __forceinline__ unsigned q_take(KParams& p) {
   return threadIdx.x == 0
-             ? __hip_atomic_fetch_add(q_ctl(p, q_my_ring(p)) + QC_HEAD, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+             ? __hip_atomic_fetch_add(q_ctl(p) + QC_HEAD, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
              : 0u;
 }
 // Thread 0 reads ticket tk's slot without waiting for it (issued beside an item's last memory
 // round trip, so a slot that is already filled costs no round trip of its own in q_wait).
 __device__ __forceinline__ unsigned long long q_peek(KParams& p, unsigned tk) {
   return threadIdx.x == 0
-             ? __hip_atomic_load((const g_u64*)q_slot(p, q_my_ring(p), tk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+             ? __hip_atomic_load((const g_u64*)q_slot(p, tk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
              : 0ull;
 }
 __device__ __forceinline__ unsigned q_wait(KParams& p, unsigned tk, int* bc, unsigned long long pre) {
@@ -2626,7 +2617,7 @@ __device__ __forceinline__ unsigned q_wait(KParams& p, unsigned tk, int* bc, uns
     const bool ready = (v >> 32) == (unsigned long long)(tk + 1u);
     if (!ready) v = QK_EXIT;
     if (!ready && !(__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR)) {
-      const g_u64* slot = (const g_u64*)q_slot(p, q_my_ring(p), tk);
+      const g_u64* slot = (const g_u64*)q_slot(p, tk);
       const unsigned long long t0 = wall_clock64();
       while (((v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != (unsigned long long)(tk + 1u)) {
         __builtin_amdgcn_s_sleep(2);
@@ -3711,10 +3702,7 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
     }
     __syncthreads();
     if (tot > 0) {
-      // the i-th admitted graph starts on ring i % qrings (and stays there)
-      const int R = p.qrings;
-      for (int r = 0; r < R; ++r)
-        q_push(p, (first - r + R - 1) / R, [&](int i) { return q_item(QK_ENV, 0, run[r + R * i], 0); }, bc, r);
+      q_push(p, first, [&](int i) { return q_item(QK_ENV, 0, run[i], 0); }, bc);
     } else {
       q_push_exit(p, bc);
     }
@@ -3746,7 +3734,7 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
         // diagnostics (MD_VARIANT bit 8): pops whose slot was already filled at the early read
         // (slot 18), and the queue's backlog beyond the held ticket summed over pops (slot 19)
         if ((pre >> 32) == (unsigned long long)(tk + 1u)) atomicAdd(qp + 18, 1ull);
-        const unsigned tl = __hip_atomic_load(q_ctl(p, q_my_ring(p)) + QC_TAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned tl = __hip_atomic_load(q_ctl(p) + QC_TAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         atomicAdd(qp + 19, (unsigned long long)max(0, (int)(tl - tk)));
       }
       item = q_wait(p, tk, bc, pre);

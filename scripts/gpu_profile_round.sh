@@ -1,8 +1,10 @@
 #!/bin/bash
 # Round profile on the GPU box (run from the repo root), in this order so that the bench line
 # carries the traffic measured from the same build in the same session:
-#  1. rocprofv3 kernel-trace stats of the single-graph, batch (256) and C5 (4096) workloads;
-#  2. PMC passes of the single-graph and batch workloads, one counter group per run
+#  1. rocprofv3 kernel-trace stats of the single-graph, batch (256), C5 (4096), degree-cost and
+#     N = 18 000 testReal-sized (degree step 1, unit stepRatio 0.01) workloads;
+#  2. PMC passes of every workload (HBM traffic and the SQ_1 group; SQ_2/SQ_3 for the single
+#     graph and the batch), one counter group per run
 #     (FETCH_SIZE / WRITE_SIZE for HBM traffic; SQ groups for MFMA busy, wave states, LDS, the
 #     instruction mix; GRBM_GUI_ACTIVE for the clock; MI355X_MICROARCH.md PMC slots);
 #  3. scripts/rocprof_summary.py -> summary.txt + traffic.json (tagged with the kernel source
@@ -18,6 +20,9 @@ export TMPDIR=/tmp
 SINGLE="--batch-graphs 0 --c5-graphs 0 --no-cpu-baseline --degree-steps 0 --no-per-step --real-steps 0"
 BATCH="--steps 0 --batch-graphs 256 --c5-graphs 0 --no-cpu-baseline --degree-steps 0 --no-per-step --real-steps 0"
 C5="--steps 0 --batch-graphs 0 --c5-graphs 4096 --c5-steps 1 --no-cpu-baseline --degree-steps 0 --no-per-step --real-steps 0"
+DEGREE="--steps 0 --batch-graphs 0 --c5-graphs 0 --no-cpu-baseline --degree-steps 2 --no-per-step --real-steps 0"
+REAL_DEGREE="--steps 0 --batch-graphs 0 --c5-graphs 0 --no-cpu-baseline --degree-steps 0 --no-per-step --real-steps 1 --real-cases degree"
+REAL_UNIT="--steps 0 --batch-graphs 0 --c5-graphs 0 --no-cpu-baseline --degree-steps 0 --no-per-step --real-steps 1 --real-cases unit"
 SQ1="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_F32 SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT"
 SQ2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_VALU SQ_INSTS_SALU SQ_VALU_MFMA_COEXEC_CYCLES"
 SQ3="SQ_INSTS_FLAT SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAVES"
@@ -32,14 +37,26 @@ cd /tmp
 run single_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/single -o run -- python $R/bench.py $SINGLE
 run batch_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/batch -o run -- python $R/bench.py $BATCH --batch-steps 2
 run c5_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/c5 -o run -- python $R/bench.py $C5
-for W in single batch; do
-  if [ $W = single ]; then ARGS="$SINGLE --steps 2 --warmup 1"; else ARGS="$BATCH --batch-steps 1"; fi
-  run pmc_fetch_$W 180 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch_$W -o run -- python $R/bench.py $ARGS
-  run pmc_write_$W 180 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write_$W -o run -- python $R/bench.py $ARGS
-  run pmc_sq1_$W 180 rocprofv3 --pmc $SQ1 -d $OUT/pmc_sq1_$W -o run -- python $R/bench.py $ARGS
-  run pmc_sq2_$W 180 rocprofv3 --pmc $SQ2 -d $OUT/pmc_sq2_$W -o run -- python $R/bench.py $ARGS
-  timeout -s KILL 120 rocprofv3 --pmc $SQ3 -d $OUT/pmc_sq3_$W -o run -- python $R/bench.py $ARGS > $OUT/pmc_sq3_$W.log 2>&1
-  echo "pmc_sq3_$W rc=$? (optional)"
+run degree_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/degree -o run -- python $R/bench.py $DEGREE
+run real_degree_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/real_degree -o run -- python $R/bench.py $REAL_DEGREE
+run real_unit_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/real_unit -o run -- python $R/bench.py $REAL_UNIT
+for W in single batch c5 degree real_degree real_unit; do
+  case $W in
+    single) ARGS="$SINGLE --steps 2 --warmup 1" ;;
+    batch) ARGS="$BATCH --batch-steps 1" ;;
+    c5) ARGS="$C5" ;;
+    degree) ARGS="$DEGREE" ;;
+    real_degree) ARGS="$REAL_DEGREE" ;;
+    real_unit) ARGS="$REAL_UNIT" ;;
+  esac
+  run pmc_fetch_$W 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch_$W -o run -- python $R/bench.py $ARGS
+  run pmc_write_$W 240 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write_$W -o run -- python $R/bench.py $ARGS
+  run pmc_sq1_$W 240 rocprofv3 --pmc $SQ1 -d $OUT/pmc_sq1_$W -o run -- python $R/bench.py $ARGS
+  if [ $W = single ] || [ $W = batch ]; then
+    run pmc_sq2_$W 180 rocprofv3 --pmc $SQ2 -d $OUT/pmc_sq2_$W -o run -- python $R/bench.py $ARGS
+    timeout -s KILL 120 rocprofv3 --pmc $SQ3 -d $OUT/pmc_sq3_$W -o run -- python $R/bench.py $ARGS > $OUT/pmc_sq3_$W.log 2>&1
+    echo "pmc_sq3_$W rc=$? (optional)"
+  fi
 done
 cd $R
 python scripts/rocprof_summary.py $OUT > /dev/null && cp $OUT/traffic.json profiles/traffic.json && echo "summary done"

@@ -4,8 +4,9 @@
 * kernel-trace runs (single/, batch/): per-kernel calls / total / average / min / max duration
   (the --stats view) from the rocpd SQLite output;
 * PMC passes (pmc_<group>_<workload>/): per-dispatch counter values of the workload's main
-  kernel (md_rollout_kernel for the single graph, md_queue_kernel for the batch), averaged per
-  launch.
+  kernel (md_rollout_kernel for the single graph, the degree-cost graph and the N = 18 000
+  testReal-sized cases; md_queue_kernel for the batch and C5, with their tail launches),
+  averaged per launch.
 
 Derived per launch (written to traffic.json, which bench.py reads when its `src_hash` equals the
 hash of the kernel sources being benchmarked):
@@ -27,7 +28,8 @@ import sqlite3
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-KERNELS = {"single": "md_rollout_kernel", "batch": "md_queue_kernel", "c5": "md_queue_kernel"}
+KERNELS = {"single": "md_rollout_kernel", "batch": "md_queue_kernel", "c5": "md_queue_kernel",
+           "degree": "md_rollout_kernel", "real_degree": "md_rollout_kernel", "real_unit": "md_rollout_kernel"}
 CUS, SIMDS, XCDS, PEAK_TF = 256, 4, 8, 157.3
 
 
@@ -87,7 +89,7 @@ def workload(d, w, lines):
                 vals[c] = v
                 lines.append(f"== {w} {c} per {kernel} dispatch (raw): {[round(x, 1) for x in v]}")
     m = {c: mean(v) for c, v in vals.items()}
-    if w == "batch":
+    if w in ("batch", "c5"):
         # the tail launch of each batch rollout (md_rollout_kernel: the last graphs the queue
         # hands to the lock-step kernel): its traffic per dispatch, so bench.py can report the
         # traffic of a whole batch step
@@ -138,10 +140,11 @@ def main():
     import bench
     d = sys.argv[1]
     lines = [f"kernel sources hash {bench.kernel_src_hash()}"]
-    report = {w: workload(d, w, lines) for w in ("single", "batch", "c5")}
-    out = dict(report["single"])
-    out["batch"] = report["batch"]
-    out["c5"] = report["c5"]
+    report = {w: workload(d, w, lines) for w in KERNELS if os.path.isdir(os.path.join(d, w))}
+    out = dict(report.get("single", {}))
+    for w in KERNELS:
+        if w != "single" and w in report:
+            out[w] = report[w]
     out["src_hash"] = bench.kernel_src_hash()
     out["source"] = f"rocprofv3 PMC passes, {os.path.basename(os.path.normpath(d))} (scripts/gpu_profile_round.sh)"
     with open(os.path.join(d, "traffic.json"), "w") as fo:
