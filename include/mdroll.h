@@ -241,8 +241,6 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *                     instead of jointly (default 1)
  *   MD_QPARK          queue mode: once every graph is admitted and at most this many still
  *                     run, they continue in one lock-step launch (default 8, 0 = off, <= 16)
- *   MD_QXCD           1: queue mode with 8 XCD-affine work rings (a graph's items stay on the
- *                     workgroups of one XCD; default 0: one ring)
  *   MD_HOST_HANDSHAKE 0: end the launch on a tie and relaunch after the host selection
  *                     (default 1: in-kernel hand-shake through mapped host memory)
  *   MD_POLL_US        host-thread polling interval of the hand-shake (µs)
@@ -255,13 +253,10 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *                     state instead of building the next state from the result phase A takes
  *   MD_SPEC_ABORT     0: a speculative fixed point runs to the end even when phase A has taken
  *                     another result of its request (default 1: it stops after the round)
- *   MD_DF             single-graph rollouts in dedicated mode with the layer split: 3 (default)
+ *   MD_DF             single-graph rollouts in dedicated mode with the layer split: 1 (default)
  *                     dataflow mode (no grid barrier, tagged hand-offs) whose tiles derive
- *                     phase A's pick from the arg-max partials and prebuild from it; 1 without
- *                     that (the prebuild waits for phase A's early word); 2 prebuilds from
- *                     speculative workgroup 0's result before phase A picks; 0 grid barriers
- *   MD_SELF_SPEC      0: the speculative workgroups wait for phase A's early word instead of
- *                     tile 0's derivation of it (MD_DF=3)
+ *                     phase A's pick from the arg-max partials and prebuild from it; 0 grid
+ *                     barriers (the tiles prebuild from phase A's early word)
  *   MD_FP_SHORTCUT    0: every mutual-LMCC fixed point runs its confirmation round (default 1:
  *                     a pruned partition certified by its spanning forests ends the fixed point)
  *   MD_FIRST_REQ      0: no speculative request at a rollout's first environment step (default

@@ -168,9 +168,6 @@ struct md_ctx {
   // a speculative fixed point stops once phase A has taken another result of its request or a
   // later request is out (MD_SPEC_ABORT=0: always runs to the end)
   bool abort_on = true;
-  bool df_r0 = false;  // measured: no gain over the early-word prebuild alone
-  bool df_self = true;  // MD_DF=3 (default): tiles derive phase A's pick (df_wait_rec)
-  bool self_spec = true;  // ... and tile 0 publishes it to the speculative workgroups (MD_SELF_SPEC=0: off)
   bool fp_short = true;  // MD_FP_SHORTCUT=0: every fixed point runs its confirmation round
   bool first_req = true;  // MD_FIRST_REQ=0: no speculative request at a rollout's first step
   DevBuf<unsigned long long> dfbuf;
@@ -570,9 +567,8 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
     p.df = c->dfbuf.p;
     p.df_mt = c->df_mt;
     p.df_n = c->df_n;
-    p.df_r0 = c->df_r0 ? 1 : 0;
-    p.df_self = c->df_self ? 1 : 0;
-    if (c->df_self && p.pre_ew != nullptr && c->self_spec) p.self_ew = (unsigned long long*)(c->ctl.p + CTL_SELF);
+    // tile 0 hands its derivation of phase A's early word to the speculative workgroups
+    if (p.pre_ew != nullptr) p.self_ew = (unsigned long long*)(c->ctl.p + CTL_SELF);
   }
   p.qmode = qmode ? 1 : 0;
   p.qpair = c->pair_on ? 1 : 0;
@@ -776,14 +772,9 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_H0G")) c->h0g_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_EARLY")) c->early_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_SPEC_ABORT")) c->abort_on = std::atoi(v) != 0;
-  if (const char* v = std::getenv("MD_SELF_SPEC")) c->self_spec = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_FP_SHORTCUT")) c->fp_short = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_FIRST_REQ")) c->first_req = std::atoi(v) != 0;
-  if (const char* v = std::getenv("MD_DF")) {
-    c->df_on = std::atoi(v) != 0;
-    c->df_r0 = std::atoi(v) == 2;  // MD_DF=2: with the prebuild from speculative workgroup 0's result
-    c->df_self = std::atoi(v) == 3;
-  }
+  if (const char* v = std::getenv("MD_DF")) c->df_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_SPEC")) c->spec_n = std::max(0, std::min(SPEC_MAX, std::atoi(v)));
   md_status st = MD_OK;
   do {
@@ -805,8 +796,8 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   }
   *out = c;
   if (trace_on())
-    std::fprintf(stderr, "md trace: create ctx %p df %d r0 %d self %d variant %d spec %d\n", (void*)c, c->df_on ? 1 : 0,
-                 c->df_r0 ? 1 : 0, c->df_self ? 1 : 0, c->variant, c->spec_n);
+    std::fprintf(stderr, "md trace: create ctx %p df %d variant %d spec %d\n", (void*)c, c->df_on ? 1 : 0, c->variant,
+                 c->spec_n);
   return MD_OK;
 }
 

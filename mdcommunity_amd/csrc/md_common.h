@@ -186,10 +186,8 @@ struct Params {
   unsigned long long* df;
   int df_mt;                       // tiles of the largest graph the buffer is sized for
   int df_n;                        // nodes of that graph
-  int df_r0;                       // 1: tiles prebuild from speculative workgroup 0's result before phase A picks
   int fp_short;                    // 1: mutual-LMCC fixed points end by the confirmation shortcut (mcc_fixed_point)
   int first_req;                   // 1: a rollout's first step requests degree-ranked speculative results (env_step)
-  int df_self;                     // 1: tiles derive phase A's pick from the arg-max partials (df_wait_rec)
 };
 // dataflow buffer size (granules) for graphs of at most n nodes / mt tiles
 inline long long df_granules(int n, int mt) { return 64 + 772LL * mt + 8LL * 64 * n; }

@@ -1422,8 +1422,10 @@ __device__ __noinline__ void nbc_store(KParams&, int slot, const float*, bool ok
 // two features each in CSR order.
 // deg_ovr / hp_ovr (iteration 1 speculated during phase A): the residual degrees and the
 // first-layer rows of the speculative result instead of the graph's arrays.
-// dcap: first-layer rows by degree are clamped to [0, dcap] (the prebuild's table of the result's
-// dmax: a prebuild from a slot being rewritten must not address beyond it).
+// dcap: first-layer rows by degree are clamped to [1, dcap] (the prebuild's table of the result's
+// dmax, whose row d sits at hp + d rows: a prebuild from a slot being rewritten must not address
+// outside it -- row 0 of the dmax-1 table would lie 256 B before the h0g allocation; every node on
+// a tile's rows or lists has degree >= 1, so consistent data are unaffected).
 __device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it, const int*, float*, int L,
                                            const int* deg_ovr = nullptr, const float* hp_ovr = nullptr,
                                            int dcap = 0x7fffffff) {
@@ -1449,7 +1451,7 @@ __device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it,
   const int v = rows[r];
   float2 own = {0.f, 0.f}, acc = {0.f, 0.f};
   if (v >= 0) {
-    const int ov = table ? min(max(ldc(deg + v), 0), dcap) : v;
+    const int ov = table ? min(max(ldc(deg + v), 1), dcap) : v;
     if (MD_BOK(v < gi.n && ov >= 0 && ov < gi.n, 1)) own = ldc2(hp, ov * 256 + q * 8);
   }
   const int myoff = hdr[l * 16 + r], mycnt = hdr[32 + l * 16 + r];
@@ -1466,7 +1468,7 @@ __device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it,
       src[i] = -1;
       if (b < nbat && k < SROWS * 16 && row < totl) {
         const int id = nbl[row];
-        src[i] = MD_BOK(id < gi.n, 4) ? (table ? min(max(ldc(deg + id), 0), dcap) : id) : -1;
+        src[i] = MD_BOK(id < gi.n, 4) ? (table ? min(max(ldc(deg + id), 1), dcap) : id) : -1;
         if (!MD_BOK(src[i] < gi.n, 5)) src[i] = -1;
       }
     }
@@ -1741,10 +1743,9 @@ __device__ __forceinline__ void df_store_tile(KParams&, int j, int L, int it, un
          make_float4(e[(2 * c2) * LDT + rr], tf, e[(2 * c2 + 1) * LDT + rr], tf));
 }
 
-// dft != 0 (dataflow mode): the outputs go out as granules tagged dft (df_store_tile); defer:
-// none at all -- they stay in LDS (E, X) for df_store_tile once the result is confirmed.
+// dft != 0 (dataflow mode): the outputs go out as granules tagged dft (df_store_tile).
 __device__ __forceinline__ bool spec_iteration1(KParams&, const GraphInfo gi, int j, int L, unsigned long long ew,
-                                             unsigned dft = 0, bool defer = false, unsigned long long* ts = nullptr) {
+                                             unsigned dft = 0, unsigned long long* ts = nullptr) {
   KParams& p = kp();
   float* const lds = lds_base();
   float* const scr = lds + L_SCR;
@@ -1766,7 +1767,6 @@ __device__ __forceinline__ bool spec_iteration1(KParams&, const GraphInfo gi, in
   normalize_tile_split(scr + S_E, scr, L);
   __syncthreads();
   TSTAMP(27);  // updated, normalised
-  if (defer) return true;
   if (dft != 0) {
     df_store_tile(p, j, L, 1, dft);
     __syncthreads();
@@ -4259,10 +4259,7 @@ __device__ __noinline__ void spec_loop(KParams&) {
 // with `full`, also its "full" granule: phase A has finished, not just published the record
 // early), 2 when `watch` is set and the early word changed first (new value in the LDS word at
 // L_MISC + 42), 0 on an error anywhere.  Uniform.
-// With `watch`, also 3 when speculative workgroup 0's result for this step's request (spec_req of
-// step req_step) has its features published and differs from the LDS word at L_MISC + 38 (then
-// updated): the likeliest next state, prebuilt before phase A has picked (p.df_r0).
-// Self-pick (p.df_self, nt_self = the previous step's tile count, <= 64): the wave also polls the
+// Self-pick (nt_self = the previous step's tile count, <= 64): the wave also polls the
 // previous step's arg-max partials (phase A's inputs) and, once all are in, combines them exactly
 // as phase A does; a unique maximum whose node is the candidate of a started or finished result
 // of request req_step gives the early word phase A will publish, returned as 4 (L_MISC + 38) --
@@ -4282,7 +4279,6 @@ __device__ __forceinline__ int df_wait_rec(KParams&, unsigned tag, bool watch, b
     const int lane = threadIdx.x;
     const bool w = watch && p.pre_ew != nullptr;
     const bool wr = w && req_step >= 0 && p.sres != nullptr && p.spec_req != nullptr;
-    const bool w0 = wr && p.df_r0;
     bool ws = wr && nt_self > 0 && nt_self <= 64 && !p.host_select && misc[30] == 0;
     const unsigned ptag = (unsigned)(req_step + 1) << 1;  // the partials of step req_step (df_tag)
     const float* const apb = (const float*)df_ap(p);
@@ -4296,10 +4292,7 @@ __device__ __forceinline__ int df_wait_rec(KParams&, unsigned tag, bool watch, b
       if (lane < 7) g = __hip_atomic_load((const g_u64*)(p.df + DF_REC + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else if (lane == 8) g = __hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else if (lane == 7 && w) g = __hip_atomic_load((const g_u64*)p.pre_ew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else if (lane == 9 && (w0 || ws)) g = __hip_atomic_load((const g_u64*)p.spec_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else if (lane == 10 && w0)
-        g = __hip_atomic_load((const g_u64*)(p.sres + (size_t)spec_slot_index(0, req_step) * p.sres_stride + SRES_FEAT),
-                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else if (lane == 9 && ws) g = __hip_atomic_load((const g_u64*)p.spec_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pc = pa;
       if (ws && lane < nt_self) {
         pa = ldc4(apb, lane * 32);
@@ -4318,7 +4311,7 @@ __device__ __forceinline__ int df_wait_rec(KParams&, unsigned tag, bool watch, b
           }
           sv = ew;
           // (phase A's early word equal to this step's self-pick: that prebuild is the one)
-          if (!(p.df_self && ew == s0 && (unsigned)(ew >> 32) != 0u)) {
+          if (!(ew == s0 && (unsigned)(ew >> 32) != 0u)) {
             res = 2;
             break;
           }
@@ -4369,20 +4362,6 @@ __device__ __forceinline__ int df_wait_rec(KParams&, unsigned tag, bool watch, b
               res = 4;
               break;
             }
-          }
-        }
-      }
-      if (w0) {
-        const unsigned rlo = __shfl((unsigned)g, 9, 64), rhi = __shfl((unsigned)(g >> 32), 9, 64);
-        const unsigned flo = __shfl((unsigned)g, 10, 64), fhi = __shfl((unsigned)(g >> 32), 10, 64);
-        if ((int)rhi == req_step && rlo == flo && rlo != 0u) {
-          // early word form {request tag << 32 | candidate << 16 | slot}
-          const unsigned long long e0 = ((unsigned long long)rlo << 32) | ((unsigned long long)(fhi & 0xffffu) << 16) |
-                                        (unsigned)spec_slot_index(0, req_step);
-          if (e0 != s0) {
-            if (lane == 0) *tried0 = e0;
-            res = 3;
-            break;
           }
         }
       }
@@ -4509,49 +4488,36 @@ __device__ __noinline__ void df_tiles(KParams&) {
       misc[30] = 0;  // this step's self-pick not decided yet (df_wait_rec)
     }
     __syncthreads();
-    // the step record; meanwhile the iteration-1 prebuild, first from speculative workgroup 0's
-    // result (the likeliest pick, ready before phase A has picked), then, if phase A's early word
-    // names another result, from that one (rows and sums are tagged with the result's slot)
-    // A prebuild from workgroup 0's result keeps its iteration-1 outputs in LDS until phase A's
-    // early word names that result (another result's prebuild then rebuilds the rows): its rows
-    // belong to that result's tile assignment, so storing them for a result phase A does not
-    // take could overwrite rows that other tiles own in the actual state.  A prebuild from the
-    // early word stores at once (the early word is the applied result unless the rollout ends).
+    // the step record; meanwhile the iteration-1 prebuild, first from the self-pick (the result
+    // phase A will take, derived from the previous step's arg-max partials before phase A's slot
+    // check), then, if phase A's early word names another result, from that one (rows and sums
+    // are tagged with the result's slot; both store at once: phase A takes the same node, hence
+    // the same state and tile assignment)
     int pre_state = 0, r;
     unsigned long long pre_used = 0ull;
-    bool deferred = false;
-    while ((r = df_wait_rec(p, (unsigned)(pstep + 1), true, false, p.df_r0 || p.df_self ? pstep - 1 : -1,
-                            p.df_self && pstep >= 1 ? (nl_prev + TILE - 1) / TILE : 0)) >= 2) {
-      const unsigned long long ew = r == 2 ? *seen : *tried0;  // (3: workgroup 0's result, 4: the self-pick)
+    while ((r = df_wait_rec(p, (unsigned)(pstep + 1), true, false, pstep - 1,
+                            pstep >= 1 ? (nl_prev + TILE - 1) / TILE : 0)) >= 2) {
+      const unsigned long long ew = r == 2 ? *seen : *tried0;  // (4: the self-pick)
       if (ew != 0ull && ew != pre_used) {
         DF_STAMP_MAX(54);
         pre_used = 0ull;
-        deferred = false;
         // diagnostics: tile 0's layer-0 workgroup stamps the pieces of its prebuild
         unsigned long long* const pts = p.prof != nullptr && tb == 0 && pstep < p.prof_cap ? p.prof + (size_t)pstep * PROF_SLOTS : nullptr;
         pre_state = prebuild_lists(p, gi, j, L, ew, pts, r >= 3 ? *seen : 0ull);
         DF_STAMP_MAX(55);
         if (pre_state) pre_used = ew;
-        // a prebuild from workgroup 0's result that phase A's early word has already overtaken
-        // (it names another result) stops after its lists
+        // a self-pick prebuild that phase A's early word has already overtaken (it names another
+        // result) stops after its lists
         const unsigned long long now = ((unsigned long long)(unsigned)misc[37] << 32) | (unsigned)misc[36];
         if (r >= 3 && pre_state == 1 && now != 0ull && now != *seen && now != ew) {
           pre_state = 0;
           pre_used = 0ull;
         }
         // the whole of iteration 1 too (MD_VARIANT bit 128: lists only)
-        if (pre_state == 1 && !(p.variant & 128) &&
-            spec_iteration1(p, gi, j, L, ew, df_ptag(df_tag(pstep), ew), r == 3, pts)) {
+        if (pre_state == 1 && !(p.variant & 128) && spec_iteration1(p, gi, j, L, ew, df_ptag(df_tag(pstep), ew), pts))
           pre_state = 3;
-          deferred = r == 3;
-        }
         DF_STAMP_MAX(56);
         DF_STAMP_TILE(2);
-      } else if (r == 2 && ew == pre_used && deferred) {
-        // phase A took workgroup 0's result: its prebuilt outputs go out now
-        df_store_tile(p, j, L, 1, df_ptag(df_tag(pstep), ew));
-        __syncthreads();
-        deferred = false;
       }
     }
     if (r != 1 || misc[50] != ST_RUN) break;
@@ -4568,10 +4534,6 @@ __device__ __noinline__ void df_tiles(KParams&) {
       unsigned long long* const ps = p.prof + (size_t)pstep * PROF_SLOTS;
       atomicMax(ps + (pre_ok == 3 ? 77 : 76), wall_clock64());  // latest record seen, with / without prebuild
       if (pre_ok != 3) atomicAdd(ps + 79, 1ull);                 // tiles without the confirmed prebuild
-    }
-    if (pre_ok == 3 && deferred) {  // (the early word was not seen before the record)
-      df_store_tile(p, j, L, 1, df_ptag(df_tag(pstep), cw));
-      __syncthreads();
     }
     // a tile without the confirmed prebuild reads phase A's outputs: the whole of phase A first
     if (pre_ok != 3 && df_wait_rec(p, (unsigned)(pstep + 1), false, true) != 1) break;
