@@ -980,7 +980,7 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   }
   HIPCHK(c, c->covered.alloc(tn + 4));
   HIPCHK(c, c->live.alloc(4 * tn));  // {node, CSR begin l0, l1, extents} per live position
-  HIPCHK(c, c->gscr.alloc(5 * tn));  // global-mode environment scratch (20 B per node; always, so MD_VARIANT=64 can force that mode)
+  HIPCHK(c, c->gscr.alloc(GSCR_WORDS * tn));  // global-mode environment scratch (always, so MD_VARIANT=64 can force that mode)
   HIPCHK(c, c->pend.alloc(tn));
   HIPCHK(c, c->tr_action.alloc(tn));
   HIPCHK(c, c->tr_rank.alloc(tn));

@@ -102,7 +102,7 @@ struct Params {
   float* H[2][2];                  // [layer][buffer] node embeddings, node-major x 64
   float* h0tab[2];                 // [layer] first-layer embedding: by degree (unit) / by node (degree cost)
   float* q;                        // per node (-inf = masked)
-  int* gscr;                       // phase-A scratch in global memory for graphs too big for LDS: 5 per node
+  int* gscr;                       // phase-A scratch in global memory for graphs too big for LDS: GSCR_WORDS per node
   long long* tpart;                // grid-wide environment step: per-workgroup partials [2][TEAM_MAX_WG][16]
   int* tctl;                       // grid-wide environment step: {actions (-1: none), first action}
   float* spart;                    // per tile: [3 sums][2 layers][64] virtual-node partial sums
@@ -189,6 +189,8 @@ struct Params {
   int fp_short;                    // 1: mutual-LMCC fixed points end by the confirmation shortcut (mcc_fixed_point)
   int first_req;                   // 1: a rollout's first step requests degree-ranked speculative results (env_step)
 };
+// global-mode environment scratch words per node (md_env.h env_view, team_env_step)
+constexpr int GSCR_WORDS = 9;
 // dataflow buffer size (granules) for graphs of at most n nodes / mt tiles
 inline long long df_granules(int n, int mt) { return 64 + 772LL * mt + 8LL * 64 * n; }
 

@@ -912,7 +912,9 @@ __device__ __forceinline__ EnvView<GL> env_view(KParams& p, const GraphInfo& gi,
   }
   E.gcov = p.covered + gi.node_off;
   if constexpr (GL) {
-    int* gs = p.gscr + 5 * (size_t)gi.node_off;  // par0, par1, deg0, deg1, LMCC counts (team step)
+    // par0, par1, deg0, deg1, LMCC counts (team step), the team step's second parent buffers and
+    // its degree arrays (env_layout's global-mode counterpart; GSCR_WORDS per node)
+    int* gs = p.gscr + GSCR_WORDS * (size_t)gi.node_off;
     E.par0 = gs;
     E.par1 = gs + n;
     E.deg0 = gs + 2 * n;
@@ -1547,30 +1549,52 @@ __device__ bool team_reduce(KParams& p, Team& T, const long long (&v)[K], unsign
 // Mutual-LMCC fixed point of mcc_fixed_point on the whole grid (cover >= 0: cover that node in
 // the first union pass; its covered edge counts per layer in cc).  LMCC size in lm, pruned edge
 // counts in pr.  Labels (component roots) end in E.deg0 / E.deg1 as there.
+// Two grid barriers per round instead of three: the prune of round r (by round r's labels) and
+// the union of round r + 1 are one edge pass -- each thread decides per alive edge whether the
+// other layer's labels separate its endpoints (pruned) or it is united -- on parent arrays
+// double-buffered by round (round r + 1's are reset during round r's label pass).  The edge set
+// each union pass sees, and so every partition, label and pruned edge, is the three-pass loop's.
+// deg_zero (the features' degree arrays, grid-wide scratch): zeroed in the init pass.
 __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, int* cnt, int cover, bool set_cover, int& lm,
-                                 int* pr, int* cc) {
+                                 int* pr, int* cc, int* deg_zero = nullptr) {
   const int n = E.gi->n, et = E.et, e0 = E.e0;
+  int* const pb[2][2] = {{E.par0, E.par1}, {E.par0 + 5 * n, E.par0 + 6 * n}};  // gscr: par0, par1 | par0', par1'
   if (T.acc != nullptr && threadIdx.x == 0) T.t = wall_clock64();
   for (int x = T.gt; x < n; x += T.gs) {
-    uf_store(E.par0, x, x);
-    uf_store(E.par1, x, x);
+    uf_store(pb[0][0], x, x);
+    uf_store(pb[0][1], x, x);
+    if (deg_zero != nullptr) {
+      uf_store(deg_zero, x, 0);
+      uf_store(deg_zero, n + x, 0);
+    }
   }
   if (grid_sync(p, *T.target, T.flag)) return true;
   TEAM_ACC(T, 6);
   if (set_cover && cover >= 0 && threadIdx.x == 0) stc(E.gcov + cover, (uint8_t)1);  // read by the count pass
-  bool first = true;
   pr[0] = pr[1] = 0;
-  while (true) {
-    long long k0 = 0, k1 = 0;
+  for (int round = 0;; ++round) {
+    const bool first = round == 0;
+    int* const P0 = pb[round & 1][0];
+    int* const P1 = pb[round & 1][1];
+    long long k0 = 0, k1 = 0, c0 = 0, c1 = 0;
     if (T.prof_any != nullptr) T.t0any = wall_clock64();
     for (int e = T.gt; e < et; e += T.gs) {
       if (E.state(e) != E_ALIVE) continue;
       const int u = E.u(e), v = E.v(e);
+      if (!first) {
+        // the previous round's prune: layer-0 edges by the layer-1 components and vice versa
+        auto other = e < e0 ? E.deg1 : E.deg0;
+        if (uf_load(other, u) != uf_load(other, v)) {
+          E.kill(e, E_PRUNED);
+          if (e < e0) c0++; else c1++;
+          continue;
+        }
+      }
       if (first && cover >= 0 && (u == cover || v == cover)) {
         E.kill(e, E_COVERED);
         if (e < e0) k0++; else k1++;
       } else {
-        uf_unite_h(e < e0 ? E.par0 : E.par1, u, v);
+        uf_unite_h(e < e0 ? P0 : P1, u, v);
       }
     }
     if (first)  // LMCC counters, used after the last round
@@ -1588,45 +1612,29 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
     if (grid_sync(p, *T.target, T.flag)) return true;
     TEAM_ACC(T, 1);
     if (T.acc != nullptr && threadIdx.x == 0) T.acc[0] += 1;
+    // labels of this round; the next round's parents reset (nobody reads them in this round)
+    int* const Q0 = pb[(round + 1) & 1][0];
+    int* const Q1 = pb[(round + 1) & 1][1];
     long long diff = 0;
     for (int x = T.gt; x < n; x += T.gs) {
-      const int r0 = uf_find_h(E.par0, x), r1 = uf_find_h(E.par1, x);
+      const int r0 = uf_find_h(P0, x), r1 = uf_find_h(P1, x);
       uf_store(E.deg0, x, r0);
       uf_store(E.deg1, x, r1);
+      uf_store(Q0, x, x);
+      uf_store(Q1, x, x);
       diff += r0 != r1;
     }
-    const long long v3[3] = {diff, k0, k1};
-    long long t3[3];
-    if (team_reduce<3>(p, T, v3, 0u, t3, nullptr)) return true;
+    const long long v5[5] = {diff, k0, k1, c0, c1};
+    long long t5[5];
+    if (team_reduce<5>(p, T, v5, 0u, t5, nullptr)) return true;
     TEAM_ACC(T, 2);
     if (first && cover >= 0) {
-      cc[0] = (int)t3[1];
-      cc[1] = (int)t3[2];
+      cc[0] = (int)t5[1];
+      cc[1] = (int)t5[2];
     }
-    first = false;
-    if (t3[0] == 0) break;
-    // prune every alive edge whose endpoints the other layer separates; the next round's forests
-    // start over (the parents are not read by this pass)
-    long long c0 = 0, c1 = 0;
-    for (int e = T.gt; e < et; e += T.gs) {
-      if (E.state(e) != E_ALIVE) continue;
-      const int u = E.u(e), v = E.v(e);
-      auto other = e < e0 ? E.deg1 : E.deg0;
-      if (uf_load(other, u) != uf_load(other, v)) {
-        E.kill(e, E_PRUNED);
-        if (e < e0) c0++; else c1++;
-      }
-    }
-    for (int x = T.gt; x < n; x += T.gs) {
-      uf_store(E.par0, x, x);
-      uf_store(E.par1, x, x);
-    }
-    const long long v2[2] = {c0, c1};
-    long long t2[2];
-    if (team_reduce<2>(p, T, v2, 0u, t2, nullptr)) return true;
-    TEAM_ACC(T, 3);
-    pr[0] += (int)t2[0];
-    pr[1] += (int)t2[1];
+    pr[0] += (int)t5[3];
+    pr[1] += (int)t5[4];
+    if (t5[0] == 0) break;
   }
   // the LMCC: non-covered nodes per component (layer-0 label = layer-1 label at the fixed point);
   // the largest count is the maximum over the adds' results (each word's last add sees its total)
@@ -1647,22 +1655,25 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
 // env_features on the whole grid: residual degrees by edge-parallel atomics, then per workgroup a
 // contiguous node range (workgroup order = ascending ids) for the live list, its base from the
 // live counts of the lower workgroups.
+// dg: the degree arrays (2n words of gscr); zeroed: already zeroed (by the fixed point's init pass).
 __device__ bool team_features(KParams& p, Team& T, const EnvView<true>& E, int n, int* gdeg0, int* gdeg1, float* lv,
-                              float* q, EnvAgg& ag) {
+                              float* q, EnvAgg& ag, int* dg, bool zeroed) {
   const int e0 = E.e0;
   if (T.acc != nullptr && threadIdx.x == 0) T.t = wall_clock64();
-  for (int x = T.gt; x < n; x += T.gs) {
-    uf_store(E.par0, x, 0);
-    uf_store(E.par1, x, 0);
+  if (!zeroed) {
+    for (int x = T.gt; x < n; x += T.gs) {
+      uf_store(dg, x, 0);
+      uf_store(dg, n + x, 0);
+    }
+    if (grid_sync(p, *T.target, T.flag)) return true;
   }
-  if (grid_sync(p, *T.target, T.flag)) return true;
-  // (par1 follows par0: one index space l * n + node for the combined atomics)
+  // (layer 1's degrees follow layer 0's: one index space l * n + node for the combined atomics)
   for (int eb = T.gt - lane_id(); eb < E.et; eb += T.gs) {
     const int e = eb + lane_id();
     const bool on = e < E.et && E.state(e) == E_ALIVE;
     const int base = e < e0 ? 0 : n;
-    agg_add1(E.par0, on ? base + E.u(e) : 0, on);
-    agg_add1(E.par0, on ? base + E.v(e) : 0, on);
+    agg_add1(dg, on ? base + E.u(e) : 0, on);
+    agg_add1(dg, on ? base + E.v(e) : 0, on);
   }
   if (grid_sync(p, *T.target, T.flag)) return true;
   const int cw = (n + p.n_main - 1) / p.n_main;
@@ -1671,7 +1682,7 @@ __device__ bool team_features(KParams& p, Team& T, const EnvView<true>& E, int n
   const int x0 = min(w1, w0 + (int)threadIdx.x * ct), x1 = min(w1, x0 + ct);
   long long nlive = 0, dm0 = 0, dm1 = 0, sd0 = 0, sd1 = 0, bad = 0, th0 = 0, th1 = 0;
   for (int x = x0; x < x1; ++x) {
-    const int d0 = uf_load(E.par0, x), d1 = uf_load(E.par1, x);
+    const int d0 = uf_load(dg, x), d1 = uf_load(dg, n + x);
     stc(gdeg0 + x, d0);
     stc(gdeg1 + x, d1);
     stc(q + x, NEG_INF);
@@ -1693,7 +1704,7 @@ __device__ bool team_features(KParams& p, Team& T, const EnvView<true>& E, int n
   if (team_reduce<8>(p, T, v8, 0xc0u, t8, &before)) return true;
   int k = (int)before + off;
   for (int x = x0; x < x1; ++x) {
-    if (uf_load(E.par0, x) > 0) {
+    if (uf_load(dg, x) > 0) {
       const int b0 = E.grp[0][x], b1 = E.grp[1][x];
       const int x0e = E.grp[0][x + 1], x1e = E.grp[1][x + 1];
       if (MD_BOK(k < n, 9))
@@ -1724,7 +1735,9 @@ __device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_f
   GraphVar& gv = *(GraphVar*)(lds_base() + L_GV);
   const bool books = blockIdx.x == 0;
   const EnvView<true> E = env_view<true>(p, gi, (int*)(lds_base() + L_SCR));
-  int* cnt = p.gscr + 5 * (size_t)gi.node_off + 4 * n;
+  int* cnt = p.gscr + GSCR_WORDS * (size_t)gi.node_off + 4 * n;
+  int* dg = p.gscr + GSCR_WORDS * (size_t)gi.node_off + 7 * n;  // the features' degrees (2n)
+  bool zeroed = false;  // dg zeroed by a fixed point's init pass
   // every workgroup follows the same control flow: alive counts and s0 from the graph's
   // GraphVar as the last phase A stored it
   int alive0 = ldc(&p.gvar[g].alive[0]), alive1 = ldc(&p.gvar[g].alive[1]);
@@ -1739,7 +1752,8 @@ __device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_f
     int pr[2], c[2], lm = 0;
     // (workgroup 0 sets covered(a) after the fixed point's first barrier: every workgroup has
     // read it by then)
-    if (team_fixed_point(p, T, E, cnt, a, books, lm, pr, c)) return true;
+    if (team_fixed_point(p, T, E, cnt, a, books, lm, pr, c, zeroed ? nullptr : dg)) return true;
+    zeroed = true;
     alive0 -= c[0] + pr[0];
     alive1 -= c[1] + pr[1];
     if (books && threadIdx.x == 0) {
@@ -1760,7 +1774,8 @@ __device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_f
   }
   if (!s0_done && *err == 0) {
     int pr[2], lm = 0;
-    if (team_fixed_point(p, T, E, cnt, -1, false, lm, pr, nullptr)) return true;
+    if (team_fixed_point(p, T, E, cnt, -1, false, lm, pr, nullptr, zeroed ? nullptr : dg)) return true;
+    zeroed = true;
     if (books && threadIdx.x == 0) {
       gv.removed[0] += pr[0];
       gv.removed[1] += pr[1];
@@ -1771,7 +1786,7 @@ __device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_f
   }
   EnvAgg ag;
   if (team_features(p, T, E, n, p.deg[0] + gi.node_off, p.deg[1] + gi.node_off, (float*)(p.live + 4 * (size_t)gi.node_off),
-                    p.q + gi.node_off, ag))
+                    p.q + gi.node_off, ag, dg, zeroed))
     return true;
   if (books) {
     if (ag.bad && *err == 0) *err = ERR_LIVE_MISMATCH;
