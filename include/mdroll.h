@@ -209,60 +209,69 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
                        int64_t edge_cap, int64_t* amb_out, int64_t* amb_count, int64_t amb_cap);
 
 /*
- * Diagnostic environment knobs, read once by md_create.  None changes any result (every
- * combination is covered by the GPU tests, which check identical rollouts); they select
- * between equivalent execution strategies for A/B measurement and for exercising fallbacks:
+ * Environment switches, read once by md_create.  None changes any result: each selects between
+ * equivalent execution strategies (for A/B measurement and for exercising fallbacks), and each
+ * has a GPU identity test that checks identical rollouts (named after the switch):
  *   MD_VARIANT        bit mask, default 0:
- *                       1     single-graph rollouts: no iteration-1 prebuild during phase A (the
- *                             tiles build their rows, lists and iteration 1 after barrier A)
+ *                       1     single-graph rollouts: no iteration-1 prebuild during phase A
+ *                             (test_iteration1_prebuild_same_rollouts)
  *                       2     one graph too large for LDS: its environment step on one workgroup
- *                             (and through the work queue) instead of on every workgroup
- *                             (team_env_step); with 64 and MD_ENV_MODE=0 that step also runs
- *                             for graphs that fit
- *                       4     iteration-1 gathers read the graph's own first-layer table (phase A
- *                             copies the precomputed rows) instead of the precomputed table
- *                       8     per-piece queue-mode profile stamps (md_profile; qprof build)
- *                       16    no neighbour-list cache (every tile rebuilds its lists)
- *                       32    lock-step shared mode instead of the device work queue (> 16 graphs)
+ *                             instead of on every workgroup (team_env_step); with 64 and
+ *                             MD_ENV_MODE=0 that step also runs for graphs that fit
+ *                             (test_grid_wide_environment_step)
+ *                       32    lock-step shared mode instead of the device work queue (> 16
+ *                             graphs; the path batches with graphs of >= 8192 tiles take)
+ *                             (test_shared_mode_batch_matches_dedicated)
  *                       64    environment state in HBM even when it fits in LDS
- *                       128   iteration-1 prebuild limited to the rows and neighbour lists (the
- *                             first message-passing iteration runs after barrier A)
- *                       256   push single-item stages instead of running them inline (queue mode)
+ *                             (test_global_memory_environment_mode, test_grid_wide_environment_step)
+ *                       128   iteration-1 prebuild limited to the rows and neighbour lists
+ *                             (test_iteration1_prebuild_same_rollouts)
  *                       512..1536 (bits 9-10 = 1..3)  tiles per queue work item (default 2)
- *                       2048  K2 end-game shortcut off (one forward pass per removal step)
- *                       4096  queue mode: iteration-1 tiles build their own neighbour lists
- *                             instead of loading the ones the environment item wrote
- *                       bits 13-15 = k  queue-mode tail threshold at 16 k running graphs
- *                             (7: never; default 1/8 of the admission limit)
+ *                             (test_queue_admission_limit_matches_single)
+ *                       2048  K2 end-game shortcut off: one forward pass per removal step (the
+ *                             bench's per_step_protocol_value;
+ *                             test_k2_endgame_in_one_handshake_matches_per_step)
  *                       bits 16+  queue-mode admission limit (graphs running at once)
+ *                             (test_queue_admission_limit_matches_single)
  *   MD_ENV_MODE       0: no dedicated environment workgroups for small batches (shared
- *                     mode); default 1
+ *                     mode); default 1 (test_grid_wide_environment_step)
  *   MD_PAIR           0: queue-mode work items run their two tiles one after the other
- *                     instead of jointly (default 1)
+ *                     instead of jointly (default 1; test_paired_tiles_match_single_tiles)
  *   MD_QPARK          queue mode: once every graph is admitted and at most this many still
- *                     run, they continue in one lock-step launch (default 8, 0 = off, <= 16)
+ *                     run, they continue in one lock-step launch (default 8, 0 = off, <= 16;
+ *                     tests/test_gpu_batch.py test_tail_handoff_off_same_rollouts)
  *   MD_HOST_HANDSHAKE 0: end the launch on a tie and relaunch after the host selection
- *                     (default 1: in-kernel hand-shake through mapped host memory)
- *   MD_POLL_US        host-thread polling interval of the hand-shake (µs)
+ *                     (default 1: in-kernel hand-shake through mapped host memory;
+ *                     test_host_handshake_modes_same_rollouts)
  *   MD_H0G            0: rebuild the unit-cost first-layer tables per step instead of the
- *                     precomputed per-dmax tables
- *   MD_HOST_STATS     set: print hand-shake timing statistics to stderr
+ *                     precomputed per-dmax tables (test_precomputed_first_layer_tables)
  *   MD_SPEC           speculative environment workgroups of a single-graph rollout (0..32,
- *                     default 32, 0 = off; md_spec_stats)
+ *                     default 32, 0 = off; md_spec_stats; test_speculative_steps_match_plain)
  *   MD_EARLY          0: speculative workgroups wait for phase A's write-back and restage the
  *                     state instead of building the next state from the result phase A takes
+ *                     (test_speculative_steps_match_plain)
  *   MD_SPEC_ABORT     0: a speculative fixed point runs to the end even when phase A has taken
- *                     another result of its request (default 1: it stops after the round)
+ *                     another result of its request (default 1: it stops after the round;
+ *                     test_speculative_steps_match_plain)
  *   MD_DF             single-graph rollouts in dedicated mode with the layer split: 1 (default)
  *                     dataflow mode (no grid barrier, tagged hand-offs) whose tiles derive
  *                     phase A's pick from the arg-max partials and prebuild from it; 0 grid
  *                     barriers (the tiles prebuild from phase A's early word)
+ *                     (test_dataflow_mode_same_rollouts)
  *   MD_FP_SHORTCUT    0: every mutual-LMCC fixed point runs its confirmation round (default 1:
- *                     a pruned partition certified by its spanning forests ends the fixed point)
+ *                     a pruned partition certified by its spanning forests ends the fixed point;
+ *                     test_fixed_point_shortcut_same_rollouts)
  *   MD_FIRST_REQ      0: no speculative request at a rollout's first environment step (default
- *                     1: candidates ranked by residual degree, as no prediction exists yet)
+ *                     1: candidates ranked by residual degree, as no prediction exists yet;
+ *                     test_first_request_same_rollouts)
+ * Diagnostics and resources (no effect on any computation):
+ *   MD_VARIANT bit 8  per-piece queue-mode profile stamps (md_profile; qprof build)
+ *   MD_POLL_US        host-thread polling interval of the hand-shake (µs)
+ *   MD_HOST_STATS     set: print hand-shake timing statistics to stderr
  *   MD_PROF_ALL       md_profile_read returns every non-empty record row (the dataflow mode's
  *                     per-tile rows after the step records), not only the step records
+ *   MD_TRACE          1: every device allocation and kernel launch to stderr (maps a GPU
+ *                     memory-fault address to a buffer and a launch)
  *   MD_MAX_CUS        use at most this many CUs (>= 8; default: all), e.g. for several ranks
  *                     sharing one GPU, whose persistent grids must be co-resident
  */

@@ -124,6 +124,7 @@ struct md_ctx {
   DevBuf<uint8_t> estate[2], calive[2], covered;
   DevBuf<int> deg[2], live, gscr, pend, tr_action, tr_rank, tr_stat, glist, ctl;
   DevBuf<long long> tpart;  // grid-wide environment step: per-workgroup partials [2][TEAM_MAX_WG][16]
+  DevBuf<int> lab_ok;       // per graph: the grid-wide step's class labels are current
   DevBuf<float> H[2][2], h0tab[2], q, spart, apart, ybuf, hbuf, tr_q, node_w;
   DevBuf<unsigned long long> xbuf;
   DevBuf<int> nbc;  // neighbour-list cache slots (tiles of the largest launch)
@@ -196,7 +197,7 @@ struct md_ctx {
       H[l][0].release(); H[l][1].release();
     }
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
-    tr_stat.release(); glist.release(); gtoff.release(); ctl.release(); tpart.release(); q.release(); spart.release();
+    tr_stat.release(); glist.release(); gtoff.release(); ctl.release(); tpart.release(); lab_ok.release(); q.release(); spart.release();
     apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); nbc.release(); qslot.release(); qg.release(); tr_q.release(); node_w.release();
     sres.release(); qspec.release(); bars.release(); dfbuf.release();
     df_graph.clear();
@@ -258,6 +259,7 @@ Params make_params(md_ctx* c) {
   p.gscr = c->gscr.p;
   p.tpart = c->tpart.p;
   p.tctl = c->ctl.p + CTL_TEAM;
+  p.lab_ok = c->lab_ok.p;
   p.spart = c->spart.p;
   p.apart = c->apart.p;
   p.ybuf = c->ybuf.p;
@@ -514,7 +516,7 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
   // dataflow mode: a single-graph rollout in dedicated mode with the layer split, no grid
   // barrier (md_kernels.hip df_*; the graph qualified at load, MD_DF=0 keeps the barriers)
   const bool df = run_mode == RUN_ROLLOUT && n_env == 1 && ngl == 1 && !team_env && c->dfbuf.p != nullptr &&
-                  c->df_graph[gl[0]] && 2 * ((c->hinfo[gl[0]].n + TILE - 1) / TILE) <= grid - 2 && !(c->variant & 16);
+                  c->df_graph[gl[0]] && 2 * ((c->hinfo[gl[0]].n + TILE - 1) / TILE) <= grid - 2;
   HIPCHK(c, hipMemcpyAsync(c->glist.p, gl, sizeof(int) * ngl, hipMemcpyHostToDevice, c->stream));
   if (qmode) {
     // queue-mode neighbour-list cache slots: each graph slot's tiles from its launch prefix
@@ -990,6 +992,8 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->glist.alloc(n_graphs));
   HIPCHK(c, c->ctl.alloc(CTL_WORDS));
   if (c->tpart.p == nullptr) HIPCHK(c, c->tpart.alloc(2 * (size_t)TEAM_MAX_WG * 16));
+  HIPCHK(c, c->lab_ok.alloc(n_graphs));
+  HIPCHK(c, hipMemsetAsync(c->lab_ok.p, 0, sizeof(int) * n_graphs, c->stream));
   HIPCHK(c, c->bars.alloc(8 * 64));
   HIPCHK(c, c->spart.alloc(tt * 384));
   HIPCHK(c, c->apart.alloc(tt * 4));
@@ -1426,6 +1430,7 @@ md_status md_set_state(md_ctx* c, int graph, const uint8_t* covered, const uint8
     v.alive[l] = calive;
   }
   HIPCHK(c, hipMemcpy(c->covered.p + gi.node_off, covered, gi.n, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemset(c->lab_ok.p + graph, 0, sizeof(int)));  // the grid-wide step's class labels are stale
   v.n_cov = ncov;
   v.s0_done = 1;
   v.npend = 0;

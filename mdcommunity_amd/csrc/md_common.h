@@ -105,6 +105,8 @@ struct Params {
   int* gscr;                       // phase-A scratch in global memory for graphs too big for LDS: GSCR_WORDS per node
   long long* tpart;                // grid-wide environment step: per-workgroup partials [2][TEAM_MAX_WG][16]
   int* tctl;                       // grid-wide environment step: {actions (-1: none), first action}
+  int* lab_ok;                     // per graph: 1 while gscr's class labels and class sizes describe the
+                                   //   current state (team_env_step keeps them; every other state change clears)
   float* spart;                    // per tile: [3 sums][2 layers][64] virtual-node partial sums
   float* apart;                    // per tile: arg-max partial {max, second, idx, count}
   float* ybuf;                     // per graph: [2][64] virtual-node embedding after iteration 2
@@ -190,7 +192,7 @@ struct Params {
   int first_req;                   // 1: a rollout's first step requests degree-ranked speculative results (env_step)
 };
 // global-mode environment scratch words per node (md_env.h env_view, team_env_step)
-constexpr int GSCR_WORDS = 9;
+constexpr int GSCR_WORDS = 10;
 // dataflow buffer size (granules) for graphs of at most n nodes / mt tiles
 inline long long df_granules(int n, int mt) { return 64 + 772LL * mt + 8LL * 64 * n; }
 

@@ -1089,7 +1089,7 @@ __device__ __forceinline__ void h0_update(KParams& p, const GraphInfo& gi, Graph
       const int dm = l ? dm1 : dm0;
       if (dm == (l ? hd1 : hd0)) continue;
       float* tab = p.h0tab[l] + (size_t)gi.node_off * EMB;  // degrees <= n-1 fit the graph's rows
-      if (dm <= p.h0g_dm && p.h0g != nullptr && !(p.variant & 4)) continue;  // the tiles read the precomputed table
+      if (dm <= p.h0g_dm && p.h0g != nullptr) continue;  // the tiles read the precomputed table
       if (dm <= p.h0g_dm) {
         // the table of this dmax is precomputed (md_h0_kernel at load): a 16-byte copy
         const float* src = p.h0g + h0g_row(dm, 1) * EMB;
@@ -1169,6 +1169,8 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
   (void)et;  // bounds checks only
   int* ia = (int*)area;
   QENV_INIT();
+  // (this step changes the state without the grid-wide step's class labels: they go stale)
+  if (threadIdx.x == 0 && p.lab_ok != nullptr) stc(p.lab_ok + gi.gidx, 0);
   const EnvView<GL> E = env_view<GL>(p, gi, ia);
   if constexpr (!GL) {
     if (!staged) env_stage_lds(E, n);
@@ -1555,14 +1557,28 @@ __device__ bool team_reduce(KParams& p, Team& T, const long long (&v)[K], unsign
 // double-buffered by round (round r + 1's are reset during round r's label pass).  The edge set
 // each union pass sees, and so every partition, label and pruned edge, is the three-pass loop's.
 // deg_zero (the features' degree arrays, grid-wide scratch): zeroed in the init pass.
+// Class restriction (cls != nullptr, cover >= 0): cls[x] is x's class (its root label) in the
+// mutual partition the previous fixed point left, and cnt[r] the non-covered size of the class
+// rooted at r.  Every alive edge lies inside one class there (crossing edges were pruned), so
+// covering node a changes only a's class C_a: every other class stays connected in both layers
+// with no edge leaving it, hence a class of the new fixed point as well.  The passes then run on
+// C_a's nodes and edges alone (the others are skipped by their class), and the LMCC is the
+// largest of the untouched classes' sizes and the recounted sizes inside C_a -- the same fixed
+// point, pruned edges, labels and LMCC as the unrestricted loop (which runs when cls == nullptr
+// and establishes cls and cnt).  cls is updated to the new labels in the count pass.
 __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, int* cnt, int cover, bool set_cover, int& lm,
-                                 int* pr, int* cc, int* deg_zero = nullptr) {
+                                 int* pr, int* cc, int* deg_zero = nullptr, int* cls = nullptr, bool restrict_cls = false) {
   const int n = E.gi->n, et = E.et, e0 = E.e0;
   int* const pb[2][2] = {{E.par0, E.par1}, {E.par0 + 5 * n, E.par0 + 6 * n}};  // gscr: par0, par1 | par0', par1'
+  const bool rs = restrict_cls && cls != nullptr && cover >= 0;
+  const int La = rs ? uf_load(cls, cover) : -1;  // a's class
   if (T.acc != nullptr && threadIdx.x == 0) T.t = wall_clock64();
   for (int x = T.gt; x < n; x += T.gs) {
-    uf_store(pb[0][0], x, x);
-    uf_store(pb[0][1], x, x);
+    if (!rs || uf_load(cls, x) == La) {
+      uf_store(pb[0][0], x, x);
+      uf_store(pb[0][1], x, x);
+      uf_store(cnt, x, 0);  // (unrestricted: every class is recounted)
+    }
     if (deg_zero != nullptr) {
       uf_store(deg_zero, x, 0);
       uf_store(deg_zero, n + x, 0);
@@ -1572,6 +1588,20 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
   TEAM_ACC(T, 6);
   if (set_cover && cover >= 0 && threadIdx.x == 0) stc(E.gcov + cover, (uint8_t)1);  // read by the count pass
   pr[0] = pr[1] = 0;
+  // The thread's first edge (e = T.gt: the grid has at least as many threads as most graphs have
+  // edges) stays in registers for the whole fixed point -- alive flag, endpoints, class test --
+  // instead of three dependent loads per round: only this thread changes its state here.
+  const bool e1 = T.gt < et;
+  bool a1 = false;
+  int u1 = 0, v1 = 0;
+  if (e1) {
+    a1 = E.state(T.gt) == E_ALIVE;
+    u1 = E.u(T.gt);
+    v1 = E.v(T.gt);
+    if (a1 && rs && uf_load(cls, u1) != La) a1 = false;  // an edge of another class (both ends in it)
+  }
+  // (node passes likewise: the thread's first node's class test)
+  const bool x1in = T.gt < n && (!rs || uf_load(cls, T.gt) == La);
   for (int round = 0;; ++round) {
     const bool first = round == 0;
     int* const P0 = pb[round & 1][0];
@@ -1579,8 +1609,11 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
     long long k0 = 0, k1 = 0, c0 = 0, c1 = 0;
     if (T.prof_any != nullptr) T.t0any = wall_clock64();
     for (int e = T.gt; e < et; e += T.gs) {
-      if (E.state(e) != E_ALIVE) continue;
-      const int u = E.u(e), v = E.v(e);
+      const bool own = e == T.gt;
+      if (own ? !a1 : E.state(e) != E_ALIVE) continue;
+      const int u = own ? u1 : E.u(e), v = own ? v1 : E.v(e);
+      if (!own && rs && uf_load(cls, u) != La) continue;  // an edge of another class (both ends in it)
+      if (own) a1 = false;  // (set again below when it stays alive)
       if (!first) {
         // the previous round's prune: layer-0 edges by the layer-1 components and vice versa
         auto other = e < e0 ? E.deg1 : E.deg0;
@@ -1595,10 +1628,9 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
         if (e < e0) k0++; else k1++;
       } else {
         uf_unite_h(e < e0 ? P0 : P1, u, v);
+        if (own) a1 = true;
       }
     }
-    if (first)  // LMCC counters, used after the last round
-      for (int x = T.gt; x < n; x += T.gs) uf_store(cnt, x, 0);
     if (T.acc != nullptr) {  // diagnostics: workgroup 0's own union work (slot 88), before the barrier
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -1617,6 +1649,7 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
     int* const Q1 = pb[(round + 1) & 1][1];
     long long diff = 0;
     for (int x = T.gt; x < n; x += T.gs) {
+      if (x == T.gt ? !x1in : (rs && uf_load(cls, x) != La)) continue;  // labels of the untouched classes stay
       const int r0 = uf_find_h(P0, x), r1 = uf_find_h(P1, x);
       uf_store(E.deg0, x, r0);
       uf_store(E.deg1, x, r1);
@@ -1638,11 +1671,18 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
   }
   // the LMCC: non-covered nodes per component (layer-0 label = layer-1 label at the fixed point);
   // the largest count is the maximum over the adds' results (each word's last add sees its total)
+  // (restricted: the untouched classes' sizes from cnt at their roots, C_a's recounted; cls takes
+  // the new labels)
   long long best = 0;
   for (int xb = T.gt - lane_id(); xb < n; xb += T.gs) {
     const int x = xb + lane_id();
-    const bool on = x < n && !E.covered(x);
-    best = max(best, (long long)agg_add1_max(cnt, on ? uf_load(E.deg0, x) : 0, on));
+    const int cx = x < n && rs ? uf_load(cls, x) : La;
+    const bool mine = x < n && cx == La;  // (unrestricted: every node)
+    if (x < n && !mine && cx == x) best = max(best, (long long)uf_load(cnt, x));
+    const int lab = mine ? uf_load(E.deg0, x) : 0;
+    const bool on = mine && !E.covered(x);
+    best = max(best, (long long)agg_add1_max(cnt, on ? lab : 0, on));
+    if (mine && cls != nullptr) uf_store(cls, x, lab);
   }
   const long long vb[1] = {best};
   long long tb[1];
@@ -1737,11 +1777,16 @@ __device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_f
   const EnvView<true> E = env_view<true>(p, gi, (int*)(lds_base() + L_SCR));
   int* cnt = p.gscr + GSCR_WORDS * (size_t)gi.node_off + 4 * n;
   int* dg = p.gscr + GSCR_WORDS * (size_t)gi.node_off + 7 * n;  // the features' degrees (2n)
+  int* cls = p.gscr + GSCR_WORDS * (size_t)gi.node_off + 9 * n;  // class labels (team_fixed_point)
   bool zeroed = false;  // dg zeroed by a fixed point's init pass
+
   // every workgroup follows the same control flow: alive counts and s0 from the graph's
   // GraphVar as the last phase A stored it
   int alive0 = ldc(&p.gvar[g].alive[0]), alive1 = ldc(&p.gvar[g].alive[1]);
   const int s0_done = ldc(&p.gvar[g].s0_done);
+  // the class labels and sizes are current when the last state change was this step's (every
+  // workgroup reads the flag before workgroup 0 can set it: the first fixed point's barrier)
+  bool labels = p.lab_ok != nullptr && ldc(p.lab_ok + g) != 0 && s0_done;
   *err = 0;
   for (int k = 0; k < pend_n; ++k) {
     if (alive0 == 0 || alive1 == 0) break;  // terminal between queued actions
@@ -1752,8 +1797,9 @@ __device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_f
     int pr[2], c[2], lm = 0;
     // (workgroup 0 sets covered(a) after the fixed point's first barrier: every workgroup has
     // read it by then)
-    if (team_fixed_point(p, T, E, cnt, a, books, lm, pr, c, zeroed ? nullptr : dg)) return true;
+    if (team_fixed_point(p, T, E, cnt, a, books, lm, pr, c, zeroed ? nullptr : dg, cls, labels)) return true;
     zeroed = true;
+    labels = true;
     alive0 -= c[0] + pr[0];
     alive1 -= c[1] + pr[1];
     if (books && threadIdx.x == 0) {
@@ -1774,8 +1820,9 @@ __device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_f
   }
   if (!s0_done && *err == 0) {
     int pr[2], lm = 0;
-    if (team_fixed_point(p, T, E, cnt, -1, false, lm, pr, nullptr, zeroed ? nullptr : dg)) return true;
+    if (team_fixed_point(p, T, E, cnt, -1, false, lm, pr, nullptr, zeroed ? nullptr : dg, cls, false)) return true;
     zeroed = true;
+    labels = true;
     if (books && threadIdx.x == 0) {
       gv.removed[0] += pr[0];
       gv.removed[1] += pr[1];
@@ -1784,6 +1831,9 @@ __device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_f
       gv.s0_done = 1;
     }
   }
+  // the labels stay current for the next step only when every fixed point ran here (a step with
+  // no fixed point, e.g. a terminal graph's queued action, changes nothing)
+  if (books && threadIdx.x == 0 && p.lab_ok != nullptr) stc(p.lab_ok + g, (labels && *err == 0) ? 1 : 0);
   EnvAgg ag;
   if (team_features(p, T, E, n, p.deg[0] + gi.node_off, p.deg[1] + gi.node_off, (float*)(p.live + 4 * (size_t)gi.node_off),
                     p.q + gi.node_off, ag, dg, zeroed))

@@ -909,7 +909,7 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
 // then copies nothing -- else the graph's own table, rebuilt by phase A.  The dmax load goes
 // out beside the degree loads it is needed with.
 __device__ __forceinline__ const float* first_layer_rows(KParams& p, const GraphInfo& gi, int l) {
-  if (p.h0g != nullptr && !(p.variant & 4)) {  // MD_VARIANT bit 4: the graph's own table (phase A copies)
+  if (p.h0g != nullptr) {
     const int dm = ldc(&p.gvar[gi.gidx].dmax[l]);
     if (dm >= 1 && dm <= p.h0g_dm) return p.h0g + (h0g_row(dm, 1) - 1) * EMB;  // row d at base + d rows
   }
@@ -1756,7 +1756,7 @@ __device__ __forceinline__ bool spec_iteration1(KParams&, const GraphInfo gi, in
   int dm = 0x7fffffff;
   if (p.node_w == nullptr) {  // unit cost: rows by degree, from the precomputed table of the result's dmax
     dm = ((const int*)(lds + L_MISC))[40];  // (read by prebuild_lists, which runs just before)
-    if (p.h0g == nullptr || (p.variant & 4) || dm < 1 || dm > p.h0g_dm) return false;
+    if (p.h0g == nullptr || dm < 1 || dm > p.h0g_dm) return false;
     hp = p.h0g + (h0g_row(dm, 1) - 1) * EMB;
   }
   gather_tile2s(p, gi, 1, rows, scr, L, sl + sres_deg(et) + L * n, hp, dm);
@@ -2560,15 +2560,11 @@ __device__ __forceinline__ int q_tiles_per_item(KParams& p) {
   const int f = (p.variant >> 9) & 3;
   return f == 0 ? 2 : f;
 }
-// In the launch's tail (every graph admitted and at most q_tail(p) still running) a step's
-// tiles go one per item: fewer graphs share the chip, so each stage's items are spread over
-// more workgroups (per graph and step the tiles per item are fixed: qg word bits 28-29).
-// MD_VARIANT bits 13-15 = k set the tail at 16 k running graphs (7: never), default 1/8 of
-// the workgroups.
-__device__ __forceinline__ int q_tail(KParams& p) {
-  const int v = (p.variant >> 13) & 7;
-  return v == 0 ? (int)gridDim.x / 8 : (v == 7 ? -1 : 16 * v);
-}
+// In the launch's tail (every graph admitted and at most 1/8 of the workgroups' count still
+// running) a step's tiles go one per item: fewer graphs share the chip, so each stage's items
+// are spread over more workgroups (per graph and step the tiles per item are fixed: qg word
+// bits 28-29).
+__device__ __forceinline__ int q_tail(KParams&) { return (int)gridDim.x / 8; }
 // Pushes n items f(0..n-1); every thread of the workgroup calls it.  The ring's head / tail
 // tickets sit on a line of their own (p.qring); Q_CAP slots.
 __device__ __forceinline__ g_u32* q_ctl(KParams& p) { return (g_u32*)p.qring; }
@@ -2819,10 +2815,10 @@ __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int
     }                                                             \
   } while (0)
   const int slot = p.gtoff[gl] + j;  // neighbour-list cache slot: the graph's tile within the launch
-  const bool cacheable = slot < p.nbc_slots && !(p.variant & 16);
+  const bool cacheable = slot < p.nbc_slots;
   // iteration 1: the environment item built this step's lists when its flag says so (read in
   // the same round trip as the speculative reload)
-  const bool want = cacheable && (it > 1 || !(p.variant & 4096));
+  const bool want = cacheable;
   int cw = 0, ch = 0, built = 0;
   if (want) {
     const int* src = p.nbc + (size_t)slot * NBC_INTS;
@@ -2866,7 +2862,7 @@ __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int
       __syncthreads();
     }
   } else {
-    nb_ok = !(p.variant & 16) && build_nb_lists(p, gi, rows, scr, nullptr, -1);
+    nb_ok = build_nb_lists(p, gi, rows, scr, nullptr, -1);
     if (cacheable) nbc_store(p, slot, scr, nb_ok);
   }
   QTS(1);
@@ -3539,8 +3535,8 @@ __device__ __noinline__ void queue_pair(KParams&, float* lds, int g, int gl, int
   bool cacheable[2], want[2];
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
-    cacheable[b] = slot0 + b < p.nbc_slots && !(p.variant & 16);
-    want[b] = cacheable[b] && (it > 1 || !(p.variant & 4096));
+    cacheable[b] = slot0 + b < p.nbc_slots;
+    want[b] = cacheable[b];
   }
   // both tiles' cached lists (first 256 words per layer), headers and the "built" flag in one
   // round trip, with the rows from the live list
@@ -3599,7 +3595,7 @@ __device__ __noinline__ void queue_pair(KParams&, float* lds, int g, int gl, int
         __syncthreads();
       }
     } else {
-      nb_ok[b] = !(p.variant & 16) && build_nb_lists(p, gi, nullptr, nullptr, nullptr, -1, false, nbo[b], P2_FLAG + 8);
+      nb_ok[b] = build_nb_lists(p, gi, nullptr, nullptr, nullptr, -1, false, nbo[b], P2_FLAG + 8);
       if (cacheable[b]) nbc_store(p, slot0 + b, scr, nb_ok[b], nbo[b]);
     }
   }
@@ -3721,8 +3717,7 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
   // A single-item stage that a workgroup enables (virtual-node part 2 after the last
   // iteration-2 task, the environment step after the last iteration-3 tile) runs on that
   // workgroup right away instead of queueing behind the backlog: one queue wait less on the
-  // graph's critical path per stage (MD_VARIANT bit 256 pushes them instead).
-  const bool inline_cont = !(p.variant & 256);
+  // graph's critical path per stage.
   unsigned cont = 0u;
   while (true) {
     unsigned item;
@@ -3794,13 +3789,13 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
         __syncthreads();
         const int tpi = bc[5];
         const int nt = (nl + TILE - 1) / TILE, ni = (nt + tpi - 1) / tpi;
-        // this step's neighbour lists for the iteration-1 tiles (MD_VARIANT bit 12: off)
+        // this step's neighbour lists for the iteration-1 tiles
 #ifdef MD_QPROF
         const unsigned long long tqb = wall_clock64();
 #endif
         // (in the tail -- one tile per item -- the iteration-1 tiles build their own lists: the
         // environment item is on the graph's critical path and most workgroups are idle)
-        const bool built = lds_env && !(p.variant & (4096 | 16)) && tpi > 1 && env_build_lists(p, p.ginfo[g], gl);
+        const bool built = lds_env && tpi > 1 && env_build_lists(p, p.ginfo[g], gl);
 #ifdef MD_QPROF
         if (qp != nullptr && (p.variant & 8) && threadIdx.x == 0) atomicAdd(qp + 86, wall_clock64() - tqb);
 #endif
@@ -3873,11 +3868,9 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
       if (next == 1) {
         q_push(p, ni + 1, [&](int i) { return i < ni ? q_item_tile(2, gl, i, nt, tpi) : q_item(QK_VN, 1, gl, 0); }, bc);
       } else if (next == 2) {
-        if (inline_cont) cont = q_item(QK_VN, 2, gl, 0);
-        else q_push(p, 1, [&](int) { return q_item(QK_VN, 2, gl, 0); }, bc);
+        cont = q_item(QK_VN, 2, gl, 0);
       } else if (next == 3) {
-        if (inline_cont) cont = q_item(QK_ENV, 1, gl, 0);
-        else q_push(p, 1, [&](int) { return q_item(QK_ENV, 1, gl, 0); }, bc);
+        cont = q_item(QK_ENV, 1, gl, 0);
       } else q_push(p, ni, [&](int i) { return q_item_tile(3, gl, i, nt, tpi); }, bc);
     }
     if (qp != nullptr && threadIdx.x == 0) atomicAdd(qp + (kind == QK_TILE ? 4 + it : kind == QK_VN ? 2 + it : kind), (tq = wall_clock64()) - ti);
@@ -4873,7 +4866,7 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
         // several tiles per workgroup: iteration 1 caches the tile's neighbour lists in HBM
         // (slot t), iterations 2-3 reload them with the rows (first 256 words per layer
         // speculatively, the rest only when a layer has more than 512 entries)
-        const bool multi = (t1 - t0 > 1 || !ded) && t < p.nbc_slots && !(p.variant & 16);
+        const bool multi = (t1 - t0 > 1 || !ded) && t < p.nbc_slots;
         const bool cached = multi && it > 1;
         int cw = 0, ch = 0;
         if (cached) {
@@ -4938,7 +4931,7 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
           } else if (prebuilt) {
             nb_ok = pre_ok == 1;  // (2: lists over NB_CAP, the per-row gather)
           } else if (it == 1 || t1 - t0 > 1 || !ded) {
-            nb_ok = !(p.variant & 16) && build_nb_lists(p, gi, rows, scr, ts, sit ? L : -1);
+            nb_ok = build_nb_lists(p, gi, rows, scr, ts, sit ? L : -1);
             if (multi) nbc_store(p, t, scr, nb_ok);
           }
           TSTAMP(55);
@@ -5143,6 +5136,7 @@ __global__ void md_reset_kernel(Params p) {
     v.status = ST_RUN;
     v.argmax = -1;
     p.gvar[g] = v;
+    p.lab_ok[g] = 0;
   }
 }
 

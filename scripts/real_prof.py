@@ -63,6 +63,8 @@ if len(T):
     print("  team step: rounds median %.0f mean %.2f; median us %s" % (
         np.median(T[:, 80]), T[:, 80].mean(), "  ".join("%s %.1f" % (k, np.median(T[:, 81 + i]) / 100) for i, k in enumerate(nm))),
           flush=True)
+    print("  union pass per round: workgroup 0's own work %.1f us, slowest workgroup's %.1f us (median over steps)" % (
+        np.median(T[:, 88] / rd) / 100, np.median(T[:, 89]) / 100), flush=True)
     print("  team step per round us: union %.1f label %.1f prune %.1f" % (
         np.median(T[:, 81] / rd) / 100, np.median(T[:, 82] / rd) / 100, np.median(T[:, 83] / np.maximum(rd - 1, 1)) / 100),
           flush=True)

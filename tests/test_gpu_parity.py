@@ -168,9 +168,11 @@ def test_errors_are_reported(eng):
         eng.load_graphs([(3, np.array([[0, 0]]), np.array([[0, 1]]))])  # self-loop
 
 
-def test_shared_mode_batch_matches_dedicated(eng):
-    """A launch of more than 16 graphs takes the shared phase-A path (every workgroup steps
-    graphs, then tiles); its rollouts equal the dedicated-workgroup path of single graphs."""
+def test_shared_mode_batch_matches_dedicated(eng, monkeypatch):
+    """A launch of more than 16 graphs runs through the device work queue, and with MD_VARIANT
+    bit 32 in the lock-step shared mode (every workgroup steps graphs, then tiles: the path of
+    batches whose graphs exceed the queue's tile field); both equal the dedicated-workgroup path
+    of single graphs."""
     names = ["gmm200_s7", "er100", "er300_dense"]
     zs = [load_golden(nm) for nm in names]
     graphs = [(int(z["n_nodes"]), z["edges0"], z["edges1"]) for z in zs]
@@ -186,6 +188,68 @@ def test_shared_mode_batch_matches_dedicated(eng):
     out = eng.rollout()
     for i, (s, r) in enumerate(out):
         assert (s.tolist(), r.tolist()) == single[i % 3], i
+    monkeypatch.setenv("MD_VARIANT", "32")
+    e = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
+    try:
+        e.load_graphs(batch)
+        e.reset()
+        out = e.rollout()
+        for i, (s, r) in enumerate(out):
+            assert (s.tolist(), r.tolist()) == single[i % 3], ("lock-step shared", i)
+    finally:
+        e.close()
+
+
+def test_host_handshake_modes_same_rollouts(monkeypatch):
+    """MD_HOST_HANDSHAKE=0 (a tie ends the launch; the host selects and relaunches) gives the
+    rollouts of the in-kernel hand-shake: single graphs with ties and end-games, and a 18-graph
+    queue-mode batch."""
+    names = ["gmm1000_s0", "gmm1000_s1", "er300_dense"]
+    graphs = [(int(z["n_nodes"]), z["edges0"], z["edges1"]) for z in map(load_golden, names)]
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MD_HOST_HANDSHAKE", mode)
+        e = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
+        try:
+            res = []
+            for g in graphs:
+                e.load_graphs([g])
+                e.reset()
+                res += [(s.tolist(), r.tolist()) for s, r in e.rollout()]
+            e.load_graphs([graphs[i % 3] for i in range(18)])
+            e.reset()
+            res += [(s.tolist(), r.tolist()) for s, r in e.rollout()]
+            out[mode] = res
+        finally:
+            e.close()
+    assert out["0"] == out["1"]
+
+
+def test_first_request_same_rollouts(monkeypatch):
+    """MD_FIRST_REQ=0 (no speculative request at a rollout's first environment step) gives the
+    rollouts of the default degree-ranked first request (single graphs, dataflow and barrier
+    modes)."""
+    names = ["gmm1000_s0", "gmm200_s7", "er300_dense"]
+    graphs = [(int(z["n_nodes"]), z["edges0"], z["edges1"]) for z in map(load_golden, names)]
+    out = {}
+    for fr in ("1", "0"):
+        for df in ("1", "0"):
+            monkeypatch.setenv("MD_FIRST_REQ", fr)
+            monkeypatch.setenv("MD_DF", df)
+            e = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
+            try:
+                res = []
+                for g in graphs:
+                    e.load_graphs([g])
+                    for _ in range(2):
+                        e.reset_deferred()
+                        res += [(s.tolist(), r.tolist()) for s, r in e.rollout()]
+                out[(fr, df)] = res
+            finally:
+                e.close()
+    base = out[("1", "1")]
+    for k, v in out.items():
+        assert v == base, k
 
 
 @pytest.mark.parametrize("admit,tpi", [(1, 2), (4, 1), (4, 3), (64, 2)])
