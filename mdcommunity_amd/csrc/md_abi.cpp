@@ -125,6 +125,7 @@ struct md_ctx {
   DevBuf<int> deg[2], live, gscr, pend, tr_action, tr_rank, tr_stat, glist, ctl;
   DevBuf<long long> tpart;  // grid-wide environment step: per-workgroup partials [2][TEAM_MAX_WG][16]
   DevBuf<int> lab_ok;       // per graph: the grid-wide step's class labels are current
+  DevBuf<uint16_t> prank;   // static union ranks (team_env_step), graphs of <= 65535 nodes
   DevBuf<float> H[2][2], h0tab[2], q, spart, apart, ybuf, hbuf, tr_q, node_w;
   DevBuf<unsigned long long> xbuf;
   DevBuf<int> nbc;  // neighbour-list cache slots (tiles of the largest launch)
@@ -197,7 +198,7 @@ struct md_ctx {
       H[l][0].release(); H[l][1].release();
     }
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
-    tr_stat.release(); glist.release(); gtoff.release(); ctl.release(); tpart.release(); lab_ok.release(); q.release(); spart.release();
+    tr_stat.release(); glist.release(); gtoff.release(); ctl.release(); tpart.release(); lab_ok.release(); prank.release(); q.release(); spart.release();
     apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); nbc.release(); qslot.release(); qg.release(); tr_q.release(); node_w.release();
     sres.release(); qspec.release(); bars.release(); dfbuf.release();
     df_graph.clear();
@@ -260,6 +261,7 @@ Params make_params(md_ctx* c) {
   p.tpart = c->tpart.p;
   p.tctl = c->ctl.p + CTL_TEAM;
   p.lab_ok = c->lab_ok.p;
+  p.prank = c->prank.p;
   p.spart = c->spart.p;
   p.apart = c->apart.p;
   p.ybuf = c->ybuf.p;
@@ -951,6 +953,38 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
       }
     }
   }
+  // static union ranks of the grid-wide environment step (md_env.h uf_unite_r): per graph the
+  // nodes ordered by descending static degree (both layers), ties by the hashed priority
+  // (uf_pri), rank = position; every graph's block starts at an even index
+  std::vector<uint16_t> ranks;
+  {
+    // (only graphs the grid-wide step can run: too large for LDS, or any graph of a small batch,
+    // where MD_VARIANT=64 forces that step; rank_off = -1 otherwise)
+    size_t off = 0;
+    for (int g = 0; g < n_graphs; ++g) {
+      const bool want = info[g].n <= 65535 &&
+                        (n_graphs <= DEDICATED_MAX_GRAPHS || !phase_a_fits_lds_host(info[g].n, info[g].e[0] + info[g].e[1]));
+      info[g].rank_off = want ? (int)off : -1;
+      if (want) off += (size_t)((info[g].n + 1) & ~1);
+    }
+    ranks.assign(std::max<size_t>(2, off), 0);
+    std::vector<int> ord;
+    for (int g = 0; g < n_graphs; ++g) {
+      const GraphInfo& gi = info[g];
+      if (gi.rank_off < 0) continue;
+      const int* r0 = rowptr[0].data() + gi.roff[0];
+      const int* r1 = rowptr[1].data() + gi.roff[1];
+      ord.resize(gi.n);
+      for (int x = 0; x < gi.n; ++x) ord[x] = x;
+      auto deg = [&](int x) { return (r0[x + 1] - r0[x]) + (r1[x + 1] - r1[x]); };
+      std::sort(ord.begin(), ord.end(), [&](int a, int b) {
+        const int da = deg(a), db = deg(b);
+        if (da != db) return da > db;
+        return (unsigned)a * 2654435761u < (unsigned)b * 2654435761u;
+      });
+      for (int k = 0; k < gi.n; ++k) ranks[gi.rank_off + ord[k]] = (uint16_t)k;
+    }
+  }
   c->ng = n_graphs;
   c->hinfo = info;
   c->hvar.assign(n_graphs, GraphVar{});
@@ -993,6 +1027,8 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->ctl.alloc(CTL_WORDS));
   if (c->tpart.p == nullptr) HIPCHK(c, c->tpart.alloc(2 * (size_t)TEAM_MAX_WG * 16));
   HIPCHK(c, c->lab_ok.alloc(n_graphs));
+  HIPCHK(c, c->prank.alloc(ranks.size()));
+  HIPCHK(c, hipMemcpyAsync(c->prank.p, ranks.data(), sizeof(uint16_t) * ranks.size(), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->lab_ok.p, 0, sizeof(int) * n_graphs, c->stream));
   HIPCHK(c, c->bars.alloc(8 * 64));
   HIPCHK(c, c->spart.alloc(tt * 384));

@@ -59,6 +59,7 @@ struct GraphInfo {           // immutable after md_load_graphs
   int coff[2];               // into CSR entry arrays (2 e entries per graph)
   int tile_off;              // into per-tile arrays (ceil(n / 16) tiles per graph)
   int gidx;                  // the graph's index (its GraphVar)
+  int rank_off;              // into the static union ranks (even: read as u32 pairs)
 };
 
 struct GraphVar {            // mutable per-graph state
@@ -105,6 +106,7 @@ struct Params {
   int* gscr;                       // phase-A scratch in global memory for graphs too big for LDS: GSCR_WORDS per node
   long long* tpart;                // grid-wide environment step: per-workgroup partials [2][TEAM_MAX_WG][16]
   int* tctl;                       // grid-wide environment step: {actions (-1: none), first action}
+  const uint16_t* prank;           // per node: static union rank (descending degree; team_env_step), or null
   int* lab_ok;                     // per graph: 1 while gscr's class labels and class sizes describe the
                                    //   current state (team_env_step keeps them; every other state change clears)
   float* spart;                    // per tile: [3 sums][2 layers][64] virtual-node partial sums

@@ -13,6 +13,7 @@
 typedef __attribute__((address_space(3))) int lds_i32;
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) unsigned lds_u32;
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v2u lds_u2;
@@ -171,6 +172,23 @@ __device__ __forceinline__ void uf_unite_h(P par, int a, int b) {
     b = uf_find_h(par, b);
     if (a == b) return;
     if (uf_pri(a) > uf_pri(b)) { const int t = a; a = b; b = t; }
+    if (uf_cas(par, b, b, a) == b) return;
+  }
+}
+// uf_unite_h with the priority of a static rank (rk, LDS): node x's position when the graph's
+// nodes are ordered by descending static degree (both layers), ties by uf_pri.  A hub is the
+// root of its tree from its first union on, so its neighbours hook under it with a
+// compare-and-swap on their OWN parent word: with the hashed priority, a hub's root was in turn
+// the larger-priority side of many concurrent unions, every one retrying its compare-and-swap on
+// that one word (the union pass's stragglers at N = 18 000).  Roots are still one canonical node
+// per node set (the least rank), the same in both layers.
+template <class P>
+__device__ __forceinline__ void uf_unite_r(P par, int a, int b, const lds_u16* rk) {
+  while (true) {
+    a = uf_find_h(par, a);
+    b = uf_find_h(par, b);
+    if (a == b) return;
+    if (rk[a] > rk[b]) { const int t = a; a = b; b = t; }
     if (uf_cas(par, b, b, a) == b) return;
   }
 }
@@ -1567,7 +1585,8 @@ __device__ bool team_reduce(KParams& p, Team& T, const long long (&v)[K], unsign
 // point, pruned edges, labels and LMCC as the unrestricted loop (which runs when cls == nullptr
 // and establishes cls and cnt).  cls is updated to the new labels in the count pass.
 __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, int* cnt, int cover, bool set_cover, int& lm,
-                                 int* pr, int* cc, int* deg_zero = nullptr, int* cls = nullptr, bool restrict_cls = false) {
+                                 int* pr, int* cc, int* deg_zero = nullptr, int* cls = nullptr, bool restrict_cls = false,
+                                 const lds_u16* rk = nullptr) {
   const int n = E.gi->n, et = E.et, e0 = E.e0;
   int* const pb[2][2] = {{E.par0, E.par1}, {E.par0 + 5 * n, E.par0 + 6 * n}};  // gscr: par0, par1 | par0', par1'
   const bool rs = restrict_cls && cls != nullptr && cover >= 0;
@@ -1627,7 +1646,8 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
         E.kill(e, E_COVERED);
         if (e < e0) k0++; else k1++;
       } else {
-        uf_unite_h(e < e0 ? P0 : P1, u, v);
+        if (rk != nullptr) uf_unite_r(e < e0 ? P0 : P1, u, v, rk);
+        else uf_unite_h(e < e0 ? P0 : P1, u, v);
         if (own) a1 = true;
       }
     }
@@ -1787,6 +1807,17 @@ __device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_f
   // the class labels and sizes are current when the last state change was this step's (every
   // workgroup reads the flag before workgroup 0 can set it: the first fixed point's barrier)
   bool labels = p.lab_ok != nullptr && ldc(p.lab_ok + g) != 0 && s0_done;
+  // the static union ranks (md_abi.cpp, at load) in the tile scratch, free during the step (after
+  // the team's own reduction words)
+  const lds_u16* rk = nullptr;
+  if (p.prank != nullptr && gi.rank_off >= 0 && n <= TEAM_RANK_MAX) {
+    lds_u16* dst = (lds_u16*)(uint16_t*)(lds_base() + L_SCR + TEAM_RANK_OFF);
+    const unsigned* src = (const unsigned*)(p.prank + gi.rank_off);  // (rank_off even)
+    const int nw = (n + 1) >> 1;
+    for (int i = threadIdx.x; i < nw; i += NTHREADS) ((lds_u32*)(unsigned*)dst)[i] = src[i];
+    __syncthreads();
+    rk = dst;
+  }
   *err = 0;
   for (int k = 0; k < pend_n; ++k) {
     if (alive0 == 0 || alive1 == 0) break;  // terminal between queued actions
@@ -1797,7 +1828,7 @@ __device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_f
     int pr[2], c[2], lm = 0;
     // (workgroup 0 sets covered(a) after the fixed point's first barrier: every workgroup has
     // read it by then)
-    if (team_fixed_point(p, T, E, cnt, a, books, lm, pr, c, zeroed ? nullptr : dg, cls, labels)) return true;
+    if (team_fixed_point(p, T, E, cnt, a, books, lm, pr, c, zeroed ? nullptr : dg, cls, labels, rk)) return true;
     zeroed = true;
     labels = true;
     alive0 -= c[0] + pr[0];
@@ -1820,7 +1851,7 @@ __device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_f
   }
   if (!s0_done && *err == 0) {
     int pr[2], lm = 0;
-    if (team_fixed_point(p, T, E, cnt, -1, false, lm, pr, nullptr, zeroed ? nullptr : dg, cls, false)) return true;
+    if (team_fixed_point(p, T, E, cnt, -1, false, lm, pr, nullptr, zeroed ? nullptr : dg, cls, false, rk)) return true;
     zeroed = true;
     labels = true;
     if (books && threadIdx.x == 0) {

@@ -88,6 +88,10 @@ constexpr int NB_CAP = NB_CAP_ENTRIES;      // alive neighbour entries per layer
 constexpr int S_END = S_NBL + NB_CAP;
 constexpr int STG_ROWS = 68;                // neighbour rows per layer staged per batch ([S_M, S_HID))
 constexpr int L_TOTAL = L_SCR + S_END;      // floats of dynamic LDS per workgroup
+// grid-wide environment step (md_env.h team_env_step) in the tile scratch: env_view's block-scan
+// temp at 0, the team reductions' words at TEAM_TMP_OFF, the static union ranks (u16) after them
+constexpr int TEAM_TMP_OFF = 1024, TEAM_RANK_OFF = 2048;
+constexpr int TEAM_RANK_MAX = 2 * (S_END - TEAM_RANK_OFF);  // nodes whose ranks fit
 // Paired tiles (queue mode, md_kernels.hip queue_pair): the two tiles of a 2-tile work item run
 // every piece once for their 32 rows.  Transposed blocks [layer][row block][K][LDT] (a row
 // block = one tile's 16 rows, the single-tile layout twice); M aliases P and X once their
@@ -4702,7 +4706,7 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
         T.use = 0;
         T.target = &target;
         T.flag = bflag;
-        T.tmp = (int*)(scr + S_M);
+        T.tmp = (int*)(scr + TEAM_TMP_OFF);
         T.acc = nullptr;
         T.t = 0;
         T.prof_any = p.prof != nullptr && pstep < p.prof_cap ? p.prof + (size_t)pstep * PROF_SLOTS + 80 : nullptr;
