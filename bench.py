@@ -863,6 +863,10 @@ def rank_main(args):
             "ms_per_step": max_elapsed / max(1, args.steps) * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
+            "value_note": "replica weak scaling: each rank rolls out its own copy of the headline graph (a "
+                          "single-graph rollout does not shard); the strong-scaled north_star figure is "
+                          "c5.value (4096 graphs split over the ranks), its 8-GPU prediction "
+                          "c5.rank_shard_at_8.predicted_8_gpu_ratio",
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic (GMM generator = reference U/GMM.py streams; random seed graphs)",

@@ -192,6 +192,34 @@ __device__ __forceinline__ void uf_unite_r(P par, int a, int b, const lds_u16* r
     if (uf_cas(par, b, b, a) == b) return;
   }
 }
+// diagnostics (md_profile): uf_unite_r counting its parent loads and compare-and-swaps (ops)
+// and its failed compare-and-swaps (fails)
+template <class P>
+__device__ __forceinline__ int uf_find_hc(P par, int v, int& ops) {
+  int cur = uf_load(par, v);
+  ++ops;
+  if (cur != v) {
+    int prev = v, next;
+    while (++ops, cur != (next = uf_load(par, cur))) {
+      uf_store(par, prev, next);
+      prev = cur;
+      cur = next;
+    }
+  }
+  return cur;
+}
+template <class P>
+__device__ __forceinline__ void uf_unite_rc(P par, int a, int b, const lds_u16* rk, int& ops, int& fails) {
+  while (true) {
+    a = uf_find_hc(par, a, ops);
+    b = uf_find_hc(par, b, ops);
+    if (a == b) return;
+    if (rk[a] > rk[b]) { const int t = a; a = b; b = t; }
+    ++ops;
+    if (uf_cas(par, b, b, a) == b) return;
+    ++fails;
+  }
+}
 
 // ------------------------------------------------------------------ layout and view
 // LDS layout of a graph's environment (words from the start of the phase-A area): the edge
@@ -1626,6 +1654,8 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
     int* const P0 = pb[round & 1][0];
     int* const P1 = pb[round & 1][1];
     long long k0 = 0, k1 = 0, c0 = 0, c1 = 0;
+    int d_ops = 0, d_fails = 0, d_un = 0;  // diagnostics (prof_any)
+    unsigned long long d_tmax = 0;
     if (T.prof_any != nullptr) T.t0any = wall_clock64();
     for (int e = T.gt; e < et; e += T.gs) {
       const bool own = e == T.gt;
@@ -1646,8 +1676,17 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
         E.kill(e, E_COVERED);
         if (e < e0) k0++; else k1++;
       } else {
-        if (rk != nullptr) uf_unite_r(e < e0 ? P0 : P1, u, v, rk);
-        else uf_unite_h(e < e0 ? P0 : P1, u, v);
+        if (rk != nullptr && T.prof_any != nullptr) {
+          const unsigned long long t0 = wall_clock64();
+          uf_unite_rc(e < e0 ? P0 : P1, u, v, rk, d_ops, d_fails);
+          const unsigned long long dt = wall_clock64() - t0;
+          d_tmax = dt > d_tmax ? dt : d_tmax;
+          d_un++;
+        } else if (rk != nullptr) {
+          uf_unite_r(e < e0 ? P0 : P1, u, v, rk);
+        } else {
+          uf_unite_h(e < e0 ? P0 : P1, u, v);
+        }
         if (own) a1 = true;
       }
     }
@@ -1660,6 +1699,44 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0) __hip_atomic_fetch_max(T.prof_any + 9, wall_clock64() - T.t0any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // per-thread union counts: 90 max parent loads + CASes of a thread, 91 their sum, 92 unions,
+      // 93 the longest union (ticks), 94 failed CASes (summed over the step's rounds; maxima over
+      // them); one set of atomics per workgroup
+      unsigned long long mo = (unsigned long long)d_ops, so = mo, su = (unsigned long long)d_un,
+                         sf = (unsigned long long)d_fails, mt = d_tmax;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long x = __shfl_xor(mo, o, 64), y = __shfl_xor(mt, o, 64);
+        mo = x > mo ? x : mo;
+        mt = y > mt ? y : mt;
+        so += __shfl_xor(so, o, 64);
+        su += __shfl_xor(su, o, 64);
+        sf += __shfl_xor(sf, o, 64);
+      }
+      unsigned long long* lt = (unsigned long long*)T.tmp;  // [8 waves][5]
+      if (lane_id() == 0) {
+        lt[wave_id() * 5 + 0] = mo;
+        lt[wave_id() * 5 + 1] = so;
+        lt[wave_id() * 5 + 2] = su;
+        lt[wave_id() * 5 + 3] = mt;
+        lt[wave_id() * 5 + 4] = sf;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        for (int w = 1; w < NTHREADS / 64; ++w) {
+          mo = max(mo, lt[w * 5 + 0]);
+          so += lt[w * 5 + 1];
+          su += lt[w * 5 + 2];
+          mt = max(mt, lt[w * 5 + 3]);
+          sf += lt[w * 5 + 4];
+        }
+        __hip_atomic_fetch_max(T.prof_any + 10, mo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(T.prof_any + 11, so, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(T.prof_any + 12, su, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(T.prof_any + 13, mt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(T.prof_any + 14, sf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
     }
     if (grid_sync(p, *T.target, T.flag)) return true;
     TEAM_ACC(T, 1);
@@ -1668,6 +1745,7 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
     int* const Q0 = pb[(round + 1) & 1][0];
     int* const Q1 = pb[(round + 1) & 1][1];
     long long diff = 0;
+    const unsigned long long tl0 = T.prof_any != nullptr ? wall_clock64() : 0ull;
     for (int x = T.gt; x < n; x += T.gs) {
       if (x == T.gt ? !x1in : (rs && uf_load(cls, x) != La)) continue;  // labels of the untouched classes stay
       const int r0 = uf_find_h(P0, x), r1 = uf_find_h(P1, x);
@@ -1676,6 +1754,11 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
       uf_store(Q0, x, x);
       uf_store(Q1, x, x);
       diff += r0 != r1;
+    }
+    if (T.prof_any != nullptr) {  // slowest workgroup's label work (slot 95: the largest of the step's rounds)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_fetch_max(T.prof_any + 15, wall_clock64() - tl0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const long long v5[5] = {diff, k0, k1, c0, c1};
     long long t5[5];

@@ -10,7 +10,9 @@
 #  3. scripts/rocprof_summary.py -> summary.txt + traffic.json (tagged with the kernel source
 #     hash), copied to profiles/traffic.json where bench.py reads it;
 #  4. the default bench line.
-# Usage: bash scripts/gpu_profile_round.sh r03 [nobench]  (then bench.py on its own, reading the
+# Usage: bash scripts/gpu_profile_round.sh r03 [nobench]
+# (WL="single batch" limits the workloads, SUMMARY=0 stops before the summary: a round split
+# over several gpurun calls into the same gpurun_out/prof_<tag>)  (then bench.py on its own, reading the
 # profiles/traffic.json copied from gpurun_out/prof_<tag>/traffic.json)
 TAG=${1:-r03}
 R=$(pwd)
@@ -34,13 +36,18 @@ run() {  # name seconds cmd...
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
 cd /tmp
-run single_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/single -o run -- python $R/bench.py $SINGLE
-run batch_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/batch -o run -- python $R/bench.py $BATCH --batch-steps 2
-run c5_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/c5 -o run -- python $R/bench.py $C5
-run degree_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/degree -o run -- python $R/bench.py $DEGREE
-run real_degree_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/real_degree -o run -- python $R/bench.py $REAL_DEGREE
-run real_unit_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/real_unit -o run -- python $R/bench.py $REAL_UNIT
-for W in single batch c5 degree real_degree real_unit; do
+WL=${WL:-single batch c5 degree real_degree real_unit}
+for W in $WL; do
+  case $W in
+    single) run single_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/single -o run -- python $R/bench.py $SINGLE ;;
+    batch) run batch_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/batch -o run -- python $R/bench.py $BATCH --batch-steps 2 ;;
+    c5) run c5_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/c5 -o run -- python $R/bench.py $C5 ;;
+    degree) run degree_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/degree -o run -- python $R/bench.py $DEGREE ;;
+    real_degree) run real_degree_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/real_degree -o run -- python $R/bench.py $REAL_DEGREE ;;
+    real_unit) run real_unit_trace 300 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/real_unit -o run -- python $R/bench.py $REAL_UNIT ;;
+  esac
+done
+for W in $WL; do
   case $W in
     single) ARGS="$SINGLE --steps 2 --warmup 1" ;;
     batch) ARGS="$BATCH --batch-steps 1" ;;
@@ -59,6 +66,7 @@ for W in single batch c5 degree real_degree real_unit; do
   fi
 done
 cd $R
+[ "${SUMMARY:-1}" = 0 ] && exit 0
 python scripts/rocprof_summary.py $OUT > /dev/null && cp $OUT/traffic.json profiles/traffic.json && echo "summary done"
 if [ "${2:-}" != "nobench" ]; then
   timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err

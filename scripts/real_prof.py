@@ -2,7 +2,9 @@
 mdcommunity_amd.synth, the bench's real_scale object): workgroup 0's phase stamps of the
 lock-step kernel (md_profile) split each step into the grid-wide environment step (team_env_step,
 stamps 0 -> 3), barrier A (3 -> 4) and the three message-passing iterations with their barriers
-(4 -> 10), plus the team step's own pieces (slots 80-87, scripts/team_prof.py).
+(4 -> 10), plus the team step's own pieces (slots 80-87, scripts/team_prof.py) and the union
+pass's per-thread counts (slots 88-95: parent loads and compare-and-swaps, failed ones, the
+longest union, the slowest workgroup's union and label work).
 Usage: python scripts/real_prof.py [degree|unit] [n]"""
 import os
 import sys
@@ -65,7 +67,13 @@ if len(T):
           flush=True)
     print("  union pass per round: workgroup 0's own work %.1f us, slowest workgroup's %.1f us (median over steps)" % (
         np.median(T[:, 88] / rd) / 100, np.median(T[:, 89]) / 100), flush=True)
-    print("  team step per round us: union %.1f label %.1f prune %.1f" % (
-        np.median(T[:, 81] / rd) / 100, np.median(T[:, 82] / rd) / 100, np.median(T[:, 83] / np.maximum(rd - 1, 1)) / 100),
+    un = np.maximum(T[:, 92], 1)
+    print("  unions: %.0f per step, parent loads + CASes per union %.2f (mean), most by one thread %d (median "
+          "over steps; max %d), failed CASes per union %.4f, longest union %.2f us (median; max %.2f); slowest "
+          "workgroup's label work %.1f us" % (
+              np.median(T[:, 92]), np.median(T[:, 91] / un), np.median(T[:, 90]), T[:, 90].max(),
+              np.median(T[:, 94] / un), np.median(T[:, 93]) / 100, T[:, 93].max() / 100, np.median(T[:, 95]) / 100),
           flush=True)
+    print("  team step per round us: union %.1f label %.1f" % (
+        np.median(T[:, 81] / rd) / 100, np.median(T[:, 82] / rd) / 100), flush=True)
 eng.close()
