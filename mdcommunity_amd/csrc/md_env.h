@@ -175,52 +175,65 @@ __device__ __forceinline__ void uf_unite_h(P par, int a, int b) {
     if (uf_cas(par, b, b, a) == b) return;
   }
 }
-// uf_unite_h with the priority of a static rank (rk, LDS): node x's position when the graph's
-// nodes are ordered by descending static degree (both layers), ties by uf_pri.  A hub is the
-// root of its tree from its first union on, so its neighbours hook under it with a
-// compare-and-swap on their OWN parent word: with the hashed priority, a hub's root was in turn
-// the larger-priority side of many concurrent unions, every one retrying its compare-and-swap on
-// that one word (the union pass's stragglers at N = 18 000).  Roots are still one canonical node
-// per node set (the least rank), the same in both layers.
-template <class P>
-__device__ __forceinline__ void uf_unite_r(P par, int a, int b, const lds_u16* rk) {
-  while (true) {
-    a = uf_find_h(par, a);
-    b = uf_find_h(par, b);
-    if (a == b) return;
-    if (rk[a] > rk[b]) { const int t = a; a = b; b = t; }
-    if (uf_cas(par, b, b, a) == b) return;
-  }
-}
-// diagnostics (md_profile): uf_unite_r counting its parent loads and compare-and-swaps (ops)
-// and its failed compare-and-swaps (fails)
-template <class P>
-__device__ __forceinline__ int uf_find_hc(P par, int v, int& ops) {
-  int cur = uf_load(par, v);
-  ++ops;
-  if (cur != v) {
-    int prev = v, next;
-    while (++ops, cur != (next = uf_load(par, cur))) {
-      uf_store(par, prev, next);
-      prev = cur;
-      cur = next;
+// Union by a static rank (rk, LDS): node x's position when the graph's nodes are ordered by
+// descending static degree (both layers), ties by uf_pri.  A hub is the root of its tree from its
+// first union on, so its neighbours hook under it with a compare-and-swap on their OWN parent
+// word: with the hashed priority, a hub's root was in turn the larger-priority side of many
+// concurrent unions, every one retrying its compare-and-swap on that one word (the union pass's
+// stragglers at N = 18 000).  Roots are still one canonical node per node set (the least rank),
+// the same in both layers.
+// Both endpoints' paths are climbed in lockstep: one round trip per hop serves both
+// climbs (two independent device-coherent loads in flight instead of two dependent find loops),
+// path splitting on the way; two roots: the lower-ranked one is hooked under the other (a
+// failed compare-and-swap re-reads); paths that meet stop.
+// (CNT: diagnostics, the round trips in *ops -- a hop's two loads count once -- and the failed
+// compare-and-swaps in *fails)
+template <bool CNT = false, class P>
+__device__ __forceinline__ void uf_unite_r2(P par, int a, int b, const lds_u16* rk, int* ops = nullptr,
+                                            int* fails = nullptr) {
+  int ap = -1, bp = -1;
+  while (a != b) {
+    const int na = uf_load(par, a), nb = uf_load(par, b);
+    if (CNT) ++*ops;
+    if (na == a && nb == b) {
+      const bool sw = rk[a] > rk[b];
+      const int hi = sw ? a : b, lo = sw ? b : a;  // hi: the root of lower rank (larger value)
+      if (CNT) ++*ops;
+      if (uf_cas(par, hi, hi, lo) == hi) return;
+      if (CNT) ++*fails;
+      continue;
+    }
+    if (na != a) {
+      if (ap >= 0) uf_store(par, ap, na);
+      ap = a;
+      a = na;
+    }
+    if (nb != b) {
+      if (bp >= 0) uf_store(par, bp, nb);
+      bp = b;
+      b = nb;
     }
   }
-  return cur;
 }
+// the roots of x in both layers' parent arrays, the two climbs in lockstep (path halving)
 template <class P>
-__device__ __forceinline__ void uf_unite_rc(P par, int a, int b, const lds_u16* rk, int& ops, int& fails) {
+__device__ __forceinline__ int2 uf_find2_h(P p0, P p1, int x) {
+  int a = x, b = x, qa = -1, qb = -1;
   while (true) {
-    a = uf_find_hc(par, a, ops);
-    b = uf_find_hc(par, b, ops);
-    if (a == b) return;
-    if (rk[a] > rk[b]) { const int t = a; a = b; b = t; }
-    ++ops;
-    if (uf_cas(par, b, b, a) == b) return;
-    ++fails;
+    const int na = uf_load(p0, a), nb = uf_load(p1, b);
+    if (na == a && nb == b) return make_int2(a, b);
+    if (na != a) {
+      if (qa >= 0) uf_store(p0, qa, na);  // halving: qa's parent was a
+      qa = a;
+      a = na;
+    }
+    if (nb != b) {
+      if (qb >= 0) uf_store(p1, qb, nb);
+      qb = b;
+      b = nb;
+    }
   }
 }
-
 // ------------------------------------------------------------------ layout and view
 // LDS layout of a graph's environment (words from the start of the phase-A area): the edge
 // region first (u16 endpoints, state, state at the last write-back, covered flags) so a
@@ -1678,12 +1691,12 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
       } else {
         if (rk != nullptr && T.prof_any != nullptr) {
           const unsigned long long t0 = wall_clock64();
-          uf_unite_rc(e < e0 ? P0 : P1, u, v, rk, d_ops, d_fails);
+          uf_unite_r2<true>(e < e0 ? P0 : P1, u, v, rk, &d_ops, &d_fails);
           const unsigned long long dt = wall_clock64() - t0;
           d_tmax = dt > d_tmax ? dt : d_tmax;
           d_un++;
         } else if (rk != nullptr) {
-          uf_unite_r(e < e0 ? P0 : P1, u, v, rk);
+          uf_unite_r2(e < e0 ? P0 : P1, u, v, rk);
         } else {
           uf_unite_h(e < e0 ? P0 : P1, u, v);
         }
@@ -1748,7 +1761,8 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
     const unsigned long long tl0 = T.prof_any != nullptr ? wall_clock64() : 0ull;
     for (int x = T.gt; x < n; x += T.gs) {
       if (x == T.gt ? !x1in : (rs && uf_load(cls, x) != La)) continue;  // labels of the untouched classes stay
-      const int r0 = uf_find_h(P0, x), r1 = uf_find_h(P1, x);
+      const int2 rr = uf_find2_h(P0, P1, x);
+      const int r0 = rr.x, r1 = rr.y;
       uf_store(E.deg0, x, r0);
       uf_store(E.deg1, x, r1);
       uf_store(Q0, x, x);

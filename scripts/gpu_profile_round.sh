@@ -11,8 +11,8 @@
 #     hash), copied to profiles/traffic.json where bench.py reads it;
 #  4. the default bench line.
 # Usage: bash scripts/gpu_profile_round.sh r03 [nobench]
-# (WL="single batch" limits the workloads, SUMMARY=0 stops before the summary: a round split
-# over several gpurun calls into the same gpurun_out/prof_<tag>)  (then bench.py on its own, reading the
+# (WL="single batch" limits the workloads; PART=a summarises that part on the box and deletes its
+# databases, for a round split over several gpurun calls: merge with rocprof_summary.py --merge)  (then bench.py on its own, reading the
 # profiles/traffic.json copied from gpurun_out/prof_<tag>/traffic.json)
 TAG=${1:-r03}
 R=$(pwd)
@@ -21,7 +21,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 SINGLE="--batch-graphs 0 --c5-graphs 0 --no-cpu-baseline --degree-steps 0 --no-per-step --real-steps 0"
 BATCH="--steps 0 --batch-graphs 256 --c5-graphs 0 --no-cpu-baseline --degree-steps 0 --no-per-step --real-steps 0"
-C5="--steps 0 --batch-graphs 0 --c5-graphs 4096 --c5-steps 1 --no-cpu-baseline --degree-steps 0 --no-per-step --real-steps 0"
+C5="--steps 0 --batch-graphs 0 --c5-graphs 4096 --c5-steps 1 --c5-shard-graphs 0 --no-cpu-baseline --degree-steps 0 --no-per-step --real-steps 0"
 DEGREE="--steps 0 --batch-graphs 0 --c5-graphs 0 --no-cpu-baseline --degree-steps 2 --no-per-step --real-steps 0"
 REAL_DEGREE="--steps 0 --batch-graphs 0 --c5-graphs 0 --no-cpu-baseline --degree-steps 0 --no-per-step --real-steps 1 --real-cases degree"
 REAL_UNIT="--steps 0 --batch-graphs 0 --c5-graphs 0 --no-cpu-baseline --degree-steps 0 --no-per-step --real-steps 1 --real-cases unit"
@@ -66,7 +66,14 @@ for W in $WL; do
   fi
 done
 cd $R
-[ "${SUMMARY:-1}" = 0 ] && exit 0
+if [ -n "${PART:-}" ]; then
+  # one part of a round split over gpurun calls: summarise this part's databases here and drop
+  # them (the merged-back gpurun_out/ is capped at 64 MiB); merge the parts' traffic_<part>.json
+  # afterwards (scripts/rocprof_summary.py --merge)
+  python scripts/rocprof_summary.py $OUT > /dev/null && mv $OUT/traffic.json $OUT/traffic_$PART.json && \
+    mv $OUT/summary.txt $OUT/summary_$PART.txt && find $OUT -name "*.db" -delete && echo "summary $PART done"
+  exit $?
+fi
 python scripts/rocprof_summary.py $OUT > /dev/null && cp $OUT/traffic.json profiles/traffic.json && echo "summary done"
 if [ "${2:-}" != "nobench" ]; then
   timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err

@@ -20,6 +20,7 @@ hash of the kernel sources being benchmarked):
 * LDS bank conflicts: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE.
 
 Usage: python scripts/rocprof_summary.py gpurun_out/prof_r02
+       python scripts/rocprof_summary.py --merge traffic.json traffic_a.json traffic_b.json
 """
 import glob
 import json
@@ -37,9 +38,12 @@ def dbs(d):
     return sorted(glob.glob(os.path.join(d, "**", "*.db"), recursive=True))
 
 
-def kernel_stats(path):
+def kernel_stats(path, main=None):
     cur = sqlite3.connect(path).cursor()
     rows = list(cur.execute("select name, duration, grid_x, workgroup_x from kernels"))
+    if main is not None:  # (C5: the main kernel's dispatches of the 4096-graph size only)
+        md = big([d for n, d, _, _ in rows if main in n])
+        rows = [r for r in rows if main not in r[0] or r[1] in md]
     out = {}
     for name, dur, gx, wx in rows:
         e = out.setdefault(name, {"calls": 0, "total_ns": 0, "min_ns": None, "max_ns": 0, "workgroups": set()})
@@ -70,11 +74,20 @@ def mean(x):
     return sum(x) / len(x) if x else None
 
 
+def big(x):
+    """The dispatches of the workload's main launch size: those within half of the largest
+    (a C5 profile run before --c5-shard-graphs 0 also held the 512-graph shard launches)."""
+    if not x:
+        return x
+    m = max(x)
+    return [v for v in x if v >= 0.5 * m]
+
+
 def workload(d, w, lines):
     kernel = KERNELS[w]
     out = {"kernel": kernel}
     for path in dbs(os.path.join(d, w)):
-        st = kernel_stats(path)
+        st = kernel_stats(path, kernel if w == "c5" else None)
         lines.append(f"== {w}: kernel trace {os.path.relpath(path, d)}")
         lines.append(f"{'kernel':60s} {'calls':>6s} {'total_ms':>10s} {'avg_us':>10s} {'min_us':>10s} {'max_us':>10s} workgroups")
         for k, v in sorted(st.items(), key=lambda kv: -kv[1]["total_ns"]):
@@ -88,6 +101,9 @@ def workload(d, w, lines):
             for c, v in pmc(path, kernel).items():
                 vals[c] = v
                 lines.append(f"== {w} {c} per {kernel} dispatch (raw): {[round(x, 1) for x in v]}")
+    if w == "c5" and vals.get("FETCH_SIZE"):
+        keep = [i for i, v in enumerate(vals["FETCH_SIZE"]) if v >= 0.5 * max(vals["FETCH_SIZE"])]
+        vals = {c: [v[i] for i in keep if i < len(v)] for c, v in vals.items()}
     m = {c: mean(v) for c, v in vals.items()}
     if w in ("batch", "c5"):
         # the tail launch of each batch rollout (md_rollout_kernel: the last graphs the queue
@@ -136,8 +152,27 @@ def workload(d, w, lines):
     return out
 
 
+def merge(dst, parts):
+    """traffic.json of a round profiled in parts (gpu_profile_round.sh PART=...): the first part
+    holding the single graph gives the top-level fields, every part its nested workloads."""
+    out = {}
+    for p in parts:
+        with open(p) as f:
+            t = json.load(f)
+        nested = {k: v for k, v in t.items() if k in KERNELS}
+        top = {k: v for k, v in t.items() if k not in KERNELS}
+        if "avg_ns" in top or not out:
+            out.update(top)
+        out.update(nested)
+    with open(dst, "w") as fo:
+        json.dump(out, fo, indent=1)
+
+
 def main():
     import bench
+    if sys.argv[1] == "--merge":  # rocprof_summary.py --merge out.json part_a.json part_b.json ...
+        merge(sys.argv[2], sys.argv[3:])
+        return
     d = sys.argv[1]
     lines = [f"kernel sources hash {bench.kernel_src_hash()}"]
     report = {w: workload(d, w, lines) for w in KERNELS if os.path.isdir(os.path.join(d, w))}
