@@ -1477,7 +1477,7 @@ struct Team {
   int use;         // reductions so far (partial slot = use & 1)
   unsigned* target;
   int* flag;
-  int* tmp;        // LDS, >= 8 * 16 + 16 words
+  int* tmp;        // LDS, >= 2 * (8 * 17 + 17) words (team_reduce's long longs)
   unsigned long long* acc;  // diagnostics (md_profile): per-step piece ticks of workgroup 0, else null
   unsigned long long t;
   unsigned long long* prof_any;  // diagnostics: the step's record (every workgroup), else null
@@ -1569,40 +1569,50 @@ __device__ bool team_reduce(KParams& p, Team& T, const long long (&v)[K], unsign
   }
   T.use++;
   if (grid_sync(p, *T.target, T.flag)) return true;
-  if (w == 0) {
-    long long a[K];
-    long long pre = 0;
+  // every thread reads one workgroup's partials (its K loads in flight together): one round
+  // trip for up to NTHREADS workgroups, where one wave looping over them took n_main / 64
+  long long a[K];
+  long long pre = 0;
 #pragma unroll
-    for (int k = 0; k < K; ++k) a[k] = 0;
-    for (int b = lane; b < p.n_main; b += 64) {
-      const g_u64* src = (const g_u64*)(p.tpart + ((size_t)slot * TEAM_MAX_WG + b) * 16);
+  for (int k = 0; k < K; ++k) a[k] = 0;
+  for (int b = threadIdx.x; b < p.n_main; b += NTHREADS) {
+    const g_u64* src = (const g_u64*)(p.tpart + ((size_t)slot * TEAM_MAX_WG + b) * 16);
+    long long y[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const long long y = (long long)__hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        a[k] = (maxmask >> k & 1u) ? (a[k] > y ? a[k] : y) : a[k] + y;
-        if (k == 0 && b < (int)blockIdx.x) pre += y;
-      }
+    for (int k = 0; k < K; ++k) y[k] = (long long)__hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] = (maxmask >> k & 1u) ? (a[k] > y[k] ? a[k] : y[k]) : a[k] + y[k];
+    if (b < (int)blockIdx.x) pre += y[0];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const long long y = __shfl_xor(a[k], o, 64);
+      a[k] = (maxmask >> k & 1u) ? (a[k] > y ? a[k] : y) : a[k] + y;
     }
+  }
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
+  for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
+  if (lane == 0) {  // per wave (lt's first stage is dead: read before the barrier)
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const long long y = __shfl_xor(a[k], o, 64);
-        a[k] = (maxmask >> k & 1u) ? (a[k] > y ? a[k] : y) : a[k] + y;
-      }
+    for (int k = 0; k < K; ++k) lt[w * (K + 1) + k] = a[k];
+    lt[w * (K + 1) + K] = pre;
+  }
+  __syncthreads();
+  if (threadIdx.x <= K) {
+    const int k = threadIdx.x;
+    long long c = 0;
+    for (int i = 0; i < NTHREADS / 64; ++i) {
+      const long long y = lt[i * (K + 1) + k];
+      c = (k < K && (maxmask >> k & 1u)) ? (c > y ? c : y) : c + y;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
-    if (lane == 0) {
-#pragma unroll
-      for (int k = 0; k < K; ++k) lt[8 * 16 + k] = a[k];
-      lt[8 * 16 + K] = pre;
-    }
+    lt[8 * 17 + k] = c;
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < K; ++k) tot[k] = lt[8 * 16 + k];
-  if (before != nullptr) *before = lt[8 * 16 + K];
+  for (int k = 0; k < K; ++k) tot[k] = lt[8 * 17 + k];
+  if (before != nullptr) *before = lt[8 * 17 + K];
   __syncthreads();
   return false;
 }
