@@ -113,8 +113,9 @@ def test_bench_launcher_world2_gathers_like_one_process():
     assert b2["graphs"] == 6 and b2["graphs_rank0"] == 3
     assert b2["audc_all"] == b1["audc_all"] and b2["removals_all"] == b1["removals_all"]
     assert b2["removals_per_step"] == sum(b1["removals_all"])
-    # weak scaling of the headline: each rank runs its own replica
+    # weak scaling of the headline: each rank runs its own replica, and the line says so
     assert two["config"]["removals_per_step"] == 2 * one["config"]["removals_per_step"]
+    assert two["scaling"] == "weak" and "replica" in two["value_note"] and "c5" in two["value_note"]
     # C5 (configs[4]) is strong-scaled: the same graphs at both world sizes, split over the ranks
     c2, c1 = two["c5"], one["c5"]
     assert c2["scaling"] == c1["scaling"] == "strong"
