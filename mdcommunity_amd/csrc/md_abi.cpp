@@ -953,7 +953,7 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
       }
     }
   }
-  // static union ranks of the grid-wide environment step (md_env.h uf_unite_r): per graph the
+  // static union ranks of the grid-wide environment step (md_env.h uf_unite_r2): per graph the
   // nodes ordered by descending static degree (both layers), ties by the hashed priority
   // (uf_pri), rank = position; every graph's block starts at an even index
   std::vector<uint16_t> ranks;
