@@ -452,6 +452,51 @@ def test_grid_wide_environment_step(monkeypatch):
         assert out[("64", name)] == out[("66", name)], name
 
 
+@pytest.mark.timeout(300)
+def test_grid_wide_incremental_steps_random(monkeypatch):
+    """The grid-wide step keeps the previous fixed point's class labels and sizes between its own
+    steps (lab_ok) and runs each new fixed point on the removed node's class only; every other
+    state change must drop them.  Random md_step calls (one action each; multi-action steps are
+    the step > 1 rollouts of test_grid_wide_environment_step) on gmm1000_s0 in the grid-wide
+    mode, with md_get_state / md_set_state round trips and md_predict calls in between, against
+    the oracle environment stepped along the same actions: the LMCC, the covered set, the
+    covered-edge counters (edges killed by a cover, not by an earlier prune) and the pruned-edge
+    counts after every call."""
+    from oracle import refenv
+    monkeypatch.setenv("MD_ENV_MODE", "0")
+    monkeypatch.setenv("MD_VARIANT", "64")
+    z = load_golden("gmm1000_s0")
+    n = int(z["n_nodes"])
+    g = refenv.RefGraph(n, z["edges0"], z["edges1"])
+    env = refenv.RefEnv(g, "unit")
+    e = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
+    try:
+        e.load_graphs([(n, z["edges0"], z["edges1"])])
+        assert int(e.reset()[0]) == g.max_rank
+        rng = np.random.default_rng(11)
+        for it in range(40):
+            live = refenv.featurize(g, env.covered, env.removed)[0]
+            if not live:
+                break
+            a = int(rng.choice(np.asarray(live, np.int64)))
+            lm, term = e.step(np.array([a], np.int32))
+            r = env.step(a)
+            assert int(lm[0]) == r, (it, a)
+            cov, r0, r1, cnt = e.get_state(0)
+            assert set(np.flatnonzero(cov).tolist()) == env.covered, it
+            assert [int(cnt[0]), int(cnt[1])] == env.num_covered, it
+            assert [int(cnt[2]), int(cnt[3])] == [len(env.removed[0]) // 2, len(env.removed[1]) // 2], it
+            if bool(term[0]) or env.terminal():
+                assert bool(term[0]) == env.terminal()
+                break
+            if it % 7 == 3:  # a state change outside the grid-wide step: the labels must be dropped
+                e.set_state(0, cov, r0, r1)
+            if it % 5 == 2:
+                e.predict()
+    finally:
+        e.close()
+
+
 def test_iteration1_prebuild_same_rollouts(monkeypatch):
     """Single-graph rollouts build iteration 1 (rows, alive-neighbour lists, and the whole
     first message-passing iteration) during phase A from the speculative result phase A
