@@ -7,12 +7,14 @@ device's own sequence the live set and Q (within 1e-5) equal the oracle's Predic
 every state, every pick trails the oracle's best Q by at most twice the measured |dQ| (the
 device's pick and the oracle's best each carry an error <= |dQ|), the LMCC after
 every removal equals the oracle environment's (bit-exact) and so does the AUDC.  One launch of
-all cases (more than 16 graphs: the device work queue) gives each case's single-graph rollout.
+all cases (more than 16 graphs: the device work queue) gives each case's single-graph rollout;
+so does the grid-wide environment step.  The degree-cost variant is checked the same way
+(Q, picks, LMCC; its weighted score is the agent's, tests/test_gpu_degree.py).
 The inputs are synthetic (seeded here); the oracle is pinned by tests/test_oracle.py."""
 import numpy as np
 import pytest
 
-from mdcommunity_amd import _lib, engine
+from mdcommunity_amd import _lib, engine, graph as mgraph
 from oracle import refenv, refmodel
 
 pytestmark = pytest.mark.gpu
@@ -73,22 +75,25 @@ def audc(ranks, max_rank, n):
     return s
 
 
-@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-def test_edge_case_rollout_against_oracle(eng, weights, case):
-    name, n, e0, e1 = case
+def check_along_device_sequence(eng, weights, name, n, e0, e1, cost="unit"):
+    """The device's rollout teacher-forced through the oracle (module docstring); returns the
+    device's (sequence, LMCC trace)."""
     g = refenv.RefGraph(n, e0, e1)
-    env = refenv.RefEnv(g, "unit")
-    eng.load_graphs([(n, e0, e1)])
+    env = refenv.RefEnv(g, cost)
+    if cost == "degree":
+        eng.load_graphs([(n, e0, e1)], node_w=mgraph.node_weight_array([mgraph.Graph_test.from_edges(n, e0, e1)]))
+    else:
+        eng.load_graphs([(n, e0, e1)])
     mr = int(eng.reset()[0])
     assert mr == g.max_rank, name
     seq, ranks = eng.rollout()[0]
     if env.terminal():
         assert len(seq) == 0, name
-        return
+        return seq.tolist(), ranks.tolist()
     eng.reset()
     for t, a in enumerate(seq.tolist()):
         assert not env.terminal(), (name, t)
-        ref = refenv.predict(weights, g, env.covered, env.removed)
+        ref = refenv.predict(weights, g, env.covered, env.removed, cost)
         q = eng.predict()[0].astype(np.float64)
         live = ref != MASK
         assert np.array_equal(np.isfinite(q), live), (name, t)
@@ -101,7 +106,48 @@ def test_edge_case_rollout_against_oracle(eng, weights, case):
         r = env.step(a)
         assert int(lm[0]) == r == int(ranks[t]), (name, t)
     assert env.terminal(), name
-    assert audc(ranks, mr, n) == env.score, name
+    if cost == "unit":
+        assert audc(ranks, mr, n) == env.score, name
+    return seq.tolist(), ranks.tolist()
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_edge_case_rollout_against_oracle(eng, weights, case):
+    check_along_device_sequence(eng, weights, *case)
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_edge_case_degree_cost_against_oracle(case):
+    """Degree cost (D/): node inputs [w, 1] with w = deg / maxdeg of the original layers
+    (D/graph.py:91-115; none when the initial LMCC is 1, D/graph.py:80-90)."""
+    w = refmodel.RefWeights.load(engine.DEFAULT_DEGREE)
+    e = _lib.Engine(engine.load_weights(engine.DEFAULT_DEGREE), cost_mode=_lib.MD_COST_DEGREE)
+    try:
+        check_along_device_sequence(e, w, *case, cost="degree")
+    finally:
+        e.close()
+
+
+def test_edge_cases_grid_wide_step(eng, monkeypatch):
+    """The grid-wide environment step (team_env_step; MD_ENV_MODE=0 + MD_VARIANT=64 force it on
+    small graphs) on the same graphs: the rollouts equal the default path's."""
+    want = []
+    for _, n, e0, e1 in CASES:
+        eng.load_graphs([(n, e0, e1)])
+        eng.reset()
+        s, r = eng.rollout()[0]
+        want.append((s.tolist(), r.tolist()))
+    monkeypatch.setenv("MD_ENV_MODE", "0")
+    monkeypatch.setenv("MD_VARIANT", "64")
+    e = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
+    try:
+        for (name, n, e0, e1), wnt in zip(CASES, want):
+            e.load_graphs([(n, e0, e1)])
+            assert int(e.reset()[0]) == refenv.RefGraph(n, e0, e1).max_rank, name
+            s, r = e.rollout()[0]
+            assert (s.tolist(), r.tolist()) == wnt, name
+    finally:
+        e.close()
 
 
 def test_edge_cases_in_one_queue_launch(eng):
