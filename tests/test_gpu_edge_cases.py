@@ -166,3 +166,40 @@ def test_edge_cases_in_one_queue_launch(eng):
         k = i % len(graphs)
         assert (s.tolist(), r.tolist()) == single[k], CASES[k][0]
         assert int(mr[i]) == refenv.RefGraph(*graphs[k]).max_rank, CASES[k][0]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_edge_case_multi_pick_rollout(eng, weights, case):
+    """step = 3 picks per prediction (the stepRatio path, np.argsort(-q)[:step],
+    U/MultiDismantler_torch.py:725): at each prediction the three picks are np.argsort of the
+    device's own masked row, each within twice the measured |dQ| of the oracle's third-best Q; picks stop at the
+    terminal state inside a group (:726-729); the LMCC after every removal equals the oracle's."""
+    name, n, e0, e1 = case
+    g = refenv.RefGraph(n, e0, e1)
+    env = refenv.RefEnv(g, "unit")
+    eng.load_graphs([(n, e0, e1)])
+    eng.reset()
+    seq, ranks = eng.rollout(step=3)[0]
+    seq = seq.tolist()
+    eng.reset()
+    t = 0
+    while t < len(seq):
+        assert not env.terminal(), (name, t)
+        ref = refenv.predict(weights, g, env.covered, env.removed)
+        q = eng.predict()[0].astype(np.float64)
+        live = ref != MASK
+        assert np.array_equal(np.isfinite(q), live), (name, t)
+        dq = float(np.max(np.abs(q[live] - ref[live])))
+        assert dq < Q_TOL, (name, t, dq)
+        top = np.sort(ref[live])[::-1]
+        group = seq[t:t + 3]
+        row = np.where(live, q, MASK)  # the masked float64 row the selection sorts (:286-300)
+        assert group == np.argsort(-row)[:len(group)].tolist(), (name, t)
+        for a in group:
+            assert top[min(2, len(top) - 1)] - ref[a] <= 2 * dq, (name, t, a)
+            lm, _ = eng.step(np.array([a], np.int32))
+            assert int(lm[0]) == env.step(a) == int(ranks[t]), (name, t)
+            t += 1
+            if env.terminal():
+                break
+    assert env.terminal() and t == len(seq), name
