@@ -520,9 +520,12 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
   const bool df = run_mode == RUN_ROLLOUT && n_env == 1 && ngl == 1 && !team_env && c->dfbuf.p != nullptr &&
                   c->df_graph[gl[0]] && 2 * ((c->hinfo[gl[0]].n + TILE - 1) / TILE) <= grid - 2;
   HIPCHK(c, hipMemcpyAsync(c->glist.p, gl, sizeof(int) * ngl, hipMemcpyHostToDevice, c->stream));
+  // (the host side of an async upload must outlive the copy: `to`, like `v`, lives until the
+  // launch below has been waited for)
+  std::vector<int> to;
   if (qmode) {
     // queue-mode neighbour-list cache slots: each graph slot's tiles from its launch prefix
-    std::vector<int> to(ngl + 1, 0);
+    to.assign(ngl + 1, 0);
     for (int i = 0; i < ngl; ++i) to[i + 1] = to[i] + (c->hinfo[gl[i]].n + TILE - 1) / TILE;
     HIPCHK(c, hipMemcpyAsync(c->gtoff.p, to.data(), sizeof(int) * (ngl + 1), hipMemcpyHostToDevice, c->stream));
   }
@@ -988,6 +991,7 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   c->ng = n_graphs;
   c->hinfo = info;
   c->hvar.assign(n_graphs, GraphVar{});
+  c->s0_pending = false;  // a deferred prune belonged to the graphs this load replaces
   c->tot_n = tn;
   c->tot_tiles = tt;
   c->need_gscr = big;
@@ -1289,17 +1293,28 @@ md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, i
   if (!c || step < 1) return MD_EINVAL;
   if (c->ng == 0) return fail(c, MD_ESTATE, "no graphs loaded");
   HIPCHK(c, hipSetDevice(c->device));
-  c->s0_pending = false;  // the first environment step of this rollout runs the deferred s0 prune
   const int host_select = step > 1 ? 1 : 0;
   c->last_ms = 0.0;
   c->last_launches = 0;
-  std::vector<int> gl;
+  std::vector<int> gl, idle;
   for (int g = 0; g < c->ng; ++g) {
     GraphVar& v = c->hvar[g];
     if (v.alive[0] > 0 && v.alive[1] > 0) {
       v.status = ST_RUN;
       v.npend = 0;
       gl.push_back(g);
+    } else {
+      idle.push_back(g);
+    }
+  }
+  if (c->s0_pending) {
+    // the first environment step of this rollout runs the deferred s0 prune for every graph it
+    // launches; a graph it leaves out (a layer without edges: terminal from the start) gets the
+    // prune here, exactly md_reset's launch, so its state and max_rank equal md_reset's
+    c->s0_pending = false;
+    if (!idle.empty()) {
+      md_status st = launch(c, idle, RUN_STEP, 0);
+      if (st != MD_OK) return st;
     }
   }
   std::vector<float> qrow;

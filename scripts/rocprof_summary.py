@@ -38,12 +38,9 @@ def dbs(d):
     return sorted(glob.glob(os.path.join(d, "**", "*.db"), recursive=True))
 
 
-def kernel_stats(path, main=None):
+def kernel_stats(path):
     cur = sqlite3.connect(path).cursor()
     rows = list(cur.execute("select name, duration, grid_x, workgroup_x from kernels"))
-    if main is not None:  # (C5: the main kernel's dispatches of the 4096-graph size only)
-        md = big([d for n, d, _, _ in rows if main in n])
-        rows = [r for r in rows if main not in r[0] or r[1] in md]
     out = {}
     for name, dur, gx, wx in rows:
         e = out.setdefault(name, {"calls": 0, "total_ns": 0, "min_ns": None, "max_ns": 0, "workgroups": set()})
@@ -74,20 +71,11 @@ def mean(x):
     return sum(x) / len(x) if x else None
 
 
-def big(x):
-    """The dispatches of the workload's main launch size: those within half of the largest
-    (a C5 profile run before --c5-shard-graphs 0 also held the 512-graph shard launches)."""
-    if not x:
-        return x
-    m = max(x)
-    return [v for v in x if v >= 0.5 * m]
-
-
 def workload(d, w, lines):
     kernel = KERNELS[w]
     out = {"kernel": kernel}
     for path in dbs(os.path.join(d, w)):
-        st = kernel_stats(path, kernel if w == "c5" else None)
+        st = kernel_stats(path)
         lines.append(f"== {w}: kernel trace {os.path.relpath(path, d)}")
         lines.append(f"{'kernel':60s} {'calls':>6s} {'total_ms':>10s} {'avg_us':>10s} {'min_us':>10s} {'max_us':>10s} workgroups")
         for k, v in sorted(st.items(), key=lambda kv: -kv[1]["total_ns"]):
@@ -101,9 +89,9 @@ def workload(d, w, lines):
             for c, v in pmc(path, kernel).items():
                 vals[c] = v
                 lines.append(f"== {w} {c} per {kernel} dispatch (raw): {[round(x, 1) for x in v]}")
-    if w == "c5" and vals.get("FETCH_SIZE"):
-        keep = [i for i, v in enumerate(vals["FETCH_SIZE"]) if v >= 0.5 * max(vals["FETCH_SIZE"])]
-        vals = {c: [v[i] for i in keep if i < len(v)] for c, v in vals.items()}
+    # (C5 is profiled with --c5-shard-graphs 0, gpu_profile_round.sh: every md_queue_kernel
+    # dispatch of that run is a 4096-graph launch, so all of them are kept -- no filtering by
+    # duration or traffic, which would also drop short relaunches of the same run)
     m = {c: mean(v) for c, v in vals.items()}
     if w in ("batch", "c5"):
         # the tail launch of each batch rollout (md_rollout_kernel: the last graphs the queue

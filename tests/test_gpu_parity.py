@@ -652,6 +652,31 @@ def test_deferred_reset_same_rollouts():
         e.close()
 
 
+def test_deferred_reset_then_rollout_empty_layer_graph():
+    """md_rollout after md_reset_deferred launches only graphs with edges in both
+    layers; a graph with an empty layer (terminal from the start) must still get the s0 prune,
+    so md_get_state and md_max_rank after the rollout equal md_reset's (U/mvc_env.py:52)."""
+    w = engine.load_weights(engine.DEFAULT_UNIT)
+    rng = np.random.default_rng(5)
+    iu = np.array([(i, j) for i in range(20) for j in range(i + 1, 20)], np.int32)
+    e0 = iu[rng.random(len(iu)) < 0.3]
+    z = load_golden("er100")
+    graphs = [(int(z["n_nodes"]), z["edges0"], z["edges1"]), (20, e0, np.zeros((0, 2), np.int32))]
+    e = _lib.Engine(w)
+    try:
+        e.load_graphs(graphs)
+        mr = e.reset().copy()
+        st_ref = e.get_state(1)
+        e.rollout()
+        e.reset_deferred()
+        e.rollout()
+        for a, b in zip(e.get_state(1), st_ref):
+            assert np.array_equal(a, b)
+        assert np.array_equal(e.max_rank(), mr)
+    finally:
+        e.close()
+
+
 def test_deferred_reset_then_step_predict_state():
     """After md_reset_deferred, md_step / md_predict / md_get_state / md_max_rank run the pending
     s0 prune first (U/mvc_env.py:52 before :74-87): the state, LMCC, max_rank and Q equal those

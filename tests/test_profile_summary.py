@@ -21,9 +21,3 @@ def test_merge_parts(tmp_path):
     t = json.loads(out.read_text())
     assert t["avg_ns"] == 3.9e6 and t["hbm_bytes_per_launch"] == 5.5e8 and t["src_hash"] == "h"
     assert set(t) >= {"batch", "c5", "real_degree", "real_unit"}
-
-
-def test_big_keeps_main_launch_size():
-    # two 4096-graph launches and two 512-graph shard launches (FETCH_SIZE per dispatch)
-    assert rs.big([109.7e6, 109.7e6, 13.6e6, 13.6e6]) == [109.7e6, 109.7e6]
-    assert rs.big([]) == []
