@@ -6,11 +6,14 @@ pick, U/MultiDismantler_torch.py:766).  For each: max_rank equals the oracle's; 
 device's own sequence the live set and Q (within 1e-5) equal the oracle's Predict row at
 every state, every pick trails the oracle's best Q by at most twice the measured |dQ| (the
 device's pick and the oracle's best each carry an error <= |dQ|), the LMCC after
-every removal equals the oracle environment's (bit-exact) and so does the AUDC.  One launch of
+every removal equals the oracle environment's (bit-exact) and so does the AUDC.  The same
+graphs are also checked against the REFERENCE itself (test_edge_case_against_reference, goldens
+from tests/golden/make_golden_edge.py).  One launch of
 all cases (more than 16 graphs: the device work queue) gives each case's single-graph rollout;
 so does the grid-wide environment step.  The degree-cost variant is checked the same way
 (Q, picks, LMCC; its weighted score is the agent's, tests/test_gpu_degree.py).
-The inputs are synthetic (seeded here); the oracle is pinned by tests/test_oracle.py."""
+The inputs are synthetic (seeded, tests/edge_graphs.py); the oracle is pinned by
+tests/test_oracle.py."""
 import numpy as np
 import pytest
 
@@ -23,34 +26,7 @@ Q_TOL = 1e-5
 MASK = refenv.MASK
 
 
-def er_edges(rng, nodes, p):
-    nodes = np.asarray(nodes)
-    out = []
-    for i in range(len(nodes)):
-        for j in range(i + 1, len(nodes)):
-            if rng.random() < p:
-                out.append((int(nodes[i]), int(nodes[j])))
-    rng.shuffle(out)
-    return np.array(out, np.int32).reshape(-1, 2)
-
-
-def cases():
-    rng = np.random.default_rng(2026)
-    star = np.array([(0, v) for v in range(1, 100)], np.int32)
-    tree = np.array([(int(rng.integers(0, v)), v) for v in range(1, 130)], np.int32)
-    c1, c2 = np.arange(0, 100), np.arange(100, 200)
-    return [
-        ("k2", 2, np.array([[0, 1]], np.int32), np.array([[0, 1]], np.int32)),
-        ("path_triangle", 3, np.array([[0, 1], [1, 2]], np.int32), np.array([[0, 1], [1, 2], [0, 2]], np.int32)),
-        ("shared_hub_star", 100, star, star[::-1].copy()),
-        ("isolated_nodes", 50, er_edges(rng, range(40), 0.15), er_edges(rng, range(40), 0.12)),
-        ("wave_63", 63, er_edges(rng, range(63), 0.08), er_edges(rng, range(63), 0.1)),
-        ("wave_65", 65, er_edges(rng, range(65), 0.08), er_edges(rng, range(65), 0.1)),
-        ("two_clusters", 200, np.concatenate([er_edges(rng, c1, 0.06), er_edges(rng, c2, 0.05)]),
-         np.concatenate([er_edges(rng, c1, 0.05), er_edges(rng, c2, 0.07)])),
-        ("tree_vs_dense", 130, tree, er_edges(rng, range(130), 0.2)),
-        ("layer1_empty", 20, er_edges(rng, range(20), 0.3), np.zeros((0, 2), np.int32)),
-    ]
+from edge_graphs import cases  # noqa: E402  (tests/ is on sys.path under pytest)
 
 
 CASES = cases()
@@ -203,3 +179,82 @@ def test_edge_case_multi_pick_rollout(eng, weights, case):
             if env.terminal():
                 break
     assert env.terminal() and t == len(seq), name
+
+
+# ---------------------------------------------------------------- against the reference itself
+def load_edge_golden(cost):
+    """tests/golden/edge_<cost>.npz (tests/golden/make_golden_edge.py: the reference's GetSol on
+    each edge-case graph, in the reference's own networkx edge order) as {case: {field: array}}."""
+    import json
+    import os
+    from conftest import GOLDEN
+    with np.load(os.path.join(GOLDEN, f"edge_{cost}.npz")) as z:
+        flat = {k: z[k] for k in z.files}
+    out = {}
+    for k, v in flat.items():
+        name, field = k.split("__", 1)
+        out.setdefault(name, {})[field] = v
+    with open(os.path.join(GOLDEN, "meta_edge.json")) as f:
+        meta = json.load(f)[cost]["cases"]
+    return out, meta
+
+
+AMBIG_GAP = 1e-6  # a reference top-2 gap this small is decided by its fp32 reduction order
+
+
+@pytest.mark.parametrize("cost", ["unit", "degree"])
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_edge_case_against_reference(case, cost):
+    """The device against the REFERENCE's own rollout of each edge case
+    (U/MultiDismantler_torch.py:759-784; D/ :683-706): max_rank equal; the sequence equal to
+    the reference's up to its first ambiguous prediction (an exact tie, broken by numpy's
+    argsort of the whole row, or a top-2 gap < 1e-6) and the LMCC trace equal over that prefix;
+    sequence, LMCC trace and unit-cost AUDC bit-exact when no prediction is ambiguous; and,
+    teacher-forced along the reference's sequence, Q within 1e-5 of the reference's row with the
+    same live set at every prediction."""
+    name = case[0]
+    gold, meta = load_edge_golden(cost)
+    if "error" in meta[name]:
+        # the reference itself cannot run this input (recorded by the generator: degree cost
+        # on a layer without edges, D/graph.py's weights); the oracle tests above cover it
+        assert name not in gold
+        return
+    z = gold[name]
+    n = int(z["n_nodes"])
+    e0, e1 = z["edges0"].reshape(-1, 2), z["edges1"].reshape(-1, 2)
+    deg = cost == "degree"
+    e = _lib.Engine(engine.load_weights(engine.DEFAULT_DEGREE if deg else engine.DEFAULT_UNIT),
+                    cost_mode=_lib.MD_COST_DEGREE if deg else _lib.MD_COST_UNIT)
+    try:
+        nw = mgraph.node_weight_array([mgraph.Graph_test.from_edges(n, e0, e1)]) if deg else None
+        e.load_graphs([(n, e0, e1)], node_w=nw)
+        mr = int(e.reset()[0])
+        assert mr == int(z["max_rank"])
+        seq, ranks = e.rollout()[0]
+        rseq, rranks = z["seq"].tolist(), z["ranks"].tolist()
+        st = z["step_stats"].reshape(-1, 6)
+        gap = z["step_gap"]
+        amb = [t for t in range(len(st)) if st[t, 3] > 1 or gap[t] < AMBIG_GAP]
+        first = amb[0] if amb else len(rseq)
+        k = 0
+        while k < min(len(seq), len(rseq)) and int(seq[k]) == rseq[k]:
+            k += 1
+        assert k >= min(first, len(rseq)), (name, k, first)
+        assert ranks[:k].tolist() == rranks[:k]
+        if not amb:
+            assert seq.tolist() == rseq and ranks.tolist() == rranks
+            if not deg:
+                assert audc(ranks, mr, n) == float(z["score"])
+        # Q along the reference's own sequence
+        e.reset()
+        q_all = z["q_all"].reshape(-1, n).astype(np.float64)
+        for t, a in enumerate(rseq):
+            q = e.predict()[0].astype(np.float64)
+            ref = q_all[t]
+            live = ~np.isnan(ref)
+            assert np.array_equal(np.isfinite(q), live), (name, t)
+            assert float(np.max(np.abs(q[live] - ref[live]))) < Q_TOL, (name, t)
+            lm, _ = e.step(np.array([a], np.int32))
+            assert int(lm[0]) == rranks[t], (name, t)
+    finally:
+        e.close()

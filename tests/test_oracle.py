@@ -81,3 +81,43 @@ def test_mcc_cases_match_reference():
         r0 = np.asarray([(int(u), int(v)) in rem[0] for u, v in e0], np.uint8)
         r1 = np.asarray([(int(u), int(v)) in rem[1] for u, v in e1], np.uint8)
         assert np.array_equal(r0, z[f"c{i}_r0"]) and np.array_equal(r1, z[f"c{i}_r1"])
+
+
+def _edge_goldens(cost):
+    import json
+    import os
+    from conftest import GOLDEN
+    with np.load(os.path.join(GOLDEN, f"edge_{cost}.npz")) as z:
+        flat = {k: z[k] for k in z.files}
+    out = {}
+    for k, v in flat.items():
+        name, field = k.split("__", 1)
+        out.setdefault(name, {})[field] = v
+    with open(os.path.join(GOLDEN, "meta_edge.json")) as f:
+        return out, json.load(f)[cost]["cases"]
+
+
+@pytest.mark.parametrize("cost", ["unit", "degree"])
+def test_edge_cases_match_reference(weights, weights_degree, cost):
+    """The oracle on the edge-case graphs (tests/edge_graphs.py) against the reference's own
+    rollouts of them (tests/golden/make_golden_edge.py): max_rank, sequence, LMCC trace and
+    (unit cost) AUDC equal, Q rows within 1e-6 (bit-identical on the build host)."""
+    gold, meta = _edge_goldens(cost)
+    w = weights_degree if cost == "degree" else weights
+    assert set(gold) | {k for k, m in meta.items() if "error" in m} == set(meta)
+    for name, z in gold.items():
+        n = int(z["n_nodes"])
+        g = refenv.RefGraph(n, z["edges0"].reshape(-1, 2), z["edges1"].reshape(-1, 2))
+        assert g.max_rank == int(z["max_rank"]), name
+        rows = {}
+        score, seq, ranks, _ = refenv.rollout(w, g, on_predict=lambda t, q, env: rows.__setitem__(t, q), cost=cost)
+        assert seq == z["seq"].tolist(), name
+        assert ranks == z["ranks"].tolist(), name
+        if cost == "unit":
+            assert score == float(z["score"]), name
+        q_all = z["q_all"].reshape(-1, n).astype(np.float64)
+        for t in range(len(q_all)):
+            ref = q_all[t]
+            live = ~np.isnan(ref)
+            assert np.array_equal(rows[t] != MASK, live), (name, t)
+            assert np.max(np.abs(rows[t][live] - ref[live])) <= 1e-6, (name, t)
