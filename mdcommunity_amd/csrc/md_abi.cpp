@@ -104,6 +104,7 @@ struct md_ctx {
   int env_mode = 1;  // 1: dedicated environment workgroups for small batches
   int variant = 0;   // diagnostics knob (MD_VARIANT)
   int pair_on = 1;   // queue mode: paired tiles (MD_PAIR=0: one tile at a time)
+  int wq_on = 1;     // queue mode: one work item per wave (md_wq_kernel; MD_WQ=0: per workgroup, md_queue_kernel)
   int qpark = 8;     // queue mode: at most this many graphs left -> the lock-step kernel (MD_QPARK, 0 = off)
   double last_ms = 0.0;
   int last_launches = 0;
@@ -577,7 +578,7 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
     // tile 0 hands its derivation of phase A's early word to the speculative workgroups
     if (p.pre_ew != nullptr) p.self_ew = (unsigned long long*)(c->ctl.p + CTL_SELF);
   }
-  p.qmode = qmode ? 1 : 0;
+  p.qmode = qmode ? (c->wq_on ? 2 : 1) : 0;
   p.qpair = c->pair_on ? 1 : 0;
   p.qpark = c->qpark;
   p.nglist = ngl;
@@ -773,6 +774,7 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_VARIANT")) c->variant = std::atoi(v);
   if (const char* v = std::getenv("MD_ENV_MODE")) c->env_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_PAIR")) c->pair_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MD_WQ")) c->wq_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_QPARK")) c->qpark = std::max(0, std::min(16, std::atoi(v)));
   if (const char* v = std::getenv("MD_HOST_HANDSHAKE")) c->host_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_POLL_US")) c->poll_us = std::atoi(v);

@@ -5073,6 +5073,8 @@ __global__ void __launch_bounds__(NTHREADS, 1) md_queue_kernel(Params p, const f
   kernel_exit(kpp);
 }
 
+#include "md_wave.h"
+
 __global__ void __launch_bounds__(NTHREADS, 1) md_env_kernel(Params p, const float* __restrict__ wimg) {
   if (!kargs_layout_ok()) {
     if (threadIdx.x == 0) __hip_atomic_store(p.err, ERR_ABI, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -5191,7 +5193,9 @@ void build_weight_image(const float* w, float* img) {
 }
 
 hipError_t launch_rollout(const Params& p, const float* wimg, int grid, hipStream_t s) {
-  if (p.qmode)
+  if (p.qmode == 2)
+    hipLaunchKernelGGL(md_wq_kernel, dim3(grid), dim3(NTHREADS), lds_bytes(), s, p, wimg);
+  else if (p.qmode)
     hipLaunchKernelGGL(md_queue_kernel, dim3(grid), dim3(NTHREADS), lds_bytes(), s, p, wimg);
   else if (p.run_mode == RUN_ROLLOUT)
     hipLaunchKernelGGL(md_rollout_kernel, dim3(grid), dim3(NTHREADS), lds_bytes(), s, p, wimg);
@@ -5233,6 +5237,8 @@ hipError_t set_kernel_attrs() {
                                      lds_bytes());
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)md_queue_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes());
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)md_wq_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes());
   if (e != hipSuccess) return e;
   return hipFuncSetAttribute((const void*)md_env_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes());
 }

@@ -562,6 +562,39 @@ def test_paired_tiles_match_single_tiles(monkeypatch, cost):
 
 
 @pytest.mark.parametrize("cost", ["unit", "degree"])
+def test_wave_items_match_workgroup_items(monkeypatch, cost):
+    """Batch rollouts with one work item per wave (md_wq_kernel, default: each wave runs a whole
+    tile, both layers, or a virtual-node step; environment steps in a workgroup group section)
+    give the removal sequences and LMCC traces of the per-workgroup queue kernel (MD_WQ=0,
+    md_queue_kernel): unit and degree cost, a hub graph whose tiles overflow the neighbour lists
+    (the per-row CSR gather), odd tile counts."""
+    rng = np.random.default_rng(5)
+    hub = (3000, _hub_layer(3000, 3, 2400, rng), _hub_layer(3000, 3, 2400, rng))
+    names = ["gmm200_s7", "er100", "er300_dense", "gmm1000_s1"]
+    graphs = [(int(z["n_nodes"]), z["edges0"], z["edges1"]) for z in map(load_golden, names)]
+    batch = [hub] + [graphs[i % len(graphs)] for i in range(19)]
+    w, mode = ((engine.load_weights(engine.DEFAULT_UNIT), _lib.MD_COST_UNIT) if cost == "unit" else
+               (engine.load_weights(engine.DEFAULT_DEGREE), _lib.MD_COST_DEGREE))
+    node_w = None
+    if cost == "degree":
+        from mdcommunity_amd import graph as mgraph
+        node_w = mgraph.node_weight_array([mgraph.Graph_test.from_edges(n, e0, e1) for n, e0, e1 in batch])
+    out = {}
+    for wq in ("0", "1"):
+        monkeypatch.setenv("MD_WQ", wq)
+        e = _lib.Engine(w, cost_mode=mode)
+        try:
+            e.load_graphs(batch, node_w=node_w)
+            e.reset()
+            out[wq] = [(s.tolist(), r.tolist()) for s, r in e.rollout()]
+        finally:
+            e.close()
+    assert len(out["1"]) == len(batch)
+    for i, (a, b) in enumerate(zip(out["0"], out["1"])):
+        assert a == b, i
+
+
+@pytest.mark.parametrize("cost", ["unit", "degree"])
 def test_dataflow_mode_same_rollouts(monkeypatch, cost):
     """The barrier-free dataflow mode of single-graph rollouts (MD_DF=1, default: tagged granules
     for the step record, rows and partials; the tiles derive phase A's pick from the arg-max
