@@ -105,6 +105,8 @@ struct md_ctx {
   int variant = 0;   // diagnostics knob (MD_VARIANT)
   int pair_on = 1;   // queue mode: paired tiles (MD_PAIR=0: one tile at a time)
   int wq_on = 1;     // queue mode: one work item per wave (md_wq_kernel; MD_WQ=0: per workgroup, md_queue_kernel)
+  int wqpark = 96;   // wave-item launches of more than this many graphs; at most this many still running ->
+                     // they continue in md_queue_kernel (whose per-step latency is lower; MD_WQPARK)
   int qpark = 8;     // queue mode: at most this many graphs left -> the lock-step kernel (MD_QPARK, 0 = off)
   double last_ms = 0.0;
   int last_launches = 0;
@@ -126,6 +128,8 @@ struct md_ctx {
   DevBuf<int> deg[2], live, gscr, pend, tr_action, tr_rank, tr_stat, glist, ctl;
   DevBuf<long long> tpart;  // grid-wide environment step: per-workgroup partials [2][TEAM_MAX_WG][16]
   DevBuf<int> lab_ok;       // per graph: the grid-wide step's class labels are current
+  DevBuf<int> gscr_team;    // the grid-wide step's graph-local scratch (GSCR_TEAM_WORDS x the largest n)
+  int team_owner = -1;      // the graph whose class labels gscr_team holds
   DevBuf<uint16_t> prank;   // static union ranks (team_env_step), graphs of <= 65535 nodes
   DevBuf<float> H[2][2], h0tab[2], q, spart, apart, ybuf, hbuf, tr_q, node_w;
   DevBuf<unsigned long long> xbuf;
@@ -199,7 +203,7 @@ struct md_ctx {
       H[l][0].release(); H[l][1].release();
     }
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
-    tr_stat.release(); glist.release(); gtoff.release(); ctl.release(); tpart.release(); lab_ok.release(); prank.release(); q.release(); spart.release();
+    tr_stat.release(); glist.release(); gtoff.release(); ctl.release(); tpart.release(); lab_ok.release(); gscr_team.release(); prank.release(); q.release(); spart.release();
     apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); nbc.release(); qslot.release(); qg.release(); tr_q.release(); node_w.release();
     sres.release(); qspec.release(); bars.release(); dfbuf.release();
     df_graph.clear();
@@ -262,6 +266,7 @@ Params make_params(md_ctx* c) {
   p.tpart = c->tpart.p;
   p.tctl = c->ctl.p + CTL_TEAM;
   p.lab_ok = c->lab_ok.p;
+  p.gscr_team = c->gscr_team.p;
   p.prank = c->prank.p;
   p.spart = c->spart.p;
   p.apart = c->apart.p;
@@ -506,6 +511,12 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
                         (!phase_a_fits_lds_host(c->hinfo[gl[0]].n, c->hinfo[gl[0]].e[0] + c->hinfo[gl[0]].e[1]) ||
                          (c->variant & 64));
   const bool qmode = queue_mode_ok(c, run_mode) && n_env == 0 && !team_env;
+  if (team_env && c->team_owner != gl[0]) {
+    // gscr_team is shared by the loaded graphs: class labels another graph's grid-wide step
+    // left there are not this graph's
+    HIPCHK(c, hipMemsetAsync(c->lab_ok.p + gl[0], 0, sizeof(int), c->stream));
+    c->team_owner = gl[0];
+  }
   const int grid = qmode ? c->cus : grid_size(c, v, n_env);
   // speculative environment workgroups on the CUs a single-graph rollout leaves free
   // (single-node steps only: step > 1 takes several removals per prediction)
@@ -578,9 +589,13 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
     // tile 0 hands its derivation of phase A's early word to the speculative workgroups
     if (p.pre_ew != nullptr) p.self_ew = (unsigned long long*)(c->ctl.p + CTL_SELF);
   }
-  p.qmode = qmode ? (c->wq_on ? 2 : 1) : 0;
+  // wave items for launches with enough graphs to fill the chip's waves; the last wqpark running
+  // graphs of such a launch leave it (parked) and continue in the per-workgroup queue kernel, which
+  // in turn hands its last qpark to the lock-step kernel
+  const bool wq = qmode && c->wq_on && ngl > c->wqpark;
+  p.qmode = qmode ? (wq ? 2 : 1) : 0;
   p.qpair = c->pair_on ? 1 : 0;
-  p.qpark = c->qpark;
+  p.qpark = p.qmode == 2 ? c->wqpark : c->qpark;
   p.nglist = ngl;
   p.n_env = n_env;
   p.variant = c->variant;
@@ -775,6 +790,7 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_ENV_MODE")) c->env_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_PAIR")) c->pair_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_WQ")) c->wq_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MD_WQPARK")) c->wqpark = std::max(0, std::min(4096, std::atoi(v)));
   if (const char* v = std::getenv("MD_QPARK")) c->qpark = std::max(0, std::min(16, std::atoi(v)));
   if (const char* v = std::getenv("MD_HOST_HANDSHAKE")) c->host_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_POLL_US")) c->poll_us = std::atoi(v);
@@ -1033,6 +1049,12 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->ctl.alloc(CTL_WORDS));
   if (c->tpart.p == nullptr) HIPCHK(c, c->tpart.alloc(2 * (size_t)TEAM_MAX_WG * 16));
   HIPCHK(c, c->lab_ok.alloc(n_graphs));
+  {
+    int max_n = 1;
+    for (int g = 0; g < n_graphs; ++g) max_n = std::max(max_n, (int)n_nodes[g]);
+    HIPCHK(c, c->gscr_team.alloc((size_t)GSCR_TEAM_WORDS * max_n));
+    c->team_owner = -1;
+  }
   HIPCHK(c, c->prank.alloc(ranks.size()));
   HIPCHK(c, hipMemcpyAsync(c->prank.p, ranks.data(), sizeof(uint16_t) * ranks.size(), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->lab_ok.p, 0, sizeof(int) * n_graphs, c->stream));

@@ -104,6 +104,8 @@ struct Params {
   float* h0tab[2];                 // [layer] first-layer embedding: by degree (unit) / by node (degree cost)
   float* q;                        // per node (-inf = masked)
   int* gscr;                       // phase-A scratch in global memory for graphs too big for LDS: GSCR_WORDS per node
+  int* gscr_team;                  // the grid-wide step's graph-local scratch (GSCR_TEAM_WORDS x the largest n):
+                                   //   LMCC counts, second parent buffers, feature degrees, class labels
   long long* tpart;                // grid-wide environment step: per-workgroup partials [2][TEAM_MAX_WG][16]
   int* tctl;                       // grid-wide environment step: {actions (-1: none), first action}
   const uint16_t* prank;           // per node: static union rank (descending degree; team_env_step), or null
@@ -193,8 +195,9 @@ struct Params {
   int fp_short;                    // 1: mutual-LMCC fixed points end by the confirmation shortcut (mcc_fixed_point)
   int first_req;                   // 1: a rollout's first step requests degree-ranked speculative results (env_step)
 };
-// global-mode environment scratch words per node (md_env.h env_view, team_env_step)
-constexpr int GSCR_WORDS = 10;
+// global-mode environment scratch words per node (md_env.h env_view: parents, degrees) and the
+// grid-wide step's own words per node of the graph it runs (team_env_step, one graph per launch)
+constexpr int GSCR_WORDS = 4, GSCR_TEAM_WORDS = 6;
 // dataflow buffer size (granules) for graphs of at most n nodes / mt tiles
 inline long long df_granules(int n, int mt) { return 64 + 772LL * mt + 8LL * 64 * n; }
 

@@ -971,8 +971,7 @@ __device__ __forceinline__ EnvView<GL> env_view(KParams& p, const GraphInfo& gi,
   }
   E.gcov = p.covered + gi.node_off;
   if constexpr (GL) {
-    // par0, par1, deg0, deg1, LMCC counts (team step), the team step's second parent buffers and
-    // its degree arrays (env_layout's global-mode counterpart; GSCR_WORDS per node)
+    // par0, par1, deg0, deg1 (env_layout's global-mode counterpart; GSCR_WORDS per node)
     int* gs = p.gscr + GSCR_WORDS * (size_t)gi.node_off;
     E.par0 = gs;
     E.par1 = gs + n;
@@ -1639,7 +1638,7 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
                                  int* pr, int* cc, int* deg_zero = nullptr, int* cls = nullptr, bool restrict_cls = false,
                                  const lds_u16* rk = nullptr) {
   const int n = E.gi->n, et = E.et, e0 = E.e0;
-  int* const pb[2][2] = {{E.par0, E.par1}, {E.par0 + 5 * n, E.par0 + 6 * n}};  // gscr: par0, par1 | par0', par1'
+  int* const pb[2][2] = {{E.par0, E.par1}, {p.gscr_team + n, p.gscr_team + 2 * n}};  // par0, par1 | par0', par1'
   const bool rs = restrict_cls && cls != nullptr && cover >= 0;
   const int La = rs ? uf_load(cls, cover) : -1;  // a's class
   if (T.acc != nullptr && threadIdx.x == 0) T.t = wall_clock64();
@@ -1902,9 +1901,11 @@ __device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_f
   GraphVar& gv = *(GraphVar*)(lds_base() + L_GV);
   const bool books = blockIdx.x == 0;
   const EnvView<true> E = env_view<true>(p, gi, (int*)(lds_base() + L_SCR));
-  int* cnt = p.gscr + GSCR_WORDS * (size_t)gi.node_off + 4 * n;
-  int* dg = p.gscr + GSCR_WORDS * (size_t)gi.node_off + 7 * n;  // the features' degrees (2n)
-  int* cls = p.gscr + GSCR_WORDS * (size_t)gi.node_off + 9 * n;  // class labels (team_fixed_point)
+  // (gscr_team: graph-local, sized for the largest loaded graph; md_abi.cpp clears lab_ok of a
+  // graph whenever another graph ran the grid-wide step since it last did)
+  int* cnt = p.gscr_team;                // LMCC counts (n)
+  int* dg = p.gscr_team + 3 * n;         // the features' degrees (2n)
+  int* cls = p.gscr_team + 5 * n;        // class labels (team_fixed_point)
   bool zeroed = false;  // dg zeroed by a fixed point's init pass
 
   // every workgroup follows the same control flow: alive counts and s0 from the graph's

@@ -52,9 +52,55 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 __device__ __forceinline__ int wq_uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+// The lane index, opaque to the optimiser: every lane-dependent address of an item derives from
+// it, so none is hoisted out of the item loop (hoisted, the offsets of all the items' pieces stay
+// live across the loop and spill, and each scratch reload -- a vector-memory load -- makes the
+// wave wait for every load in flight before it)
+__device__ __forceinline__ int wq_lane() {
+  int l = (int)threadIdx.x & 63;
+  asm volatile("" : "+v"(l));
+  return l;
+}
 __device__ __forceinline__ unsigned long long wq_uni64(unsigned long long x) {
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)x), hi = __builtin_amdgcn_readfirstlane((unsigned)(x >> 32));
   return ((unsigned long long)hi << 32) | lo;
+}
+
+// Piece profile of the wave items (builds with -DMD_QPROF, md_profile with MD_VARIANT bit 8):
+// device ticks per piece summed over items in prof[20 + 8 (it - 1) + piece] (scripts/batch_prof.py)
+#ifdef MD_QPROF
+#define WQTS_INIT(it_)                                                                                \
+  unsigned long long* wqd_ = (kp().prof != nullptr && (kp().variant & 8)) ? kp().prof + 20 + 8 * ((it_) - 1) : nullptr; \
+  unsigned long long wqt_ = wall_clock64()
+#define WQTS(k)                                                        \
+  do {                                                                 \
+    if (wqd_ != nullptr && lane_id() == 0) {                           \
+      const unsigned long long now_ = wall_clock64();                  \
+      atomicAdd(wqd_ + (k), now_ - wqt_);                              \
+      wqt_ = now_;                                                     \
+    }                                                                  \
+  } while (0)
+#define WQTS_RESET() wqt_ = wall_clock64()
+#define WQTA_INIT()                                                                                      \
+  unsigned long long* wqd_ = (kp().prof != nullptr && (kp().variant & 8)) ? kp().prof + 88 : nullptr; \
+  unsigned long long wqt_ = wall_clock64()
+#else
+#define WQTA_INIT() do {} while (0)
+#define WQTS_INIT(it_) do {} while (0)
+#define WQTS(k) do {} while (0)
+#define WQTS_RESET() do {} while (0)
+#endif
+
+// Event log of graph slot 0 (diagnostics, md_profile with MD_VARIANT bit 4): {event, wall clock}
+// pairs after the first 8 profile records -- 0 environment step starts, 1..3 tile stage 1..3
+// complete, 4 virtual-node part 2 done (scripts/wq_timeline.py)
+__device__ __forceinline__ void wq_event(KParams& p, int gl, int ev) {
+  if (p.prof == nullptr || !(p.variant & 4) || gl != 0 || p.prof_cap < 16) return;
+  const unsigned long long k = atomicAdd(p.prof + 8 * PROF_SLOTS - 1, 1ull);
+  if (8 * PROF_SLOTS + 2 * k + 1 < (unsigned long long)p.prof_cap * PROF_SLOTS) {
+    p.prof[8 * PROF_SLOTS + 2 * k] = (unsigned long long)ev;
+    p.prof[8 * PROF_SLOTS + 2 * k + 1] = wall_clock64();
+  }
 }
 
 // ------------------------------------------------------------------ per-wave queue operations
@@ -116,7 +162,7 @@ __device__ __forceinline__ void wq_push(KParams& p, int n, F&& f) {
 // x divided by max(sqrt(sum), 1e-12) in place.  WA is free afterwards (written again by the
 // caller before reads).
 __device__ __forceinline__ void wq_norm_rows(float* wa, f4 (&x)[4]) {
-  const int lane = lane_id(), ar = lane & 15, ak = lane >> 4;
+  const int lane = wq_lane(), ar = lane & 15, ak = lane >> 4;
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
@@ -149,7 +195,7 @@ __device__ __forceinline__ void wq_norm_rows(float* wa, f4 (&x)[4]) {
 
 // x (accumulator layout) into WA as the transposed rotated block: WA[wq_o(col, row)]
 __device__ __forceinline__ void wq_put_acc(float* wa, const f4 (&x)[4]) {
-  const int lane = lane_id(), ar = lane & 15, ak = lane >> 4;
+  const int lane = wq_lane(), ar = lane & 15, ak = lane >> 4;
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
@@ -162,10 +208,13 @@ __device__ __forceinline__ void wq_put_acc(float* wa, const f4 (&x)[4]) {
 // each batch is staged in WA and every lane adds, for each of its four rows, that row's entries
 // of the batch in list order (sequential float adds from 0, gather_pair's order).  Result:
 // WA[wq_o(k, r)] = P[r][k].
-constexpr int WQ_WIN = 4;
+#ifndef MD_WQ_WIN
+#define MD_WQ_WIN 4
+#endif
+constexpr int WQ_WIN = MD_WQ_WIN;
 __device__ __forceinline__ void wq_gather_list(KParams& p, const float* hp, int tot, int hdw, int l, float* wa,
                                                const lds_u16* wl) {
-  const int lane = lane_id(), q = lane & 15, rs = lane >> 4;
+  const int lane = wq_lane(), q = lane & 15, rs = lane >> 4;
   int offm[4], endm[4];
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
@@ -176,35 +225,48 @@ __device__ __forceinline__ void wq_gather_list(KParams& p, const float* hp, int 
 #pragma unroll
   for (int m = 0; m < 4; ++m) acc[m] = make_float4(0.f, 0.f, 0.f, 0.f);
   const int nb = (tot + 15) >> 4;
-  float4 xw[WQ_WIN][4];
-  auto issue = [&](int b, float4 (&x)[4]) {
+  // loads without branches (entries past the list's end re-read its last row, unused): an
+  // exec-masked load makes the compiler's wait counting give up (vmcnt(0) at the join)
+  const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(hp), 0, 0x7fffffff, 0x00020000);
+  v4f xw[WQ_WIN][4];
+  auto issue = [&](int b, v4f (&x)[4]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int e = 16 * b + rs + 4 * i;
-      if (b < nb && e < tot) x[i] = ldc4(hp, (int)wl[e] * 256 + q * 16);
+      const int e = min(16 * b + rs + 4 * i, tot - 1);
+      x[i] = __builtin_amdgcn_raw_buffer_load_b128(rsc, (int)wl[e] * 256 + q * 16, 0, 16 /* sc1 */);
     }
   };
   float4* stg = (float4*)wa;
-  auto consume = [&](int b, const float4 (&x)[4]) {
+  auto consume = [&](int b, const v4f (&x)[4]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      if (16 * b + rs + 4 * i < tot) stg[(rs + 4 * i) * 16 + q] = x[i];
+      if (16 * b + rs + 4 * i < tot) stg[(rs + 4 * i) * 16 + q] = make_float4(x[i].x, x[i].y, x[i].z, x[i].w);
     wave_lds_sync();
+    // a row's entries of the batch in order, eight staged loads in flight before their adds
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const int lo = max(offm[m], 16 * b), hi = min(endm[m], 16 * b + 16);
-      for (int k = lo; k < hi; ++k) {
-        const float4 y = stg[(k - 16 * b) * 16 + q];
-        acc[m].x = acc[m].x + y.x;
-        acc[m].y = acc[m].y + y.y;
-        acc[m].z = acc[m].z + y.z;
-        acc[m].w = acc[m].w + y.w;
+      for (int k = lo; k < hi; k += 8) {
+        float4 y[8];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj)
+          if (k + jj < hi) y[jj] = stg[(k + jj - 16 * b) * 16 + q];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj)
+          if (k + jj < hi) {
+            acc[m].x = acc[m].x + y[jj].x;
+            acc[m].y = acc[m].y + y[jj].y;
+            acc[m].z = acc[m].z + y[jj].z;
+            acc[m].w = acc[m].w + y[jj].w;
+          }
       }
     }
     wave_lds_sync();
   };
+  if (nb > 0) {
 #pragma unroll
-  for (int u = 0; u < WQ_WIN; ++u) issue(u, xw[u]);
+    for (int u = 0; u < WQ_WIN; ++u) issue(u, xw[u]);
+  }
   for (int b = 0; b < nb; b += WQ_WIN) {
 #pragma unroll
     for (int u = 0; u < WQ_WIN; ++u) {
@@ -231,7 +293,7 @@ __device__ __forceinline__ void wq_gather_list(KParams& p, const float* hp, int 
 // by the group-0 lanes.  Same result layout.
 __device__ __forceinline__ void wq_gather_csr(KParams& p, const GraphInfo& gi, const float* hp, bool table, int l,
                                               int vrow, float* wa) {
-  const int lane = lane_id(), q = lane & 15, grp = lane >> 4;
+  const int lane = wq_lane(), q = lane & 15, grp = lane >> 4;
   const int* rp = p.rowptr[l] + gi.roff[l];
   const int* adj = p.adj[l] + gi.coff[l];
   const uint8_t* ca = p.calive[l] + gi.coff[l];
@@ -282,50 +344,42 @@ __device__ __forceinline__ void wq_gather_csr(KParams& p, const GraphInfo& gi, c
   wave_lds_sync();
 }
 
-// One layer of one tile on one wave (iteration it): gather, node update
-// relu([P.P1 | X.P2] . P3) on the MFMA chains of update_pair, row normalisation; then (it < 3)
-// the H rows and the virtual-node partial sums (S0 of the first-layer input at it == 1, S1 / S2
-// of the new rows).  Returns the normalised rows in accumulator layout (the attention's input at
-// it == 3).
-__device__ __forceinline__ void wq_layer(KParams& p, const GraphInfo& gi, int it, int j, int l, int vrow, int nv,
-                                         int hdw, int tot, bool listed, float* wa, const lds_u16* wl, f4 (&en)[4]) {
-  const int lane = lane_id(), ar = lane & 15, ak = lane >> 4;
-  const float* wi = lds_base() + L_W;
-  const int* deg = p.deg[l] + gi.node_off;
-  const float* hp;
-  bool table = false;
+// Layer l's source rows of iteration it: the previous iteration's H, or (it == 1) the first-layer
+// rows, by residual degree (unit cost: the precomputed table of the step's dmax, `table`) or by
+// node (degree cost).
+__device__ __forceinline__ const float* wq_src(KParams& p, const GraphInfo& gi, int it, int l, bool& table) {
+  table = false;
   if (it == 1) {
     table = p.node_w == nullptr;
-    hp = table ? first_layer_rows(p, gi, l) : p.h0tab[l] + (size_t)gi.node_off * EMB;
-  } else {
-    hp = p.H[l][(it - 2) & 1] + (size_t)gi.node_off * EMB;
+    return table ? first_layer_rows(p, gi, l) : p.h0tab[l] + (size_t)gi.node_off * EMB;
   }
-  // own rows X as MFMA A operands: lane (ak, ar) holds X[ar][4 s + ak]
-  int vs = vrow;
-  if (table && lane < TILE && vrow >= 0) vs = ldc(deg + vrow);
-  const int vx = __shfl(vs, ar, 64);
-  float xa[16];
+  return p.H[l][(it - 2) & 1] + (size_t)gi.node_off * EMB;
+}
+// The 16 own rows as MFMA A operands: lane (ak, ar) holds X[ar][4 s + ak] (vx: row ar's source
+// row in lane ar's group, -1 for an empty row).
+__device__ __forceinline__ void wq_xload(const float* hp, int vx, float (&xa)[16]) {
+  const int ak = wq_lane() >> 4;
+  const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(hp), 0, 0x7fffffff, 0x00020000);
+  const int base = max(vx, 0) * 256 + 4 * ak;  // (an empty row reads row 0, then zeroes it: no branch)
 #pragma unroll
-  for (int s = 0; s < 16; ++s) xa[s] = vx >= 0 ? ldc(hp + (size_t)vx * EMB + 4 * s + ak) : 0.f;
-  // first-layer rows of the listed neighbours by degree (unit cost, iteration 1): the list
-  // entries become table rows
-  if (listed && table) {
-    lds_u16* wlw = (lds_u16*)wl;
-    for (int i0 = 0; i0 < tot; i0 += 256) {
-      int d[4];
+  for (int s = 0; s < 16; ++s)
+    xa[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsc, base + 16 * s, 0, 16 /* sc1 */));
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = i0 + lane + 64 * u;
-        d[u] = i < tot ? ldc(deg + (int)wl[i]) : 0;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = i0 + lane + 64 * u;
-        if (i < tot) wlw[i] = (uint16_t)d[u];
-      }
-    }
-    wave_lds_sync();
-  }
+  for (int s = 0; s < 16; ++s) xa[s] = vx >= 0 ? xa[s] : 0.f;
+}
+
+// One layer of one tile on one wave (iteration it), in two parts so the caller can issue the next
+// layer's loads between them.  Front: S0 (it == 1: column sums of the first-layer input rows) and
+// the gather; back: node update relu([P.P1 | X.P2] . P3) on the MFMA chains of update_pair, row
+// normalisation, the H rows and (it < 3) the virtual-node partial sums S1 / S2.  `en` returns
+// the normalised rows in accumulator layout (the attention's input at it == 3).
+__device__ __forceinline__ void wq_layer_front(KParams& p, const GraphInfo& gi, int it, int j, int l, int vrow, int nv,
+                                               int hdw, int tot, bool listed, float* wa, const lds_u16* wl,
+                                               const float (&xa)[16]) {
+  const int lane = wq_lane(), ar = lane & 15, ak = lane >> 4;
+  WQTS_INIT(it);
+  bool table;
+  const float* hp = wq_src(p, gi, it, l, table);
   if (it == 1) {
     // S0: column sums of the first-layer input rows (col_sum16's order)
 #pragma unroll
@@ -341,8 +395,17 @@ __device__ __forceinline__ void wq_layer(KParams& p, const GraphInfo& gi, int it
     stc(p.spart + (size_t)(gi.tile_off + j) * 384 + l * 64 + lane, s0);
     wave_lds_sync();
   }
+  WQTS(1);  // own rows' wait, S0
   if (listed) wq_gather_list(p, hp, tot, hdw, l, wa, wl);
   else wq_gather_csr(p, gi, hp, table, l, vrow, wa);
+  WQTS(2);  // gather
+}
+
+__device__ __forceinline__ void wq_layer_back(KParams& p, const GraphInfo& gi, int it, int j, int l, int vrow, int nv,
+                                              float* wa, const float (&xa)[16], f4 (&en)[4]) {
+  const int lane = wq_lane(), ar = lane & 15, ak = lane >> 4;
+  WQTS_INIT(it);
+  const float* wi = lds_base() + L_W;
   // update, part 1: P.P1 and X.P2 (update_pair's chains for each column block)
   f4 a1[4], a2[4];
 #pragma unroll
@@ -386,6 +449,7 @@ __device__ __forceinline__ void wq_layer(KParams& p, const GraphInfo& gi, int it
   for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
     for (int r = 0; r < 4; ++r) en[cb][r] = fmaxf(a3[cb][r], 0.f);
+  WQTS(3);  // update
   wq_norm_rows(wa, en);
   if (it < 3) {
     wq_put_acc(wa, en);
@@ -412,6 +476,7 @@ __device__ __forceinline__ void wq_layer(KParams& p, const GraphInfo& gi, int it
     }
     wave_lds_sync();
   }
+  WQTS(4);  // normalisation, sums and stores
 }
 
 // Iteration 3 of one tile on one wave after both layers: attention_q_tile's pieces --
@@ -420,8 +485,9 @@ __device__ __forceinline__ void wq_layer(KParams& p, const GraphInfo& gi, int it
 // tile's arg-max partial.  y and the graph scalars come from the head granules (tag 1).
 __device__ __forceinline__ void wq_attention(KParams& p, const GraphInfo& gi, int g, int j, int vrow,
                                              f4 (&e0)[4], f4 (&e1)[4], float* wa) {
-  const int lane = lane_id(), ar = lane & 15, ak = lane >> 4;
+  const int lane = wq_lane(), ar = lane & 15, ak = lane >> 4;
   const float* wi = lds_base() + L_W;
+  WQTA_INIT();
   // head granules: y of both layers (lanes), the graph scalars (lanes 0..15)
   float yv[2], gsv = 0.f;
   {
@@ -447,6 +513,7 @@ __device__ __forceinline__ void wq_attention(KParams& p, const GraphInfo& gi, in
     yv[1] = __uint_as_float((unsigned)gr[1]);
     gsv = __uint_as_float((unsigned)gr[2]);
   }
+  WQTS(3);  // head granules
   // F_l = tanh(E_l . T + b)
   f4 f[2][4];
 #pragma unroll
@@ -469,6 +536,7 @@ __device__ __forceinline__ void wq_attention(KParams& p, const GraphInfo& gi, in
       for (int r = 0; r < 4; ++r) f[l][cb][r] = tanhf(f[l][cb][r] + b);
     }
   }
+  WQTS(0);  // tanh GEMM
   // gate dot products per row: kind 0 F0F0, 1 F1F1, 2 F0F1 (the product rounded, then the
   // lw-weighted FMA chain over the columns in order)
   float dk[3];
@@ -500,6 +568,7 @@ __device__ __forceinline__ void wq_attention(KParams& p, const GraphInfo& gi, in
   }
   const float lb = wi[W_ILB];
   const float g0 = other_gate(0, dk[0], dk[1], dk[2], lb), g1 = other_gate(1, dk[0], dk[1], dk[2], lb);
+  WQTS(1);  // dots + gates
   // E'_l = F_l + g_l F_other (mul then add), normalised
   f4 m[2][4];
 #pragma unroll
@@ -513,6 +582,7 @@ __device__ __forceinline__ void wq_attention(KParams& p, const GraphInfo& gi, in
   }
   wq_norm_rows(wa, m[0]);
   wq_norm_rows(wa, m[1]);
+  WQTS(2);  // mix + norm
   const float cpl = wi[W_ICP + lane];
   // per layer: e = sum_b (h y_b) cp_b as the hidden layer's A operands, then relu(e . H1)
   f4 hid[2][2];
@@ -544,6 +614,7 @@ __device__ __forceinline__ void wq_attention(KParams& p, const GraphInfo& gi, in
       for (int s = 0; s < 16; ++s) hid[l][cb] = mfma16(acc[s >> 1][s & 1], wi[W_IH1 + (cb * 16 + s) * 64 + lane], hid[l][cb]);
     }
   }
+  WQTS(4);  // e-chain + hidden GEMM
   // Q head per (layer, row): relu(hidden) . w2[0..31] then the aux terms, as one FMA chain
   float* hq = wa;  // [2][16][33] (WA and WL: the lists are dead here)
 #pragma unroll
@@ -563,6 +634,7 @@ __device__ __forceinline__ void wq_attention(KParams& p, const GraphInfo& gi, in
     ql = a;
   }
   wave_lds_sync();
+  WQTS(5);  // Q head
   const float q1 = __shfl(ql, 16 + (lane & 15), 64);
   const float w0 = __shfl(gsv, 0, 64), w1 = __shfl(gsv, 1, 64);
   float bm = NEG_INF, bs = NEG_INF;
@@ -581,13 +653,15 @@ __device__ __forceinline__ void wq_attention(KParams& p, const GraphInfo& gi, in
     if (c2 != 0) argmax_combine(bm, bs, bi, bc, m2, s2, i2, c2);
   }
   if (lane == 0) stc4(p.apart + (size_t)(gi.tile_off + j) * 4, 0, make_float4(bm, bs, __int_as_float(bi), __int_as_float(bc)));
+  WQTS(6);  // q, arg-max partial, stores
 }
 
 // Work item TILE(it, j) of graph g (slot gl) on one wave: both layers, then (it == 3) the
 // attention and Q head.
 __device__ __forceinline__ void wq_tile(KParams&, int g, int gl, int it, int j) {
   KParams& p = kp();
-  const int lane = lane_id();
+  const int lane = wq_lane();
+  WQTS_INIT(it);
   float* const wa = wq_area() + WQ_WA;
   lds_u16* const wl = (lds_u16*)(uint16_t*)(wq_area() + WQ_WL);
   const GraphInfo gi = p.ginfo[g];
@@ -634,17 +708,59 @@ __device__ __forceinline__ void wq_tile(KParams&, int g, int gl, int it, int j) 
     }
     wave_lds_sync();
   }
+  // own-row sources of both layers; unit cost, iteration 1: rows and list entries by residual
+  // degree (the entries of both lists resolved in one round trip)
+  bool table;
+  const float* hp0 = wq_src(p, gi, it, 0, table);
+  const float* hp1 = wq_src(p, gi, it, 1, table);
+  int vs0 = vrow, vs1 = vrow;
+  if (table && lane < TILE && vrow >= 0) {
+    vs0 = ldc(p.deg[0] + gi.node_off + vrow);
+    vs1 = ldc(p.deg[1] + gi.node_off + vrow);
+  }
+  float xa0[16], xa1[16];
+  wq_xload(hp0, __shfl(vs0, lane & 15, 64), xa0);
+  if (table && (listed0 || listed1)) {
+    const int* dg0 = p.deg[0] + gi.node_off;
+    const int* dg1 = p.deg[1] + gi.node_off;
+    lds_u16* w1 = wl + WQ_LIST_MAX;
+    const int t0 = listed0 ? tot0 : 0, t1 = listed1 ? tot1 : 0;
+    for (int i0 = 0; i0 < max(t0, t1); i0 += 128) {
+      int d0[2], d1[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int i = i0 + lane + 64 * u;
+        d0[u] = i < t0 ? ldc(dg0 + (int)wl[i]) : 0;
+        d1[u] = i < t1 ? ldc(dg1 + (int)w1[i]) : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int i = i0 + lane + 64 * u;
+        if (i < t0) wl[i] = (uint16_t)d0[u];
+        if (i < t1) w1[i] = (uint16_t)d1[u];
+      }
+    }
+    wave_lds_sync();
+  }
   f4 e0[4], e1[4];
-  wq_layer(p, gi, it, j, 0, vrow, nv, hdw, tot0, listed0, wa, wl, e0);
-  wq_layer(p, gi, it, j, 1, vrow, nv, hdw, tot1, listed1, wa, wl + WQ_LIST_MAX, e1);
-  if (it == 3) wq_attention(p, gi, g, j, vrow, e0, e1, wa);
+  WQTS(0);  // header, rows, lists (and their first-layer rows)
+  wq_layer_front(p, gi, it, j, 0, vrow, nv, hdw, tot0, listed0, wa, wl, xa0);
+  wq_xload(hp1, __shfl(vs1, lane & 15, 64), xa1);  // (arrives under layer 0's update)
+  wq_layer_back(p, gi, it, j, 0, vrow, nv, wa, xa0, e0);
+  wq_layer_front(p, gi, it, j, 1, vrow, nv, hdw, tot1, listed1, wa, wl + WQ_LIST_MAX, xa1);
+  wq_layer_back(p, gi, it, j, 1, vrow, nv, wa, xa1, e1);
+  if (it == 3) {
+    WQTS_RESET();
+    wq_attention(p, gi, g, j, vrow, e0, e1, wa);
+    WQTS(6);  // attention + Q head
+  }
 }
 
 // ------------------------------------------------------------------ one wave's virtual node
 // graph_sum of slot k on one wave: lane c adds both layers' column c (outputs c, 64 + c), four
 // quarters of the tiles each in order, then the quarters in order.
 __device__ __forceinline__ void wq_graph_sum(KParams& p, const GraphInfo& gi, int nt, int k, float& s0, float& s1) {
-  const int lane = lane_id();
+  const int lane = wq_lane();
   const float* sp = p.spart + (size_t)gi.tile_off * 384 + k * 128 + lane;
   const int per = (nt + 3) >> 2;
   float part[2][4];
@@ -683,7 +799,7 @@ __device__ __forceinline__ void wq_graph_sum(KParams& p, const GraphInfo& gi, in
 // vrow_update on one wave: y' = normalize(relu([s.P1 | y.P2] . P3)) for both layers, each
 // output column's chains split in vrow_update's four partial chains, summed in order.
 __device__ __forceinline__ void wq_vrow(float s0, float s1, float& y0, float& y1, float* wa) {
-  const int c = lane_id();
+  const int c = wq_lane();
   const float* wi = lds_base() + L_W;
   wa[c] = s0;
   wa[64 + c] = s1;
@@ -723,7 +839,7 @@ __device__ __forceinline__ void wq_vrow(float s0, float s1, float& y0, float& y1
 // granules (tag 1) for the iteration-3 tiles.
 __device__ __forceinline__ void wq_vn(KParams&, int g, int part) {
   KParams& p = kp();
-  const int lane = lane_id();
+  const int lane = wq_lane();
   float* const wa = wq_area() + WQ_WA;
   const float* wi = lds_base() + L_W;
   const GraphInfo gi = p.ginfo[g];
@@ -820,7 +936,7 @@ __device__ __forceinline__ void wq_vn(KParams&, int g, int part) {
     const double N = (double)gi.n;
     const GraphVar* gvp = p.gvar + g;
     if (k == 0) gsv = (float)((double)ldc(&gvp->n_cov) / N);
-    else if (k == 1) gsv = (float)((double)ldc(&gvp->counter[ll]) / (double)gi.e[ll]);
+    else if (k == 1) gsv = (float)((double)ldc(&gvp->counter[ll]) / (double)(ll == 0 ? gi.e[0] : gi.e[1]));
     else if (k == 2) {
       const long long th = __hip_atomic_load((const __attribute__((address_space(1))) long long*)&gvp->twohop[ll],
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -846,6 +962,7 @@ __device__ void wq_env(KParams& p, float* lds, unsigned item) {
   const int ng = p.nglist;
   const int it = (int)((item >> 3) & 3u), gl = q_item_gl(item);
   const int g = p.glist[gl];
+  if (threadIdx.x == 0) wq_event(p, gl, 0);
   const bool lds_env = phase_a(p, g, it != 0, lds, false);
   const GraphVar& gv = *(const GraphVar*)(lds + L_GV);
   const int st = gv.status, nl = gv.n_live;
@@ -944,7 +1061,11 @@ __device__ __forceinline__ void wq_loop(KParams&, const float* __restrict__ wimg
       tot += cnt;
       __syncthreads();
     }
-    const int first = min(tot, q_admit(p));
+    // admission: every wave of the chip runs its own items, so more graphs run at once than in
+    // md_queue_kernel: up to two per workgroup (sweep over 4096 graphs: 160 / 512 / 1024 / all ->
+    // 366 / 265 / 271 / 281 ms); MD_VARIANT bits 16+ override
+    const int vadm = (int)((unsigned)p.variant >> 16);
+    const int first = min(tot, vadm > 0 ? vadm : 2 * (int)gridDim.x);
     if (threadIdx.x == 0) {
       __hip_atomic_store((g_u32*)(p.qctl + QC_REM), (unsigned)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store((g_u32*)(p.qctl + QC_ADMIT), (unsigned)(first < tot ? run[first] : ng), __ATOMIC_RELAXED,
@@ -965,6 +1086,7 @@ __device__ __forceinline__ void wq_loop(KParams&, const float* __restrict__ wimg
   unsigned cont = 0u;
   bool done = false;
   unsigned long long tq = wall_clock64();
+  const unsigned long long tq0 = tq;
   while (true) {
     if (ctl[WQC_REQ] != 0) {
       wq_group(p, wimg);
@@ -990,6 +1112,9 @@ __device__ __forceinline__ void wq_loop(KParams&, const float* __restrict__ wimg
     if (qp != nullptr && lane == 0) {
       ti = wall_clock64();
       atomicAdd(qp + 16, ti - tq);
+      // waiting ticks over the launch in 1.31 ms buckets (slots 20..63; with MD_VARIANT bit 8
+      // those slots hold the item pieces instead)
+      if (!(p.variant & 8)) atomicAdd(qp + 20 + min(43, (int)((ti - tq0) >> 17)), ti - tq);
     }
     if (kind == QK_EXIT || kind == 0u) {
       done = true;
@@ -1030,6 +1155,7 @@ __device__ __forceinline__ void wq_loop(KParams&, const float* __restrict__ wimg
       next = 4;
     }
     if (next != 0) {
+      if (lane == 0) wq_event(p, gl, next);
       const int nt = (wq_uni(ldc(p.qg + 2 * gl + 1)) >> 16) & 0xfff;
       if (next == 1) {
         wq_push(p, nt + 1, [&](int i) { return i < nt ? q_item(QK_TILE, 2, gl, i) : q_item(QK_VN, 1, gl, 0); });

@@ -1,8 +1,9 @@
 """GPU correctness of the batched configurations at full size (BASELINE.json configs[2] and the
 per-GPU slice of configs[4]): 256 and 512 two-layer GMM graphs N=1000 (generator seeds 0..255 /
-0..511, mdcommunity_amd.gmm = the reference's U/GMM.py streams) rolled out in ONE
-md_queue_kernel launch (work queue, admission limit, two tiles per work item, asynchronous tie
-hand-shakes, K2 end-games) — the launch behind bench.py's `batch` object.
+0..511, mdcommunity_amd.gmm = the reference's U/GMM.py streams) rolled out in one md_wq_kernel
+launch (one work item per wave, work queue, admission limit, asynchronous tie hand-shakes, K2
+end-games) whose tail continues in md_queue_kernel and the lock-step kernel — the launches behind
+bench.py's `batch` object.
 
 Every graph's (removal sequence, LMCC trace) must equal its own single-graph rollout
 (md_rollout_kernel, dedicated mode), and seeds 0-2 must reproduce the certified sequences and
@@ -92,10 +93,11 @@ def test_c3_256_graphs_one_queue_launch_and_tail(graphs, weights, single):
     """configs[2]: 256 graphs in one queue-mode launch (its last <= 8 running graphs continue
     in one lock-step launch, MD_QPARK) == 256 single-graph rollouts."""
     mr, outs, launches = batch_rollout(weights, graphs[:256])
-    # the queue launch, then the lock-step launch of the graphs it parked -- none when the last
-    # running graphs all end (typically by a K2 end-game) at the environment step that would
-    # park them, which depends on the order the workgroups reach them
-    assert launches in (1, 2)
+    # the wave-item launch, its last MD_WQPARK running graphs in one per-workgroup queue launch,
+    # whose last MD_QPARK continue in one lock-step launch -- fewer when the graphs a launch would
+    # park all end (typically by a K2 end-game) at the environment step that would park them,
+    # which depends on the order the workgroups reach them
+    assert launches in (1, 2, 3)
     assert sum(len(s) for s, _ in outs) > 256 * 20
     check_against_single(mr, outs, single, 0)
     check_goldens(mr, outs)
@@ -106,7 +108,7 @@ def test_c5_slice_512_graphs_one_queue_launch_and_tail(graphs, weights, single):
     """configs[4]'s per-GPU slice: 512 graphs (G_CAP) in one queue launch and its lock-step
     tail launch == single-graph rollouts."""
     mr, outs, launches = batch_rollout(weights, graphs)
-    assert launches in (1, 2)  # (see the C3 test)
+    assert launches in (1, 2, 3)  # (see the C3 test)
     check_against_single(mr, outs, single, 0)
     check_goldens(mr, outs)
 

@@ -580,6 +580,9 @@ def test_wave_items_match_workgroup_items(monkeypatch, cost):
         from mdcommunity_amd import graph as mgraph
         node_w = mgraph.node_weight_array([mgraph.Graph_test.from_edges(n, e0, e1) for n, e0, e1 in batch])
     out = {}
+    # (MD_WQPARK=0: the wave kernel runs this 20-graph batch to the end -- by default a launch of
+    # at most MD_WQPARK graphs goes to md_queue_kernel)
+    monkeypatch.setenv("MD_WQPARK", "0")
     for wq in ("0", "1"):
         monkeypatch.setenv("MD_WQ", wq)
         e = _lib.Engine(w, cost_mode=mode)
