@@ -27,6 +27,7 @@
 constexpr int WQ_AREA = 2048;                  // floats of LDS per wave
 constexpr int WQ_WA = 0, WQ_WL = 64 * LDT;     // WA [64][17] floats, WL [2][WQ_LIST_MAX] u16
 constexpr int WQ_LIST_MAX = 960;               // alive entries per layer the list area holds
+constexpr int WQ_SPEC_WORDS = 256;             // list words per layer loaded with the header
 static_assert(WQ_WL + WQ_LIST_MAX <= WQ_AREA, "list area");
 // A 16-row block in WA is transposed with a 17-float pitch (wq_o(k, row)): every access pattern
 // below is one lane base plus immediate offsets (the rotated paired-tile layout needs a lane
@@ -598,15 +599,20 @@ __device__ __forceinline__ void wq_attention(KParams& p, const GraphInfo& gi, in
       acc[s >> 1][s & 1] = 0.f;
     }
     wave_lds_sync();
-#pragma unroll 4
+    // {y_b, cp_b} pairs in WA, read by every lane at one address (an LDS broadcast)
+    wa[2 * lane] = yv[l];
+    wa[2 * lane + 1] = cpl;
+    wave_lds_sync();
+    const float2* yc = (const float2*)wa;
+#pragma unroll 8
     for (int b = 0; b < 64; ++b) {
-      const float yb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yv[l]), b));
-      const float cb_ = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cpl), b));
-      const f2v yy = {yb, yb};
-      const f2v cc = {cb_, cb_};
+      const float2 v = yc[b];
+      const f2v yy = {v.x, v.x};
+      const f2v cc = {v.y, v.y};
 #pragma unroll
       for (int k2 = 0; k2 < 8; ++k2) acc[k2] = __builtin_elementwise_fma(h[k2] * yy, cc, acc[k2]);
     }
+    wave_lds_sync();
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
       hid[l][cb] = f4{0.f, 0.f, 0.f, 0.f};
@@ -678,33 +684,40 @@ __device__ __forceinline__ void wq_tile(KParams&, int g, int gl, int it, int j) 
   const bool cacheable = slot < p.nbc_slots;
   int hdw = 0, hdx = 0, built = 0;
   const int* hd = p.nbc + (size_t)slot * NBC_INTS;
+  // the first WQ_SPEC_WORDS list words of each layer go out with the header (the lists' lengths
+  // are not known yet; longer lists load the rest after it)
+  constexpr int NS = WQ_SPEC_WORDS / 64;
+  int w0[NS], w1[NS];
   if (cacheable) {
     hdw = ldc(hd + lane);
     if (lane < 3) hdx = ldc(hd + 64 + lane);
     built = ldc(p.qg + 2 * QG_CAP + gl);
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      w0[u] = ldc(hd + NBC_HDR + lane + 64 * u);
+      w1[u] = ldc(hd + NBC_HDR + NBC_LWORDS + lane + 64 * u);
+    }
   }
   const int nv = __popcll(__ballot(lane < TILE && vrow >= 0));
   built = wq_uni(built);
   const int tot0 = __shfl(hdx, 0, 64), tot1 = __shfl(hdx, 1, 64), okf = __shfl(hdx, 2, 64);
   const bool ok = cacheable && built != 0 && okf != 0;
   const bool listed0 = ok && tot0 <= WQ_LIST_MAX, listed1 = ok && tot1 <= WQ_LIST_MAX;
-  // both layers' list entries (packed two per int)
+  // both layers' list entries (packed two per int) into WL
   {
     const int nw0 = listed0 ? (tot0 + 1) >> 1 : 0, nw1 = listed1 ? (tot1 + 1) >> 1 : 0;
     lds_i32* ww = (lds_i32*)(int*)(wq_area() + WQ_WL);
-    constexpr int NU = (WQ_LIST_MAX / 2 + 63) / 64;
-    int w0[NU], w1[NU];
 #pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const int i = lane + 64 * u;
-      w0[u] = i < nw0 ? ldc(hd + NBC_HDR + i) : 0;
-      w1[u] = i < nw1 ? ldc(hd + NBC_HDR + NBC_LWORDS + i) : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
+    for (int u = 0; u < NS; ++u) {
       const int i = lane + 64 * u;
       if (i < nw0) ww[i] = w0[u];
       if (i < nw1) ww[WQ_LIST_MAX / 2 + i] = w1[u];
+    }
+    if (nw0 > WQ_SPEC_WORDS || nw1 > WQ_SPEC_WORDS) {
+      for (int i = WQ_SPEC_WORDS + lane; i < max(nw0, nw1); i += 64) {
+        if (i < nw0) ww[i] = ldc(hd + NBC_HDR + i);
+        if (i < nw1) ww[WQ_LIST_MAX / 2 + i] = ldc(hd + NBC_HDR + NBC_LWORDS + i);
+      }
     }
     wave_lds_sync();
   }

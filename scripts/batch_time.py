@@ -18,6 +18,7 @@ eng = _lib.Engine(W)
 eng.load_graphs(graphs)
 eng.reset(); out = eng.rollout()
 rem = sum(len(o[0]) for o in out)
+lmax = max(len(o[0]) for o in out)
 ts, ws = [], []
 for _ in range(reps):
     t0 = time.perf_counter()
@@ -28,4 +29,5 @@ ts.sort(); ws.sort()
 print("batch %d (%s): removals %d, kernel ms best %.2f median %.2f -> %.0f removals/s; wall (reset + rollout) median %.2f ms -> %.0f removals/s" % (
     nb, sys.argv[3] if len(sys.argv) > 3 else "default", rem, ts[0], ts[len(ts) // 2], rem / ts[len(ts) // 2] * 1e3,
     ws[len(ws) // 2], rem / ws[len(ws) // 2] * 1e3), flush=True)
+print("  longest rollout %d removals: %.1f us of kernel per step of it" % (lmax, ts[len(ts) // 2] * 1e3 / lmax), flush=True)
 eng.close()
