@@ -123,7 +123,7 @@ struct md_ctx {
   DevBuf<GraphInfo> ginfo;
   DevBuf<GraphVar> gvar;
   size_t tot_tiles = 0;
-  DevBuf<int> rowptr[2], adj[2], epos[2], eu[2], ev[2];
+  DevBuf<int> rowptr[2], adj[2], adjx[2], epos[2], eu[2], ev[2];
   DevBuf<uint8_t> estate[2], calive[2], covered;
   DevBuf<int> deg[2], live, gscr, pend, tr_action, tr_rank, tr_stat, glist, ctl;
   DevBuf<long long> tpart;  // grid-wide environment step: per-workgroup partials [2][TEAM_MAX_WG][16]
@@ -198,7 +198,7 @@ struct md_ctx {
     ginfo.release();
     gvar.release();
     for (int l = 0; l < 2; ++l) {
-      rowptr[l].release(); adj[l].release(); epos[l].release(); eu[l].release(); ev[l].release();
+      rowptr[l].release(); adj[l].release(); adjx[l].release(); epos[l].release(); eu[l].release(); ev[l].release();
       estate[l].release(); calive[l].release(); deg[l].release(); h0tab[l].release();
       H[l][0].release(); H[l][1].release();
     }
@@ -249,6 +249,7 @@ Params make_params(md_ctx* c) {
   for (int l = 0; l < 2; ++l) {
     p.rowptr[l] = c->rowptr[l].p;
     p.adj[l] = c->adj[l].p;
+    p.adjx[l] = c->adjx[l].p;
     p.calive[l] = c->calive[l].p;
     p.epos[l] = c->epos[l].p;
     p.eu[l] = c->eu[l].p;
@@ -937,10 +938,11 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
     return fail(c, MD_EINVAL, "batch too large");
   // static CSR in reference order: row i lists i's neighbours in the order the edges appear
   // in G.edges() (the in_edges order of U/PrepareBatchGraph.py:151-160, U/graph_struct.py:63)
-  std::vector<int> rowptr[2], adj[2], epos[2], eu[2], ev[2];
+  std::vector<int> rowptr[2], adj[2], adjx[2], epos[2], eu[2], ev[2];
   for (int l = 0; l < 2; ++l) {
     rowptr[l].assign(tn + n_graphs, 0);
     adj[l].resize(2 * te[l]);
+    adjx[l].resize(2 * te[l]);
     epos[l].resize(2 * te[l]);
     eu[l].resize(te[l]);
     ev[l].resize(te[l]);
@@ -964,12 +966,16 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
       for (int i = 0; i < n; ++i) rp[i + 1] += rp[i];
       std::vector<int> fill(rp, rp + n);
       int* a = adj[l].data() + gi.coff[l];
+      int* ax = adjx[l].data() + gi.coff[l];
       int* ep = epos[l].data() + 2 * (size_t)gi.eoff[l];
+      const bool packs = gi.e[l] <= 65536 && n <= 65536;
       for (int k = 0; k < gi.e[l]; ++k) {
         const int u = eu[l][gi.eoff[l] + k], v = ev[l][gi.eoff[l] + k];
         ep[2 * k] = fill[v];
+        ax[fill[v]] = packs ? (k << 16) | u : -1;
         a[fill[v]++] = u;  // in_edges[v] gets u (U/PrepareBatchGraph.py:157)
         ep[2 * k + 1] = fill[u];
+        ax[fill[u]] = packs ? (k << 16) | v : -1;
         a[fill[u]++] = v;  // in_edges[u] gets v (:159)
       }
     }
@@ -1017,13 +1023,14 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->gvar.alloc(n_graphs));
   for (int l = 0; l < 2; ++l) {
     c->tot_e[l] = te[l];
-    HIPCHK(c, c->rowptr[l].alloc(rowptr[l].size()));
+    HIPCHK(c, c->rowptr[l].alloc(rowptr[l].size() + 4));  // + 4: env_stage_wide's 16-byte chunks
     HIPCHK(c, c->adj[l].alloc(std::max<size_t>(1, adj[l].size())));
+    HIPCHK(c, c->adjx[l].alloc(std::max<size_t>(1, adjx[l].size())));
     HIPCHK(c, c->epos[l].alloc(std::max<size_t>(1, epos[l].size())));
     HIPCHK(c, c->calive[l].alloc(std::max<size_t>(1, 2 * te[l])));
-    HIPCHK(c, c->eu[l].alloc(std::max<size_t>(1, eu[l].size())));
-    HIPCHK(c, c->ev[l].alloc(std::max<size_t>(1, ev[l].size())));
-    HIPCHK(c, c->estate[l].alloc(te[l] + 4));  // + 4: whole-word reads of the last states
+    HIPCHK(c, c->eu[l].alloc(eu[l].size() + 4));
+    HIPCHK(c, c->ev[l].alloc(ev[l].size() + 4));
+    HIPCHK(c, c->estate[l].alloc(te[l] + 16));  // + 16: whole-chunk reads of the last states
     HIPCHK(c, c->deg[l].alloc(tn));
     HIPCHK(c, c->h0tab[l].alloc(tn * EMB));
     HIPCHK(c, c->H[l][0].alloc(tn * EMB));
@@ -1031,12 +1038,13 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
     HIPCHK(c, hipMemcpyAsync(c->rowptr[l].p, rowptr[l].data(), sizeof(int) * rowptr[l].size(), hipMemcpyHostToDevice, c->stream));
     if (te[l]) {
       HIPCHK(c, hipMemcpyAsync(c->adj[l].p, adj[l].data(), sizeof(int) * adj[l].size(), hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->adjx[l].p, adjx[l].data(), sizeof(int) * adjx[l].size(), hipMemcpyHostToDevice, c->stream));
       HIPCHK(c, hipMemcpyAsync(c->epos[l].p, epos[l].data(), sizeof(int) * epos[l].size(), hipMemcpyHostToDevice, c->stream));
       HIPCHK(c, hipMemcpyAsync(c->eu[l].p, eu[l].data(), sizeof(int) * eu[l].size(), hipMemcpyHostToDevice, c->stream));
       HIPCHK(c, hipMemcpyAsync(c->ev[l].p, ev[l].data(), sizeof(int) * ev[l].size(), hipMemcpyHostToDevice, c->stream));
     }
   }
-  HIPCHK(c, c->covered.alloc(tn + 4));
+  HIPCHK(c, c->covered.alloc(tn + 16));
   HIPCHK(c, c->live.alloc(4 * tn));  // {node, CSR begin l0, l1, extents} per live position
   HIPCHK(c, c->gscr.alloc(GSCR_WORDS * tn));  // global-mode environment scratch (always, so MD_VARIANT=64 can force that mode)
   HIPCHK(c, c->pend.alloc(tn));

@@ -91,6 +91,7 @@ struct Params {
   GraphVar* gvar;
   const int* rowptr[2];            // static CSR (neighbour order = reference in_edges order)
   const int* adj[2];
+  const int* adjx[2];              // per CSR entry: (layer-local edge id << 16) | neighbour (e_l, n < 2^16; else -1)
   uint8_t* calive[2];              // per CSR entry: 1 while its edge is alive
   const int* epos[2];              // per undirected edge: its two CSR entry positions
   const int* eu[2];                // undirected endpoints (graph-local ids)

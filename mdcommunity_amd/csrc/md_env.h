@@ -530,7 +530,7 @@ struct SpecAbort {
   int step;                       // this request's step
 };
 template <bool GL>
-__device__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long long* acc, int cover, int* cc,
+__device__ __forceinline__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, unsigned long long* acc, int cover, int* cc,
                                const SpecAbort* ab = nullptr) {
   const EnvView<GL> E = Ein;  // fields in registers
   const int n = E.gi->n;
@@ -774,7 +774,7 @@ struct EnvAgg {
 // -- the graph's HBM arrays (phase A) or a speculative result slot -- and q = -inf for every
 // node when q is given.  One fused block exchange for the scan and all reductions.
 template <bool GL>
-__device__ EnvAgg env_features(const EnvView<GL>& E, int n, int* gdeg0, int* gdeg1, float* lv, float* q) {
+__device__ __forceinline__ EnvAgg env_features(const EnvView<GL>& E, int n, int* gdeg0, int* gdeg1, float* lv, float* q) {
   const int e0 = E.e0;
   // residual degrees by edge-parallel atomics
   for (int x = threadIdx.x; x < n; x += NTHREADS) {
@@ -1051,10 +1051,119 @@ __device__ __forceinline__ void env_stage_dynamic(const EnvView<false>& E, int n
   for (int x = threadIdx.x; x < n; x += NTHREADS) E.cov8[x] = ldc(E.gcov + x);
 }
 
+// LDS mode, one pass: every segment of the environment (endpoints and CSR row pointers of both
+// layers, edge states, covered flags) read as 16-byte chunks from its 16-byte-aligned start
+// (the bytes before and after a segment are other graphs' or allocation padding, discarded),
+// all of a thread's chunks in flight before the first is written to LDS -- one or two round
+// trips where env_stage_static + env_stage_dynamic take ~7 dependent batches on a C3 graph.
+// The states and covered flags are written by other workgroups: agent-coherent buffer loads.
+__device__ __forceinline__ v4u ld16_sc1(const void* base, int byte_off) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(base), 0, 0x7fffffff, 0x00020000);
+  return __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16 /* sc1 */));
+}
+// bytes [16 c - lead, 16 c - lead + 16) of a byte segment of cnt bytes -> dst
+__device__ __forceinline__ void stage_bytes(lds_u8* dst, const v4u& w, int c, int lead, int cnt) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int x = 16 * c + i - lead;
+    if (x >= 0 && x < cnt) dst[x] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+  }
+}
+__device__ __forceinline__ void env_stage_wide(const EnvView<false>& E, int n) {
+  const int tid = threadIdx.x, e0 = E.e0, e1 = E.et - E.e0;
+  // dynamic segments (uniform bases): states of layer 0 / 1, covered flags; two chunks per
+  // thread in flight per segment (up to 16 K edges per layer and 16 K nodes), the rest after
+  const uint8_t* dp[3] = {E.gst[0], E.gst[1], E.gcov};
+  const int dn[3] = {e0, e1, n};
+  constexpr int DQ = 2;
+  v4u dv[3][DQ];
+  int dlead[3], dch[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    dlead[s] = (int)((uintptr_t)dp[s] & 15);
+    dch[s] = (dlead[s] + dn[s] + 15) >> 4;
+    const uint8_t* a = dp[s] - dlead[s];
+#pragma unroll
+    for (int k = 0; k < DQ; ++k) {
+      const int c = tid + k * NTHREADS;
+      dv[s][k] = ld16_sc1(a, min(c, max(dch[s] - 1, 0)) * 16);  // clamped: branch-free loads
+    }
+  }
+  // static segments by one chunk index: u0, u1, v0, v1 (e_l ints), rp0, rp1 (n + 1 ints)
+  const int* sp[6] = {E.gu[0], E.gu[1], E.gv[0], E.gv[1], E.grp[0], E.grp[1]};
+  const int sn[6] = {e0, e1, e0, e1, n + 1, n + 1};
+  int slead[6], pre[7];
+  pre[0] = 0;
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+    slead[s] = (int)(((uintptr_t)sp[s] & 15) >> 2);  // ints before the segment in its first chunk
+    pre[s + 1] = pre[s] + ((slead[s] + sn[s] + 3) >> 2);
+  }
+  constexpr int SQ = 10;
+  lds_i32* const rp0 = E.rp[0];
+  lds_i32* const rp1 = E.rp[1];
+  for (int b = 0; b < pre[6]; b += SQ * NTHREADS) {
+    v4u w[SQ];
+#pragma unroll
+    for (int k = 0; k < SQ; ++k) {
+      const int q = min(b + k * NTHREADS + tid, pre[6] - 1);
+      const int* a = sp[0] - slead[0];
+      int c = q;
+#pragma unroll
+      for (int s = 1; s < 6; ++s)
+        if (q >= pre[s]) {
+          a = sp[s] - slead[s];
+          c = q - pre[s];
+        }
+      w[k] = *(const v4u*)(a + 4 * c);
+    }
+#pragma unroll
+    for (int k = 0; k < SQ; ++k) {
+      const int q = b + k * NTHREADS + tid;
+      if (q >= pre[6]) break;
+      int s = 0;
+#pragma unroll
+      for (int t = 1; t < 6; ++t) s += q >= pre[t];
+      int c = q, lead = slead[0], cnt = sn[0];
+#pragma unroll
+      for (int t = 1; t < 6; ++t)
+        if (s == t) {
+          c = q - pre[t];
+          lead = slead[t];
+          cnt = sn[t];
+        }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int x = 4 * c + i - lead;
+        if (x < 0 || x >= cnt) continue;
+        const unsigned v = w[k][i];
+        if (s < 2) E.u16[(s ? e0 : 0) + x] = (uint16_t)v;
+        else if (s < 4) E.v16[(s == 3 ? e0 : 0) + x] = (uint16_t)v;
+        else (s == 4 ? rp0 : rp1)[x] = (int)v;
+      }
+    }
+  }
+  lds_u8* const ddst[3] = {E.st, E.st + e0, E.cov8};
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+#pragma unroll
+    for (int k = 0; k < DQ; ++k) {
+      const int c = tid + k * NTHREADS;
+      if (c < dch[s]) stage_bytes(ddst[s], dv[s][k], c, dlead[s], dn[s]);
+    }
+    const uint8_t* a = dp[s] - dlead[s];
+    for (int c = tid + DQ * NTHREADS; c < dch[s]; c += NTHREADS) stage_bytes(ddst[s], ld16_sc1(a, c * 16), c, dlead[s], dn[s]);
+  }
+}
+
 // LDS mode: the whole environment of the last write-back, and its alive-edge list.
 __device__ __forceinline__ void env_stage_lds(const EnvView<false>& E, int n) {
-  env_stage_static(E, n);
-  env_stage_dynamic(E, n);
+  if (E.variant & 0x100) {  // MD_VARIANT bit 8 (diagnostics): the batched two-pass staging
+    env_stage_static(E, n);
+    env_stage_dynamic(E, n);
+  } else {
+    env_stage_wide(E, n);
+  }
   __syncthreads();
   build_alive<false>(E);
 }

@@ -2643,26 +2643,31 @@ __device__ __forceinline__ unsigned q_wait(KParams& p, unsigned tk, int* bc, uns
 // Queue mode, after phase A of graph slot gl in LDS mode: the alive neighbour lists of every
 // tile of the step, both layers, written to the tiles' neighbour-list cache slots in
 // nbc_store's format, so the iteration-1 tiles reload them like iterations 2-3 instead of each
-// building its own (one pass over the live rows' CSR entries on one workgroup instead of one
-// flag round trip, scan and compaction per tile).  The same lists: live rows in ascending id
-// order, 16 per tile, each row's alive CSR entries in CSR order (the reference's in_edges
-// order); a tile whose layer has more than NB_CAP entries gets ok = 0 (the per-row gather).
-// Returns false (the tiles build their lists) when the scratch does not fit.
+// building its own.  The same lists: live rows in ascending id order, 16 per tile, each row's
+// alive CSR entries in CSR order (the reference's in_edges order); a tile whose layer has more
+// than NB_CAP entries gets ok = 0 (the per-row gather).  Each CSR entry comes from the static
+// packed adjacency (adjx: layer-local edge id and neighbour in one word) and is alive when its
+// edge's state in LDS is, so both layers' entries are one round of independent loads (no
+// alive-flag reads: the flags in HBM are the same states' write-back).  Returns false (the tiles
+// build their lists) when the scratch does not fit.
 __device__ __noinline__ bool env_build_lists(KParams&, const GraphInfo gi, int gl) {
   KParams& p = kp();
   float* const lds = lds_base();
   int* ia = (int*)(lds + L_W);
-  const int n = gi.n, et = gi.e[0] + gi.e[1];
+  const int n = gi.n, e0 = gi.e[0], et = gi.e[0] + gi.e[1];
   const EnvLayout Lo = env_layout(n, et);
   const EnvView<false> E = env_view<false>(p, gi, ia);
   const int nl = ((const GraphVar*)(lds + L_GV))->n_live, nt = (nl + TILE - 1) / TILE;
-  if (Lo.total + 3 * nl + 2 * nt + 8 > A_WORDS || p.gtoff[gl] + nt > p.nbc_slots || nl <= 0) return false;
-  // scratch after the environment: node of each live position, per-position prefixes of the
-  // CSR extent and of the alive count (nl + 1 each), per-tile alive totals of both layers
+  // (the per-thread packed counts below need fewer than 2^16 CSR entries per layer)
+  if (Lo.total + 5 * nl + 2 * nt + 8 > A_WORDS || p.gtoff[gl] + nt > p.nbc_slots || nl <= 0 || gi.e[0] >= 32768 ||
+      gi.e[1] >= 32768 || n > 65536)
+    return false;
+  // scratch after the environment: node of each live position, per layer the per-position
+  // prefixes of the CSR extent and of the alive count (nl + 1 each), per-tile alive totals
   int* pn = ia + Lo.total;
-  int* px = pn + nl;
-  int* pd = px + nl + 1;
-  int* tt = pd + nl + 1;
+  int* px[2] = {pn + nl, pn + 2 * nl + 1};
+  int* pd[2] = {pn + 3 * nl + 2, pn + 4 * nl + 3};
+  int* tt = pn + 5 * nl + 4;
   int* tmp = E.tmp;
   int* base_slot = p.nbc + (size_t)p.gtoff[gl] * NBC_INTS;
   {
@@ -2677,116 +2682,138 @@ __device__ __noinline__ bool env_build_lists(KParams&, const GraphInfo gi, int g
       if (uf_load(E.deg0, x) > 0) pn[k++] = x;
   }
   __syncthreads();
-  for (int l = 0; l < 2; ++l) {
-    const lds_i32* rp = E.rp[l];
-    const auto dg = l ? E.deg1 : E.deg0;
-    const int* adj = p.adj[l] + gi.coff[l];
-    const uint8_t* ca = p.calive[l] + gi.coff[l];
-    // prefixes over live positions of the CSR extent and of the alive count
+  // prefixes over live positions of both layers' CSR extents and alive counts (residual degrees)
+  {
     const int chunk = (nl + NTHREADS - 1) / NTHREADS;
     const int i0 = min(nl, (int)threadIdx.x * chunk), i1 = min(nl, i0 + chunk);
-    int se = 0, sd = 0;
+    int sx[2] = {0, 0}, sd[2] = {0, 0};
     for (int i = i0; i < i1; ++i) {
       const int x = pn[i];
-      se += rp[x + 1] - rp[x];
-      sd += uf_load(dg, x);
+      sx[0] += E.rp[0][x + 1] - E.rp[0][x];
+      sx[1] += E.rp[1][x + 1] - E.rp[1][x];
+      sd[0] += uf_load(E.deg0, x);
+      sd[1] += uf_load(E.deg1, x);
     }
-    int te = 0, td = 0;
-    int oe = block_excl_scan(se, tmp, &te);
-    int od = block_excl_scan(sd, tmp, &td);
+    int tx = 0, td = 0;
+    const int ox = block_excl_scan(sx[0] | (sx[1] << 16), tmp, &tx);
+    const int od = block_excl_scan(sd[0] | (sd[1] << 16), tmp, &td);
+    int ax[2] = {ox & 0xffff, ox >> 16}, ad[2] = {od & 0xffff, od >> 16};
     for (int i = i0; i < i1; ++i) {
       const int x = pn[i];
-      px[i] = oe;
-      pd[i] = od;
-      oe += rp[x + 1] - rp[x];
-      od += uf_load(dg, x);
+#pragma unroll
+      for (int l = 0; l < 2; ++l) {
+        px[l][i] = ax[l];
+        pd[l][i] = ad[l];
+        ax[l] += E.rp[l][x + 1] - E.rp[l][x];
+        ad[l] += uf_load(l ? E.deg1 : E.deg0, x);
+      }
     }
     if (threadIdx.x == 0) {
-      px[nl] = te;
-      pd[nl] = td;
+      px[0][nl] = tx & 0xffff;
+      px[1][nl] = tx >> 16;
+      pd[0][nl] = td & 0xffff;
+      pd[1][nl] = td >> 16;
     }
-    __syncthreads();
-    // the CSR entries of the live rows in order, a contiguous run per thread: alive flags,
-    // then each alive entry's place in its tile's list (an entry's index among the layer's
-    // alive entries, minus that of the tile's first row)
-    const int ce = (te + NTHREADS - 1) / NTHREADS;
-    const int e0 = min(te, (int)threadIdx.x * ce), e1 = min(te, e0 + ce);
-    int i = 0;
-    {
-      int lo = 0, hi = nl - 1;  // last position with px[i] <= e0
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (px[mid] <= e0) lo = mid; else hi = mid - 1;
-      }
-      i = lo;
-    }
-    const int ist = i;
-    // flag loads eight at a time (all in flight before the first is used)
-    constexpr int B = 8;
-    int keep = 0;
-    for (int b = e0; b < e1; b += B) {
-      int cp[B], f[B];
-#pragma unroll
-      for (int u = 0; u < B; ++u) {
-        const int e = b + u;
-        cp[u] = -1;
-        if (e < e1) {
-          while (px[i + 1] <= e) ++i;
-          cp[u] = rp[pn[i]] + (e - px[i]);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < B; ++u) f[u] = cp[u] >= 0 ? ldc(ca + cp[u]) : 0;
-#pragma unroll
-      for (int u = 0; u < B; ++u) keep += f[u] != 0;
-    }
-    int tk = 0;
-    int o = block_excl_scan(keep, tmp, &tk);
-    i = ist;
-    for (int b = e0; b < e1; b += B) {
-      int cp[B], ps[B], f[B], nb[B];
-#pragma unroll
-      for (int u = 0; u < B; ++u) {
-        const int e = b + u;
-        cp[u] = -1;
-        ps[u] = 0;
-        if (e < e1) {
-          while (px[i + 1] <= e) ++i;
-          cp[u] = rp[pn[i]] + (e - px[i]);
-          ps[u] = i;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < B; ++u) {
-        f[u] = cp[u] >= 0 ? ldc(ca + cp[u]) : 0;
-        nb[u] = cp[u] >= 0 ? adj[cp[u]] : 0;
-      }
-#pragma unroll
-      for (int u = 0; u < B; ++u) {
-        if (!f[u]) continue;
-        const int j = ps[u] >> 4, w = o - pd[j << 4];
-        if (w < NB_CAP) {
-          uint16_t* ent = (uint16_t*)(base_slot + (size_t)j * NBC_INTS + NBC_HDR + l * NBC_LWORDS);
-          __hip_atomic_store((__attribute__((address_space(1))) uint16_t*)(ent + w), (uint16_t)nb[u],
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        ++o;
-      }
-    }
-    // headers: per row its offset and count in the tile's list, per tile the total
-    for (int q = threadIdx.x; q < nt * TILE; q += NTHREADS) {
-      const int j = q >> 4, r = q & 15, at = (j << 4) + r, end = min(nl, (j + 1) << 4);
-      int* hd = base_slot + (size_t)j * NBC_INTS;
-      const int tot = pd[end] - pd[j << 4];
-      stc(hd + l * 16 + r, at < nl ? pd[at] - pd[j << 4] : tot);
-      stc(hd + 32 + l * 16 + r, at < nl ? pd[at + 1] - pd[at] : 0);
-      if (r == 0) {
-        stc(hd + 64 + l, tot);
-        tt[l * nt + j] = tot;
-      }
-    }
-    __syncthreads();
   }
+  __syncthreads();
+  // each thread: a contiguous run of the live rows' CSR entries per layer; the first R of both
+  // layers loaded in one round (kept for the write pass), longer runs in further rounds
+  constexpr int R = 20;
+  int eb[2], ee[2], ist[2];
+  int xs[2][R];
+  const int* adjx[2] = {p.adjx[0] + gi.coff[0], p.adjx[1] + gi.coff[1]};
+  // the packed word of CSR extent index e (positions from i on), or -1 past the run
+  auto entry_pos = [&](int l, int e, int& i) {
+    while (px[l][i + 1] <= e) ++i;
+    return E.rp[l][pn[i]] + (e - px[l][i]);
+  };
+#pragma unroll
+  for (int l = 0; l < 2; ++l) {
+    const int te = px[l][nl], ce = (te + NTHREADS - 1) / NTHREADS;
+    eb[l] = min(te, (int)threadIdx.x * ce);
+    ee[l] = min(te, eb[l] + ce);
+    int lo = 0, hi = nl - 1;  // last position with px[i] <= eb
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (px[l][mid] <= eb[l]) lo = mid; else hi = mid - 1;
+    }
+    ist[l] = lo;
+  }
+  {
+    int cp[2][R];
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+      int i = ist[l];
+#pragma unroll
+      for (int u = 0; u < R; ++u) cp[l][u] = eb[l] + u < ee[l] ? entry_pos(l, eb[l] + u, i) : -1;
+    }
+#pragma unroll
+    for (int l = 0; l < 2; ++l)
+#pragma unroll
+      for (int u = 0; u < R; ++u) xs[l][u] = cp[l][u] >= 0 ? adjx[l][cp[l][u]] : -1;
+  }
+  auto alive = [&](int l, int x) { return x >= 0 && E.st[(x >> 16) + (l ? e0 : 0)] == E_ALIVE; };
+  int keep[2] = {0, 0};
+#pragma unroll
+  for (int l = 0; l < 2; ++l) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) keep[l] += alive(l, xs[l][u]);
+    int i = ist[l];
+    for (int b = eb[l] + R; b < ee[l]; b += R) {
+      int xr[R];
+#pragma unroll
+      for (int u = 0; u < R; ++u) xr[u] = b + u < ee[l] ? adjx[l][entry_pos(l, b + u, i)] : -1;
+#pragma unroll
+      for (int u = 0; u < R; ++u) keep[l] += alive(l, xr[u]);
+    }
+  }
+  int tk = 0;
+  const int o01 = block_excl_scan(keep[0] | (keep[1] << 16), tmp, &tk);
+#pragma unroll
+  for (int l = 0; l < 2; ++l) {
+    int o = l ? o01 >> 16 : o01 & 0xffff;
+    int i = ist[l];
+    // an alive entry's place in its tile's list: its index among the layer's alive entries,
+    // minus that of the tile's first row
+    auto put = [&](int x, int e) {
+      while (px[l][i + 1] <= e) ++i;
+      if (!alive(l, x)) return;
+      const int j = i >> 4, w = o - pd[l][j << 4];
+      if (w < NB_CAP) {
+        uint16_t* ent = (uint16_t*)(base_slot + (size_t)j * NBC_INTS + NBC_HDR + l * NBC_LWORDS);
+        __hip_atomic_store((__attribute__((address_space(1))) uint16_t*)(ent + w), (uint16_t)(x & 0xffff),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      ++o;
+    };
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+      if (eb[l] + u < ee[l]) put(xs[l][u], eb[l] + u);
+    for (int b = eb[l] + R; b < ee[l]; b += R) {
+      int xr[R];
+      int i2 = i;
+#pragma unroll
+      for (int u = 0; u < R; ++u) xr[u] = b + u < ee[l] ? adjx[l][entry_pos(l, b + u, i2)] : -1;
+#pragma unroll
+      for (int u = 0; u < R; ++u)
+        if (b + u < ee[l]) put(xr[u], b + u);
+    }
+  }
+  // headers: per row its offset and count in the tile's list, per tile the total
+  for (int q = threadIdx.x; q < 2 * nt * TILE; q += NTHREADS) {
+    const int l = q >= nt * TILE, qq = q - l * nt * TILE;
+    const int j = qq >> 4, r = qq & 15, at = (j << 4) + r, end = min(nl, (j + 1) << 4);
+    const int* d = pd[l];
+    int* hd = base_slot + (size_t)j * NBC_INTS;
+    const int tot = d[end] - d[j << 4];
+    stc(hd + l * 16 + r, at < nl ? d[at] - d[j << 4] : tot);
+    stc(hd + 32 + l * 16 + r, at < nl ? d[at + 1] - d[at] : 0);
+    if (r == 0) {
+      stc(hd + 64 + l, tot);
+      tt[l * nt + j] = tot;
+    }
+  }
+  __syncthreads();
   for (int j = threadIdx.x; j < nt; j += NTHREADS)
     stc(base_slot + (size_t)j * NBC_INTS + 66, (tt[j] <= NB_CAP && tt[nt + j] <= NB_CAP) ? 1 : 0);
   __syncthreads();

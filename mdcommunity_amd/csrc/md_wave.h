@@ -93,8 +93,9 @@ __device__ __forceinline__ unsigned long long wq_uni64(unsigned long long x) {
 #endif
 
 // Event log of graph slot 0 (diagnostics, md_profile with MD_VARIANT bit 4): {event, wall clock}
-// pairs after the first 8 profile records -- 0 environment step starts, 1..3 tile stage 1..3
-// complete, 4 virtual-node part 2 done (scripts/wq_timeline.py)
+// pairs after the first 8 profile records -- 6 ENV item taken, 0 environment step starts (group
+// section), 5 its tiles pushed, 1..3 tile stage 1..3 complete, 4 virtual-node part 2 done
+// (scripts/wq_timeline.py)
 __device__ __forceinline__ void wq_event(KParams& p, int gl, int ev) {
   if (p.prof == nullptr || !(p.variant & 4) || gl != 0 || p.prof_cap < 16) return;
   const unsigned long long k = atomicAdd(p.prof + 8 * PROF_SLOTS - 1, 1ull);
@@ -999,6 +1000,7 @@ __device__ void wq_env(KParams& p, float* lds, unsigned item) {
       stc(p.qg + 2 * QG_CAP + gl, built ? 1 : 0);
     }
     q_push(p, nt, [&](int i) { return q_item(QK_TILE, 1, gl, i); }, bc);
+    if (threadIdx.x == 0) wq_event(p, gl, 5);
   } else if (st == ST_WAIT_HOST) {
     q_push(p, 1, [&](int) { return q_item(QK_ENV, 1, gl, 0); }, bc);  // poll again later
   } else {
@@ -1135,6 +1137,7 @@ __device__ __forceinline__ void wq_loop(KParams&, const float* __restrict__ wimg
       continue;
     }
     if (kind == QK_ENV) {
+      if (lane == 0) wq_event(p, q_item_gl(item), 6);
       if (lane == 0) {
         const int s = __hip_atomic_fetch_add((int*)(ctl + WQC_REQ), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         ctl[WQC_ITEMS + s] = (int)item;

@@ -24,27 +24,30 @@ ev = P[8 * 96: 8 * 96 + 2 * n].reshape(-1, 2)
 t0 = ev[0, 1]
 names = {0: "ENV", 1: "st1", 2: "st2", 3: "st3", 4: "VN2"}
 print(f"batch {nb}: kernel {ms:.2f} ms, {launches} launches, {n} events of graph slot 0")
-# per step: ENV start -> st1 -> st2 -> VN2 -> st3 -> next ENV
+# per step: ENV taken (6) -> group start (0) -> tiles pushed (5) -> st1 -> st2 -> VN2 -> st3
 steps, cur = [], {}
 for e, t in ev:
     e = int(e)
-    if e == 0:
+    if e == 6:
         if cur:
             steps.append(cur)
-        cur = {0: t}
+        cur = {6: t}
     else:
-        cur[e] = t
+        cur.setdefault(e, t)
 if cur:
     steps.append(cur)
+order = (6, 0, 5, 1, 2, 4, 3)
+labels = ("rendezvous", "ENV", "->it1 done", "it2", "VN2", "it3", "->next ENV taken")
 d = []
 for i, s in enumerate(steps):
-    if all(k in s for k in (0, 1, 2, 4, 3)) and i + 1 < len(steps):
-        nxt = steps[i + 1][0]
-        d.append((s[1] - s[0], s[2] - s[1], s[4] - s[2], s[3] - s[4], nxt - s[3]))
+    if all(k in s for k in order) and i + 1 < len(steps):
+        ts = [s[k] for k in order] + [steps[i + 1][6]]
+        d.append(np.diff(ts))
 d = np.asarray(d) / 100.0
 if len(d):
-    print("steps with a forward pass: %d; median us: ENV->it1 done %.1f, it2 %.1f, VN2 %.1f, it3 %.1f, ->next ENV start %.1f; total %.1f" % (
-        (len(d),) + tuple(np.median(d, axis=0)) + (np.median(d.sum(axis=1)),)))
+    print("steps with a forward pass: %d; median us: " % len(d) +
+          ", ".join("%s %.1f" % (l, v) for l, v in zip(labels, np.median(d, axis=0))) +
+          "; total %.1f" % np.median(d.sum(axis=1)))
     print("mean us: " + " ".join("%.1f" % x for x in d.mean(axis=0)))
 print("graph slot 0 span %.2f ms over %d steps" % ((ev[-1, 1] - t0) / 1e5, len(steps)))
 eng.close()
