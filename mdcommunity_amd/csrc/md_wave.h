@@ -85,7 +85,21 @@ __device__ __forceinline__ unsigned long long wq_uni64(unsigned long long x) {
 #define WQTA_INIT()                                                                                      \
   unsigned long long* wqd_ = (kp().prof != nullptr && (kp().variant & 8)) ? kp().prof + 88 : nullptr; \
   unsigned long long wqt_ = wall_clock64()
+// the ENV item's pieces in prof[44 + piece] (thread 0 of the group section)
+#define WQTE_INIT()                                                                                      \
+  unsigned long long* wqe_ = (kp().prof != nullptr && (kp().variant & 8)) ? kp().prof + 44 : nullptr; \
+  unsigned long long wqte_ = wall_clock64()
+#define WQTE(k)                                                        \
+  do {                                                                 \
+    if (wqe_ != nullptr && threadIdx.x == 0) {                         \
+      const unsigned long long now_ = wall_clock64();                  \
+      atomicAdd(wqe_ + (k), now_ - wqte_);                             \
+      wqte_ = now_;                                                    \
+    }                                                                  \
+  } while (0)
 #else
+#define WQTE_INIT() do {} while (0)
+#define WQTE(k) do {} while (0)
 #define WQTA_INIT() do {} while (0)
 #define WQTS_INIT(it_) do {} while (0)
 #define WQTS(k) do {} while (0)
@@ -977,7 +991,9 @@ __device__ void wq_env(KParams& p, float* lds, unsigned item) {
   const int it = (int)((item >> 3) & 3u), gl = q_item_gl(item);
   const int g = p.glist[gl];
   if (threadIdx.x == 0) wq_event(p, gl, 0);
+  WQTE_INIT();
   const bool lds_env = phase_a(p, g, it != 0, lds, false);
+  WQTE(0);  // phase A
   const GraphVar& gv = *(const GraphVar*)(lds + L_GV);
   const int st = gv.status, nl = gv.n_live;
   __syncthreads();
@@ -992,15 +1008,18 @@ __device__ void wq_env(KParams& p, float* lds, unsigned item) {
     __syncthreads();
     park = bc[6] != 0;
   }
+  WQTE(1);  // park check
   if (st == ST_RUN && !park) {
     const int nt = (nl + TILE - 1) / TILE;
     const bool built = lds_env && env_build_lists(p, p.ginfo[g], gl);
+    WQTE(2);  // neighbour lists
     if (threadIdx.x == 0) {
       stc(p.qg + 2 * gl + 1, nt | (nt << 16) | (1 << 28));
       stc(p.qg + 2 * QG_CAP + gl, built ? 1 : 0);
     }
     q_push(p, nt, [&](int i) { return q_item(QK_TILE, 1, gl, i); }, bc);
     if (threadIdx.x == 0) wq_event(p, gl, 5);
+    WQTE(3);  // stage word, push
   } else if (st == ST_WAIT_HOST) {
     q_push(p, 1, [&](int) { return q_item(QK_ENV, 1, gl, 0); }, bc);  // poll again later
   } else {
@@ -1037,7 +1056,10 @@ __device__ __noinline__ void wq_group(KParams&, const float* __restrict__ wimg) 
   __syncthreads();
   if (!err) {
     for (int i = 0; i < n && i < WQ_WAVES; ++i) wq_env(p, lds, items[i]);
+    WQTE_INIT();
     load_weights(lds + L_W, wimg);
+    __syncthreads();
+    WQTE(4);  // weight reload
   }
   __syncthreads();
   if (threadIdx.x == 0) {

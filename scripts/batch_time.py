@@ -19,6 +19,10 @@ eng.load_graphs(graphs)
 eng.reset(); out = eng.rollout()
 rem = sum(len(o[0]) for o in out)
 lmax = max(len(o[0]) for o in out)
+if os.environ.get("MD_LENS"):
+    L = np.sort([len(o[0]) for o in out])[::-1]
+    print("rollout lengths, longest first:", " ".join(str(x) for x in L[:24]), "... graphs longer than 40/60/80:",
+          (L > 40).sum(), (L > 60).sum(), (L > 80).sum(), flush=True)
 ts, ws = [], []
 for _ in range(reps):
     t0 = time.perf_counter()

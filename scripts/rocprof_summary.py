@@ -5,7 +5,8 @@
   (the --stats view) from the rocpd SQLite output;
 * PMC passes (pmc_<group>_<workload>/): per-dispatch counter values of the workload's main
   kernel (md_rollout_kernel for the single graph, the degree-cost graph and the N = 18 000
-  testReal-sized cases; md_queue_kernel for the batch and C5, with their tail launches),
+  testReal-sized cases; md_wq_kernel for the batch and C5, with their tail launches:
+  md_queue_kernel for the last MD_WQPARK graphs, md_rollout_kernel for the last MD_QPARK),
   averaged per launch.
 
 Derived per launch (written to traffic.json, which bench.py reads when its `src_hash` equals the
@@ -29,8 +30,9 @@ import sqlite3
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-KERNELS = {"single": "md_rollout_kernel", "batch": "md_queue_kernel", "c5": "md_queue_kernel",
+KERNELS = {"single": "md_rollout_kernel", "batch": "md_wq_kernel", "c5": "md_wq_kernel",
            "degree": "md_rollout_kernel", "real_degree": "md_rollout_kernel", "real_unit": "md_rollout_kernel"}
+TAILS = ("md_queue_kernel", "md_rollout_kernel")  # a batch launch's tail hand-offs, in order
 CUS, SIMDS, XCDS, PEAK_TF = 256, 4, 8, 157.3
 
 
@@ -89,22 +91,29 @@ def workload(d, w, lines):
             for c, v in pmc(path, kernel).items():
                 vals[c] = v
                 lines.append(f"== {w} {c} per {kernel} dispatch (raw): {[round(x, 1) for x in v]}")
-    # (C5 is profiled with --c5-shard-graphs 0, gpu_profile_round.sh: every md_queue_kernel
+    # (C5 is profiled with --c5-shard-graphs 0, gpu_profile_round.sh: every md_wq_kernel
     # dispatch of that run is a 4096-graph launch, so all of them are kept -- no filtering by
     # duration or traffic, which would also drop short relaunches of the same run)
     m = {c: mean(v) for c, v in vals.items()}
     if w in ("batch", "c5"):
-        # the tail launch of each batch rollout (md_rollout_kernel: the last graphs the queue
-        # hands to the lock-step kernel): its traffic per dispatch, so bench.py can report the
-        # traffic of a whole batch step
-        tv = {}
-        for group in ("fetch", "write"):
-            for path in dbs(os.path.join(d, f"pmc_{group}_{w}")):
-                for c, v in pmc(path, "md_rollout_kernel").items():
-                    tv[c] = v
-                    lines.append(f"== {w} {c} per md_rollout_kernel (tail) dispatch (raw): {[round(x, 1) for x in v]}")
-        if tv.get("FETCH_SIZE") and tv.get("WRITE_SIZE"):
-            out["tail_hbm_bytes_per_launch"] = 2.0 * 1024.0 * mean(tv["FETCH_SIZE"]) + 1024.0 * mean(tv["WRITE_SIZE"])
+        # the tail launches of each batch rollout (md_queue_kernel: the graphs the wave-item
+        # kernel parks; md_rollout_kernel: the last ones the queue hands to the lock-step
+        # kernel): their traffic per dispatch, averaged over both, so bench.py can report the
+        # traffic of a whole batch step (main + tails)
+        tb, nd = 0.0, 0
+        for tk in TAILS:
+            tv = {}
+            for group in ("fetch", "write"):
+                for path in dbs(os.path.join(d, f"pmc_{group}_{w}")):
+                    for c, v in pmc(path, tk).items():
+                        tv[c] = v
+                        lines.append(f"== {w} {c} per {tk} (tail) dispatch (raw): {[round(x, 1) for x in v]}")
+            if tv.get("FETCH_SIZE") and tv.get("WRITE_SIZE") and len(tv["FETCH_SIZE"]) == len(tv["WRITE_SIZE"]):
+                tb += sum(2.0 * 1024.0 * f + 1024.0 * x for f, x in zip(tv["FETCH_SIZE"], tv["WRITE_SIZE"]))
+                nd += len(tv["FETCH_SIZE"])
+        if nd:
+            out["tail_hbm_bytes_per_launch"] = tb / nd
+            out["tail_dispatches"] = nd
     if m.get("FETCH_SIZE") is not None and m.get("WRITE_SIZE") is not None:
         out["fetch_bytes_per_launch"] = 2.0 * 1024.0 * m["FETCH_SIZE"]
         out["write_bytes_per_launch"] = 1024.0 * m["WRITE_SIZE"]

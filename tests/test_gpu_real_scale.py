@@ -207,3 +207,39 @@ def test_real_scale_certified_whole_sequence(real, certs, name):
         assert dq_o < Q_TOL and dq_r < Q_TOL, (dq_o, dq_r)
     finally:
         eng.close()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", ["deg_step1", "unit_step1"])
+def test_real_scale_deep_predictions_match_reference(real, certs, name):
+    """Deep predictions at real size (U/MultiDismantler_torch.py:711-736,759-784; D/...:683-706):
+    the device's Q rows at predictions 40, 80, 120, 158 (unit cost also 177, its last) of the
+    certified sequence, teacher-forced, are within Q_TOL of the REFERENCE's own rows
+    (tests/golden/real_scale_deep.npz, tests/golden/make_real_scale_deep.py), with the same mask."""
+    e0, e1, g = real
+    cost, ckpt, step = CERT_CASES[name]
+    with np.load(os.path.join(GOLDEN, "real_scale_deep.npz")) as z:
+        idx, ref = z[f"{name}_idx"], z[f"{name}_ref"]
+    seq = certs[f"{name}_seq"]
+    eng = _lib.Engine(engine.load_weights(ckpt), cost_mode=cost)
+    try:
+        nw = None
+        if cost == _lib.MD_COST_DEGREE:
+            gg = mgraph.Graph_test.from_edges(N, e0, e1)
+            mgraph.ensure_degree_weights(gg)
+            nw = mgraph.node_weight_array([gg])
+        eng.load_graphs([(N, e0, e1)], node_w=nw)
+        eng.reset()
+        want = {int(t): k for k, t in enumerate(idx.tolist())}
+        dq = 0.0
+        for t in range(int(idx.max()) + 1):
+            if t in want:
+                q, _, _, _ = eng.predict()
+                r = ref[want[t]].astype(np.float64)
+                live = np.isfinite(q)
+                assert np.array_equal(live, r != np.float32(refenv.MASK)), t
+                dq = max(dq, float(np.max(np.abs(q[live].astype(np.float64) - r[live]))))
+            eng.step(np.asarray([seq[t]], np.int32))
+        assert dq < Q_TOL, dq
+    finally:
+        eng.close()
