@@ -556,6 +556,9 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
       bytes[3] = sizeof(unsigned long long) * 2048 * std::min(XB_SLOTS, grid / 2 + 1);
     }
     if (qmode) {
+      // (wave items: the head granules carry the forward pass's prediction count as their tag)
+      ptr[2] = c->hbuf.p;
+      bytes[2] = sizeof(float) * c->hbuf.n;
       ptr[4] = c->qslot.p;
       bytes[4] = sizeof(unsigned long long) * c->qslot.n;
       ptr[5] = c->qg.p;

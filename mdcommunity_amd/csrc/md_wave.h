@@ -498,9 +498,11 @@ __device__ __forceinline__ void wq_layer_back(KParams& p, const GraphInfo& gi, i
 // Iteration 3 of one tile on one wave after both layers: attention_q_tile's pieces --
 // F_l = tanh(E_l.T + b), the gate dot products, E'_l = F_l + g_l F_other normalised, the
 // outer-product chain e = sum_b (h y_b) cp_b, relu(e.H1), the Q head, q = w0 Q0 + w1 Q1 and the
-// tile's arg-max partial.  y and the graph scalars come from the head granules (tag 1).
+// tile's arg-max partial.  y and the graph scalars come from the head granules of this forward
+// pass (tag htag = the graph's predictions so far + 1; the granules are cleared per launch): the
+// iteration-3 tiles are queued beside virtual-node part 2 and wait here for its hand-off.
 __device__ __forceinline__ void wq_attention(KParams& p, const GraphInfo& gi, int g, int j, int vrow,
-                                             f4 (&e0)[4], f4 (&e1)[4], float* wa) {
+                                             f4 (&e0)[4], f4 (&e1)[4], float* wa, unsigned htag) {
   const int lane = wq_lane(), ar = lane & 15, ak = lane >> 4;
   const float* wi = lds_base() + L_W;
   WQTA_INIT();
@@ -513,11 +515,12 @@ __device__ __forceinline__ void wq_attention(KParams& p, const GraphInfo& gi, in
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const int idx = lane + 64 * k;
-      gr[k] = 1ull << 32;
+      gr[k] = (unsigned long long)htag << 32;
       if (idx < HB_FLOATS) {
-        while (((gr[k] = __hip_atomic_load(hb + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != 1ull) {
+        while (((gr[k] = __hip_atomic_load(hb + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != htag) {
           __builtin_amdgcn_s_sleep(1);
-          if (wall_clock64() - t0 > BARRIER_TIMEOUT_TICKS) {
+          if (wall_clock64() - t0 > BARRIER_TIMEOUT_TICKS ||
+              (__hip_atomic_load((g_u32*)p.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & BAR_ERR)) {
             raise_err(p, ERR_TIMEOUT);
             gr[k] = 0ull;
             break;
@@ -614,18 +617,33 @@ __device__ __forceinline__ void wq_attention(KParams& p, const GraphInfo& gi, in
       acc[s >> 1][s & 1] = 0.f;
     }
     wave_lds_sync();
-    // {y_b, cp_b} pairs in WA, read by every lane at one address (an LDS broadcast)
+    // {y_b, cp_b} pairs in WA, read by every lane at one address (an LDS broadcast), four b per
+    // 2 x 16-byte read issued one block ahead; per b the eight products first (independent),
+    // then the eight FMAs
     wa[2 * lane] = yv[l];
     wa[2 * lane + 1] = cpl;
     wave_lds_sync();
-    const float2* yc = (const float2*)wa;
-#pragma unroll 8
-    for (int b = 0; b < 64; ++b) {
-      const float2 v = yc[b];
-      const f2v yy = {v.x, v.x};
-      const f2v cc = {v.y, v.y};
+    const float4* yc = (const float4*)wa;
+    auto term = [&](float y, float c) {
+      const f2v yy = {y, y}, cc = {c, c};
+      f2v t[8];
 #pragma unroll
-      for (int k2 = 0; k2 < 8; ++k2) acc[k2] = __builtin_elementwise_fma(h[k2] * yy, cc, acc[k2]);
+      for (int k2 = 0; k2 < 8; ++k2) t[k2] = h[k2] * yy;
+#pragma unroll
+      for (int k2 = 0; k2 < 8; ++k2) acc[k2] = __builtin_elementwise_fma(t[k2], cc, acc[k2]);
+    };
+    float4 n0 = yc[0], n1 = yc[1];
+#pragma unroll 2
+    for (int bb = 0; bb < 64; bb += 4) {
+      const float4 c0 = n0, c1 = n1;
+      if (bb + 4 < 64) {
+        n0 = yc[(bb + 4) / 2];
+        n1 = yc[(bb + 4) / 2 + 1];
+      }
+      term(c0.x, c0.y);
+      term(c0.z, c0.w);
+      term(c1.x, c1.y);
+      term(c1.z, c1.w);
     }
     wave_lds_sync();
 #pragma unroll
@@ -688,6 +706,7 @@ __device__ __forceinline__ void wq_tile(KParams&, int g, int gl, int it, int j) 
   const GraphInfo gi = p.ginfo[g];
   // rows (live list), the cached alive-neighbour lists' header and flag, one round trip
   const int nl = wq_uni(ldc(&p.gvar[g].n_live));
+  const int npred = it == 3 ? wq_uni(ldc(&p.gvar[g].npred)) : 0;  // the head granules' tag - 1
   int vrow = -1;
   if (lane < TILE) {
     const int r = j * TILE + lane;
@@ -779,7 +798,7 @@ __device__ __forceinline__ void wq_tile(KParams&, int g, int gl, int it, int j) 
   wq_layer_back(p, gi, it, j, 1, vrow, nv, wa, xa1, e1);
   if (it == 3) {
     WQTS_RESET();
-    wq_attention(p, gi, g, j, vrow, e0, e1, wa);
+    wq_attention(p, gi, g, j, vrow, e0, e1, wa, (unsigned)npred + 1u);
     WQTS(6);  // attention + Q head
   }
 }
@@ -864,7 +883,7 @@ __device__ __forceinline__ void wq_vrow(float s0, float s1, float& y0, float& y1
 
 // Virtual-node item of graph g on one wave: part 1 Y1, Y2 from S0, S1 (stored to ybuf); part 2
 // Y3 from S2, then graph_head (y, layer-mix weights, aux features) published as the head
-// granules (tag 1) for the iteration-3 tiles.
+// granules (tag: the graph's predictions so far + 1) for the iteration-3 tiles.
 __device__ __forceinline__ void wq_vn(KParams&, int g, int part) {
   KParams& p = kp();
   const int lane = wq_lane();
@@ -872,6 +891,7 @@ __device__ __forceinline__ void wq_vn(KParams&, int g, int part) {
   const float* wi = lds_base() + L_W;
   const GraphInfo gi = p.ginfo[g];
   const int nl = wq_uni(ldc(&p.gvar[g].n_live));
+  const int npred = part == 2 ? wq_uni(ldc(&p.gvar[g].npred)) : 0;
   const int nt = (nl + TILE - 1) / TILE;
   float y0, y1;
   if (part == 1) {
@@ -973,12 +993,11 @@ __device__ __forceinline__ void wq_vn(KParams&, int g, int part) {
   }
   wave_lds_sync();
   g_u64* hb = (g_u64*)(p.hbuf + 2 * ((size_t)g * HB_FLOATS));
-  __hip_atomic_store(hb + lane, (1ull << 32) | (unsigned)__float_as_uint(ys[0]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(hb + 64 + lane, (1ull << 32) | (unsigned)__float_as_uint(ys[1]), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long tag = (unsigned long long)((unsigned)npred + 1u) << 32;
+  __hip_atomic_store(hb + lane, tag | (unsigned)__float_as_uint(ys[0]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(hb + 64 + lane, tag | (unsigned)__float_as_uint(ys[1]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (lane < 16)
-    __hip_atomic_store(hb + 128 + lane, (1ull << 32) | (unsigned)__float_as_uint(gsv), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(hb + 128 + lane, tag | (unsigned)__float_as_uint(gsv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------ group section (ENV items)
@@ -992,6 +1011,14 @@ __device__ void wq_env(KParams& p, float* lds, unsigned item) {
   const int g = p.glist[gl];
   if (threadIdx.x == 0) wq_event(p, gl, 0);
   WQTE_INIT();
+  // the tail-park test's words, read before phase A instead of after it (both only move toward
+  // parking -- QC_REM down, QC_ADMIT up -- so an early read parks no graph too soon)
+  int padm = 0, prem = 0x7fffffff;
+  const bool ptest = p.qpark > 0 && ng > p.qpark;
+  if (ptest && threadIdx.x == 0) {
+    padm = ldc((const int*)(p.qctl + QC_ADMIT));
+    prem = ldc((const int*)(p.qctl + QC_REM));
+  }
   const bool lds_env = phase_a(p, g, it != 0, lds, false);
   WQTE(0);  // phase A
   const GraphVar& gv = *(const GraphVar*)(lds + L_GV);
@@ -1002,9 +1029,8 @@ __device__ void wq_env(KParams& p, float* lds, unsigned item) {
     return;
   }
   bool park = false;
-  if (st == ST_RUN && p.qpark > 0 && ng > p.qpark) {
-    if (threadIdx.x == 0)
-      bc[6] = ldc((const int*)(p.qctl + QC_ADMIT)) >= ng && ldc((const int*)(p.qctl + QC_REM)) <= p.qpark;
+  if (st == ST_RUN && ptest) {
+    if (threadIdx.x == 0) bc[6] = padm >= ng && prem <= p.qpark;
     __syncthreads();
     park = bc[6] != 0;
   }
@@ -1125,7 +1151,10 @@ __device__ __forceinline__ void wq_loop(KParams&, const float* __restrict__ wimg
   unsigned long long tq = wall_clock64();
   const unsigned long long tq0 = tq;
   while (true) {
-    if (ctl[WQC_REQ] != 0) {
+    // (a held continuation runs first: the iteration-3 tiles of its graph, maybe a wave of this
+    // workgroup among them, wait for part 2's head granules and would never reach the group's
+    // barrier)
+    if (ctl[WQC_REQ] != 0 && cont == 0u) {
       wq_group(p, wimg);
       continue;
     }
@@ -1190,7 +1219,9 @@ __device__ __forceinline__ void wq_loop(KParams&, const float* __restrict__ wimg
     } else {  // QK_VN part 2
       wq_vn(p, g, 2);
       pre = wq_peek(p, tk);
-      next = 4;
+      // (the iteration-3 tiles went out with this item; MD_VARIANT bit 9: after it)
+      next = (p.variant & 512) ? 4 : 0;
+      if (!(p.variant & 512) && lane == 0) wq_event(p, gl, 4);
     }
     if (next != 0) {
       if (lane == 0) wq_event(p, gl, next);
@@ -1198,6 +1229,9 @@ __device__ __forceinline__ void wq_loop(KParams&, const float* __restrict__ wimg
       if (next == 1) {
         wq_push(p, nt + 1, [&](int i) { return i < nt ? q_item(QK_TILE, 2, gl, i) : q_item(QK_VN, 1, gl, 0); });
       } else if (next == 2) {
+        // the iteration-3 tiles now: their layer pieces need only the iteration-2 rows, and
+        // their attention waits for this step's head granules, which part 2 publishes
+        if (!(p.variant & 512)) wq_push(p, nt, [&](int i) { return q_item(QK_TILE, 3, gl, i); });
         cont = q_item(QK_VN, 2, gl, 0);
       } else if (next == 3) {
         cont = q_item(QK_ENV, 1, gl, 0);
