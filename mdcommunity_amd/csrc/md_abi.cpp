@@ -105,7 +105,7 @@ struct md_ctx {
   int variant = 0;   // diagnostics knob (MD_VARIANT)
   int pair_on = 1;   // queue mode: paired tiles (MD_PAIR=0: one tile at a time)
   int wq_on = 1;     // queue mode: one work item per wave (md_wq_kernel; MD_WQ=0: per workgroup, md_queue_kernel)
-  int wqpark = 96;   // wave-item launches of more than this many graphs; at most this many still running ->
+  int wqpark = 128;  // wave-item launches of more than this many graphs; at most this many still running ->
                      // they continue in md_queue_kernel (whose per-step latency is lower; MD_WQPARK)
   int qpark = 8;     // queue mode: at most this many graphs left -> the lock-step kernel (MD_QPARK, 0 = off)
   double last_ms = 0.0;

@@ -2650,7 +2650,7 @@ __device__ __forceinline__ unsigned q_wait(KParams& p, unsigned tk, int* bc, uns
 // edge's state in LDS is, so both layers' entries are one round of independent loads (no
 // alive-flag reads: the flags in HBM are the same states' write-back).  Returns false (the tiles
 // build their lists) when the scratch does not fit.
-__device__ __noinline__ bool env_build_lists(KParams&, const GraphInfo gi, int gl) {
+__device__ __forceinline__ bool env_build_lists(KParams&, const GraphInfo gi, int gl) {
   KParams& p = kp();
   float* const lds = lds_base();
   int* ia = (int*)(lds + L_W);
@@ -2670,6 +2670,21 @@ __device__ __noinline__ bool env_build_lists(KParams&, const GraphInfo gi, int g
   int* tt = pn + 5 * nl + 4;
   int* tmp = E.tmp;
   int* base_slot = p.nbc + (size_t)p.gtoff[gl] * NBC_INTS;
+#ifdef MD_QPROF
+  // diagnostics (qprof build, MD_VARIANT bit 8): the builder's pieces in prof[50 + k]
+  unsigned long long* lqd = p.prof != nullptr && (p.variant & 8) ? p.prof + 50 : nullptr;
+  unsigned long long lqt = wall_clock64();
+#define LQTS(k)                                                                        \
+  do {                                                                                 \
+    if (lqd != nullptr && threadIdx.x == 0) {                                          \
+      const unsigned long long now_ = wall_clock64();                                  \
+      atomicAdd(lqd + (k), now_ - lqt);                                                \
+      lqt = now_;                                                                      \
+    }                                                                                  \
+  } while (0)
+#else
+#define LQTS(k) do {} while (0)
+#endif
   {
     // live positions (ascending ids, as the live list)
     const int chunk = (n + NTHREADS - 1) / NTHREADS;
@@ -2682,6 +2697,7 @@ __device__ __noinline__ bool env_build_lists(KParams&, const GraphInfo gi, int g
       if (uf_load(E.deg0, x) > 0) pn[k++] = x;
   }
   __syncthreads();
+  LQTS(0);
   // prefixes over live positions of both layers' CSR extents and alive counts (residual degrees)
   {
     const int chunk = (nl + NTHREADS - 1) / NTHREADS;
@@ -2716,17 +2732,19 @@ __device__ __noinline__ bool env_build_lists(KParams&, const GraphInfo gi, int g
     }
   }
   __syncthreads();
+  LQTS(1);
   // each thread: a contiguous run of the live rows' CSR entries per layer; the first R of both
-  // layers loaded in one round (kept for the write pass), longer runs in further rounds
+  // layers loaded in one round (kept for the write pass), longer runs in further rounds.  A run
+  // is walked row by row with the row's boundary and CSR base in registers (LDS reads only where
+  // the run crosses into the next live row).
   constexpr int R = 20;
-  int eb[2], ee[2], ist[2];
+  struct Walk {
+    int i, nxt, base;  // live position, its CSR-extent end, CSR position - extent index
+  };
+  int eb[2], ee[2];
+  Walk w0[2];
   int xs[2][R];
   const int* adjx[2] = {p.adjx[0] + gi.coff[0], p.adjx[1] + gi.coff[1]};
-  // the packed word of CSR extent index e (positions from i on), or -1 past the run
-  auto entry_pos = [&](int l, int e, int& i) {
-    while (px[l][i + 1] <= e) ++i;
-    return E.rp[l][pn[i]] + (e - px[l][i]);
-  };
 #pragma unroll
   for (int l = 0; l < 2; ++l) {
     const int te = px[l][nl], ce = (te + NTHREADS - 1) / NTHREADS;
@@ -2737,15 +2755,31 @@ __device__ __noinline__ bool env_build_lists(KParams&, const GraphInfo gi, int g
       const int mid = (lo + hi + 1) >> 1;
       if (px[l][mid] <= eb[l]) lo = mid; else hi = mid - 1;
     }
-    ist[l] = lo;
+    w0[l].i = lo;
+    w0[l].nxt = px[l][lo + 1];
+    w0[l].base = E.rp[l][pn[lo]] - px[l][lo];
   }
+  auto advance = [&](int l, Walk& w, int e) {
+    while (e >= w.nxt) {
+      ++w.i;
+      w.nxt = px[l][w.i + 1];
+      w.base = E.rp[l][pn[w.i]] - px[l][w.i];
+    }
+  };
   {
     int cp[2][R];
 #pragma unroll
     for (int l = 0; l < 2; ++l) {
-      int i = ist[l];
+      Walk w = w0[l];
 #pragma unroll
-      for (int u = 0; u < R; ++u) cp[l][u] = eb[l] + u < ee[l] ? entry_pos(l, eb[l] + u, i) : -1;
+      for (int u = 0; u < R; ++u) {
+        const int e = eb[l] + u;
+        cp[l][u] = -1;
+        if (e < ee[l]) {
+          advance(l, w, e);
+          cp[l][u] = w.base + e;
+        }
+      }
     }
 #pragma unroll
     for (int l = 0; l < 2; ++l)
@@ -2758,30 +2792,40 @@ __device__ __noinline__ bool env_build_lists(KParams&, const GraphInfo gi, int g
   for (int l = 0; l < 2; ++l) {
 #pragma unroll
     for (int u = 0; u < R; ++u) keep[l] += alive(l, xs[l][u]);
-    int i = ist[l];
-    for (int b = eb[l] + R; b < ee[l]; b += R) {
-      int xr[R];
+    if (eb[l] + R < ee[l]) {
+      Walk w = w0[l];
+      advance(l, w, eb[l] + R);
+      for (int b = eb[l] + R; b < ee[l]; b += R) {
+        int xr[R];
 #pragma unroll
-      for (int u = 0; u < R; ++u) xr[u] = b + u < ee[l] ? adjx[l][entry_pos(l, b + u, i)] : -1;
+        for (int u = 0; u < R; ++u) {
+          xr[u] = -1;
+          if (b + u < ee[l]) {
+            advance(l, w, b + u);
+            xr[u] = adjx[l][w.base + b + u];
+          }
+        }
 #pragma unroll
-      for (int u = 0; u < R; ++u) keep[l] += alive(l, xr[u]);
+        for (int u = 0; u < R; ++u) keep[l] += alive(l, xr[u]);
+      }
     }
   }
+  LQTS(2);
   int tk = 0;
   const int o01 = block_excl_scan(keep[0] | (keep[1] << 16), tmp, &tk);
 #pragma unroll
   for (int l = 0; l < 2; ++l) {
     int o = l ? o01 >> 16 : o01 & 0xffff;
-    int i = ist[l];
+    Walk w = w0[l];
     // an alive entry's place in its tile's list: its index among the layer's alive entries,
     // minus that of the tile's first row
     auto put = [&](int x, int e) {
-      while (px[l][i + 1] <= e) ++i;
+      advance(l, w, e);
       if (!alive(l, x)) return;
-      const int j = i >> 4, w = o - pd[l][j << 4];
-      if (w < NB_CAP) {
+      const int j = w.i >> 4, wo = o - pd[l][j << 4];
+      if (wo < NB_CAP) {
         uint16_t* ent = (uint16_t*)(base_slot + (size_t)j * NBC_INTS + NBC_HDR + l * NBC_LWORDS);
-        __hip_atomic_store((__attribute__((address_space(1))) uint16_t*)(ent + w), (uint16_t)(x & 0xffff),
+        __hip_atomic_store((__attribute__((address_space(1))) uint16_t*)(ent + wo), (uint16_t)(x & 0xffff),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       ++o;
@@ -2791,14 +2835,21 @@ __device__ __noinline__ bool env_build_lists(KParams&, const GraphInfo gi, int g
       if (eb[l] + u < ee[l]) put(xs[l][u], eb[l] + u);
     for (int b = eb[l] + R; b < ee[l]; b += R) {
       int xr[R];
-      int i2 = i;
+      Walk w2 = w;
 #pragma unroll
-      for (int u = 0; u < R; ++u) xr[u] = b + u < ee[l] ? adjx[l][entry_pos(l, b + u, i2)] : -1;
+      for (int u = 0; u < R; ++u) {
+        xr[u] = -1;
+        if (b + u < ee[l]) {
+          advance(l, w2, b + u);
+          xr[u] = adjx[l][w2.base + b + u];
+        }
+      }
 #pragma unroll
       for (int u = 0; u < R; ++u)
         if (b + u < ee[l]) put(xr[u], b + u);
     }
   }
+  LQTS(3);
   // headers: per row its offset and count in the tile's list, per tile the total
   for (int q = threadIdx.x; q < 2 * nt * TILE; q += NTHREADS) {
     const int l = q >= nt * TILE, qq = q - l * nt * TILE;
@@ -2817,6 +2868,8 @@ __device__ __noinline__ bool env_build_lists(KParams&, const GraphInfo gi, int g
   for (int j = threadIdx.x; j < nt; j += NTHREADS)
     stc(base_slot + (size_t)j * NBC_INTS + 66, (tt[j] <= NB_CAP && tt[nt + j] <= NB_CAP) ? 1 : 0);
   __syncthreads();
+  LQTS(4);
+#undef LQTS
   return true;
 }
 

@@ -62,6 +62,9 @@ if len(P) and P[0, 0] == 1 and P[0, 9] > 0:
         if P[0, 44] > 0:
             wn = ["phase A", "park check", "lists", "push", "weight reload"]
             print("  wave ENV pieces (WG-ms): " + "  ".join("%s %.1f" % (nm, v) for nm, v in zip(wn, P[0, 44:49] / 1e5)))
+        if P[0, 50] > 0:
+            ln = ["live positions", "prefixes", "entries + alive counts", "scan + list stores", "headers"]
+            print("  ENV list builder pieces (WG-ms): " + "  ".join("%s %.1f" % (nm, v) for nm, v in zip(ln, P[0, 50:55] / 1e5)))
         att_n = ["tanh GEMM", "dots+gates", "mix+norm", "head", "e-chain", "hidden+Q", "arg-max+stores"]
         print("  attention pieces (WG-ms): " + "  ".join("%s %.1f" % (nm, v) for nm, v in zip(att_n, P[0, 88:95] / 1e5)))
         sys.exit(0)
