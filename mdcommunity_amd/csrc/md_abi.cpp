@@ -104,10 +104,13 @@ struct md_ctx {
   int env_mode = 1;  // 1: dedicated environment workgroups for small batches
   int variant = 0;   // diagnostics knob (MD_VARIANT)
   int pair_on = 1;   // queue mode: paired tiles (MD_PAIR=0: one tile at a time)
+  int bspec_on = 0;  // queue launches: speculative environment steps of the likely next pick (MD_BSPEC=1: on)
+  DevBuf<int> bspec;
+  long long bspec_half = 0;
   int wq_on = 1;     // queue mode: one work item per wave (md_wq_kernel; MD_WQ=0: per workgroup, md_queue_kernel)
   int wqpark = 128;  // wave-item launches of more than this many graphs; at most this many still running ->
                      // they continue in md_queue_kernel (whose per-step latency is lower; MD_WQPARK)
-  int qpark = 8;     // queue mode: at most this many graphs left -> the lock-step kernel (MD_QPARK, 0 = off)
+  int qpark = 4;     // queue mode: at most this many graphs left -> the lock-step kernel (MD_QPARK, 0 = off)
   double last_ms = 0.0;
   int last_launches = 0;
 
@@ -203,7 +206,7 @@ struct md_ctx {
       H[l][0].release(); H[l][1].release();
     }
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
-    tr_stat.release(); glist.release(); gtoff.release(); ctl.release(); tpart.release(); lab_ok.release(); gscr_team.release(); prank.release(); q.release(); spart.release();
+    tr_stat.release(); glist.release(); gtoff.release(); ctl.release(); tpart.release(); lab_ok.release(); gscr_team.release(); bspec.release(); prank.release(); q.release(); spart.release();
     apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); nbc.release(); qslot.release(); qg.release(); tr_q.release(); node_w.release();
     sres.release(); qspec.release(); bars.release(); dfbuf.release();
     df_graph.clear();
@@ -268,6 +271,8 @@ Params make_params(md_ctx* c) {
   p.tctl = c->ctl.p + CTL_TEAM;
   p.lab_ok = c->lab_ok.p;
   p.gscr_team = c->gscr_team.p;
+  p.bspec = c->bspec.p;
+  p.bspec_half = c->bspec_half;
   p.prank = c->prank.p;
   p.spart = c->spart.p;
   p.apart = c->apart.p;
@@ -600,6 +605,7 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
   p.qmode = qmode ? (wq ? 2 : 1) : 0;
   p.qpair = c->pair_on ? 1 : 0;
   p.qpark = p.qmode == 2 ? c->wqpark : c->qpark;
+  if (!qmode) p.bspec = nullptr;  // (speculative environment items run in the queue kernels only)
   p.nglist = ngl;
   p.n_env = n_env;
   p.variant = c->variant;
@@ -794,6 +800,7 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_ENV_MODE")) c->env_mode = std::atoi(v);
   if (const char* v = std::getenv("MD_PAIR")) c->pair_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_WQ")) c->wq_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MD_BSPEC")) c->bspec_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_WQPARK")) c->wqpark = std::max(0, std::min(4096, std::atoi(v)));
   if (const char* v = std::getenv("MD_QPARK")) c->qpark = std::max(0, std::min(16, std::atoi(v)));
   if (const char* v = std::getenv("MD_HOST_HANDSHAKE")) c->host_mode = std::atoi(v);
@@ -1065,6 +1072,15 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
     for (int g = 0; g < n_graphs; ++g) max_n = std::max(max_n, (int)n_nodes[g]);
     HIPCHK(c, c->gscr_team.alloc((size_t)GSCR_TEAM_WORDS * max_n));
     c->team_owner = -1;
+  }
+  // speculative environment-step slots of queue launches (bspec_slot): per graph and removal-count
+  // parity 4 (9 + e + 2 n) ints >= the SRES layout's 35 + 3 e + 6 n; zeroed (every slot free)
+  c->bspec_half = 0;
+  c->bspec.release();
+  if (c->bspec_on && n_graphs > DEDICATED_MAX_GRAPHS) {
+    c->bspec_half = 4 * (9 * (long long)n_graphs + (long long)te[0] + (long long)te[1] + 2 * (long long)tn);
+    HIPCHK(c, c->bspec.alloc((size_t)(2 * c->bspec_half)));
+    HIPCHK(c, hipMemsetAsync(c->bspec.p, 0, sizeof(int) * (size_t)(2 * c->bspec_half), c->stream));
   }
   HIPCHK(c, c->prank.alloc(ranks.size()));
   HIPCHK(c, hipMemcpyAsync(c->prank.p, ranks.data(), sizeof(uint16_t) * ranks.size(), hipMemcpyHostToDevice, c->stream));

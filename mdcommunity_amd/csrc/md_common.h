@@ -105,6 +105,9 @@ struct Params {
   float* h0tab[2];                 // [layer] first-layer embedding: by degree (unit) / by node (degree cost)
   float* q;                        // per node (-inf = masked)
   int* gscr;                       // phase-A scratch in global memory for graphs too big for LDS: GSCR_WORDS per node
+  int* bspec;                      // queue launches: speculative environment-step results, two per graph
+                                   // (removal-count parity), SRES layout (md_kernels.hip bspec_slot); nullptr = off
+  long long bspec_half;            // ints per parity half
   int* gscr_team;                  // the grid-wide step's graph-local scratch (GSCR_TEAM_WORDS x the largest n):
                                    //   LMCC counts, second parent buffers, feature degrees, class labels
   long long* tpart;                // grid-wide environment step: per-workgroup partials [2][TEAM_MAX_WG][16]

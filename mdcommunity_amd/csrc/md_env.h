@@ -767,14 +767,50 @@ __device__ __forceinline__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, 
 struct EnvAgg {
   int nlive, dm0, dm1, sd0, sd1, bad;
   long long th0, th1;
+  int cand;  // (qs given) the live node of largest previous Q, least id first; -1 none
 };
+
+// Block arg-max of (v, i) pairs: the largest v, the least i among equal v; -1 when no thread
+// has a finite v.  All threads get the result.
+__device__ __forceinline__ int block_argmax_f(float v, int i, int* tmp) {
+  const int lane = lane_id(), w = wave_id();
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v2 = __shfl_xor(v, o, 64);
+    const int i2 = __shfl_xor(i, o, 64);
+    if (v2 > v || (v2 == v && i2 < i)) {
+      v = v2;
+      i = i2;
+    }
+  }
+  __syncthreads();
+  if (lane == 0) {
+    tmp[2 * w] = __float_as_int(v);
+    tmp[2 * w + 1] = i;
+  }
+  __syncthreads();
+  float bv = NEG_INF;
+  int bi = -1;
+#pragma unroll
+  for (int k = 0; k < NTHREADS / 64; ++k) {
+    const float v2 = __int_as_float(tmp[2 * k]);
+    const int i2 = tmp[2 * k + 1];
+    if (v2 > bv || (v2 == bv && i2 < bi && i2 >= 0)) {
+      bv = v2;
+      bi = i2;
+    }
+  }
+  __syncthreads();
+  return bv > NEG_INF ? bi : -1;
+}
 
 // Residual degrees (edge-parallel atomics over the alive edges), then the ascending live list,
 // the degrees and the per-layer aggregates of the current state, stored to (gdeg0, gdeg1, lv)
 // -- the graph's HBM arrays (phase A) or a speculative result slot -- and q = -inf for every
 // node when q is given.  One fused block exchange for the scan and all reductions.
 template <bool GL>
-__device__ __forceinline__ EnvAgg env_features(const EnvView<GL>& E, int n, int* gdeg0, int* gdeg1, float* lv, float* q) {
+__device__ __forceinline__ EnvAgg env_features(const EnvView<GL>& E, int n, int* gdeg0, int* gdeg1, float* lv, float* q,
+                                               const float* qs = nullptr) {
   const int e0 = E.e0;
   // residual degrees by edge-parallel atomics
   for (int x = threadIdx.x; x < n; x += NTHREADS) {
@@ -794,11 +830,17 @@ __device__ __forceinline__ EnvAgg env_features(const EnvView<GL>& E, int n, int*
   const int x0 = min(n, (int)threadIdx.x * chunk), x1 = min(n, x0 + chunk);
   int nlive = 0, dm0 = 0, dm1 = 0, sd0 = 0, sd1 = 0, bad = 0;
   long long th0 = 0, th1 = 0;
+  float cq = NEG_INF;
+  int ci = -1;
   for (int x = x0; x < x1; ++x) {
     const int d0 = uf_load(E.deg0, x), d1 = uf_load(E.deg1, x);
     stc(gdeg0 + x, d0);
     stc(gdeg1 + x, d1);
     if (q != nullptr) stc(q + x, NEG_INF);
+    if (qs != nullptr && d0 > 0 && qs[x] > cq) {  // ascending x: the least id keeps a tie
+      cq = qs[x];
+      ci = x;
+    }
     bad |= ((d0 > 0) != (d1 > 0));
     if (d0 > 0) {
       nlive++;
@@ -894,13 +936,16 @@ __device__ __forceinline__ EnvAgg env_features(const EnvView<GL>& E, int n, int*
   ag.bad = bad;
   ag.th0 = th0;
   ag.th1 = th1;
+  ag.cand = qs != nullptr ? block_argmax_f(cq, ci, E.tmp) : -1;
   return ag;
 }
 
 // Phase A's copy of a speculative slot's degrees, live list and aggregates (env_features of
 // the same state) to the graph's HBM arrays; q = -inf for every node.
+// (ld0, ld1: the degrees also into the LDS degree arrays, for the neighbour-list builder)
 __device__ __forceinline__ EnvAgg env_copy_features(const int* slot, int n, int et, int* gdeg0, int* gdeg1, float* lv,
-                                                    float* q) {
+                                                    float* q, const float* qs = nullptr, int* tmp = nullptr,
+                                                    lds_i32* ld0 = nullptr, lds_i32* ld1 = nullptr) {
   const int* sd = slot + sres_deg(et);
   const float* sl = (const float*)(slot + sres_live(et, n));
   // every load in one round trip: the header words, the degrees and the live entries up to n
@@ -911,6 +956,8 @@ __device__ __forceinline__ EnvAgg env_copy_features(const int* slot, int n, int 
   constexpr int U = 4;
   int d0[U], d1[U];
   float4 le[U];
+  float cq = NEG_INF;
+  int ci = -1;
   for (int x0 = threadIdx.x; x0 < n; x0 += U * NTHREADS) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -927,12 +974,21 @@ __device__ __forceinline__ EnvAgg env_copy_features(const int* slot, int n, int 
       if (x < n) {
         stc(gdeg0 + x, d0[u]);
         stc(gdeg1 + x, d1[u]);
+        if (ld0 != nullptr) {
+          uf_store(ld0, x, d0[u]);
+          uf_store(ld1, x, d1[u]);
+        }
         stc(q + x, NEG_INF);
         if (x < h[0]) stc4(lv, x * 16, le[u]);
+        if (qs != nullptr && d0[u] > 0 && (qs[x] > cq || (qs[x] == cq && x < ci))) {
+          cq = qs[x];
+          ci = x;
+        }
       }
     }
   }
   EnvAgg ag;
+  ag.cand = qs != nullptr ? block_argmax_f(cq, ci, tmp) : -1;
   ag.nlive = h[0];
   ag.dm0 = h[1];
   ag.dm1 = h[2];
@@ -943,6 +999,16 @@ __device__ __forceinline__ EnvAgg env_copy_features(const int* slot, int n, int 
   ag.th1 = (long long)(((unsigned long long)(unsigned)h[9] << 32) | (unsigned)h[8]);
   return ag;
 }
+
+// Queue launches: the speculative environment-step result slot of graph gi for the state after
+// `steps` removals (two per graph, by removal-count parity; md_abi.cpp sizes them).  SRES layout
+// plus word 24: the tag of the last speculative item that left the slot (the slot is free when
+// it equals the STARTED word's tag).
+__device__ __forceinline__ int* bspec_slot(KParams& p, const GraphInfo& gi, int steps) {
+  return p.bspec + (size_t)(steps & 1) * (size_t)p.bspec_half +
+         4 * ((size_t)9 * gi.gidx + (size_t)gi.eoff[0] + (size_t)gi.eoff[1] + 2 * (size_t)gi.node_off);
+}
+constexpr int BSPEC_EXITED = 24;
 
 // ------------------------------------------------------------------ the environment step
 // Everything phase A does for one graph once the actions to apply are known: cover each
@@ -1069,17 +1135,19 @@ __device__ __forceinline__ void stage_bytes(lds_u8* dst, const v4u& w, int c, in
     if (x >= 0 && x < cnt) dst[x] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
   }
 }
-__device__ __forceinline__ void env_stage_wide(const EnvView<false>& E, int n) {
+__device__ __forceinline__ void env_stage_wide(const EnvView<false>& E, int n, const float* gq = nullptr,
+                                               lds_u8* qdst = nullptr) {
   const int tid = threadIdx.x, e0 = E.e0, e1 = E.et - E.e0;
-  // dynamic segments (uniform bases): states of layer 0 / 1, covered flags; two chunks per
-  // thread in flight per segment (up to 16 K edges per layer and 16 K nodes), the rest after
-  const uint8_t* dp[3] = {E.gst[0], E.gst[1], E.gcov};
-  const int dn[3] = {e0, e1, n};
+  // dynamic segments (uniform bases): states of layer 0 / 1, covered flags, and (gq: batch
+  // speculation) the graph's Q row as bytes; two chunks per thread in flight per segment (up to
+  // 16 K edges per layer and 16 K nodes), the rest after
+  const uint8_t* dp[4] = {E.gst[0], E.gst[1], E.gcov, qdst != nullptr ? (const uint8_t*)gq : E.gcov};
+  const int dn[4] = {e0, e1, n, qdst != nullptr ? 4 * n : 0};
   constexpr int DQ = 2;
-  v4u dv[3][DQ];
-  int dlead[3], dch[3];
+  v4u dv[4][DQ];
+  int dlead[4], dch[4];
 #pragma unroll
-  for (int s = 0; s < 3; ++s) {
+  for (int s = 0; s < 4; ++s) {
     dlead[s] = (int)((uintptr_t)dp[s] & 15);
     dch[s] = (dlead[s] + dn[s] + 15) >> 4;
     const uint8_t* a = dp[s] - dlead[s];
@@ -1143,9 +1211,10 @@ __device__ __forceinline__ void env_stage_wide(const EnvView<false>& E, int n) {
       }
     }
   }
-  lds_u8* const ddst[3] = {E.st, E.st + e0, E.cov8};
+  lds_u8* const ddst[4] = {E.st, E.st + e0, E.cov8, qdst};
 #pragma unroll
-  for (int s = 0; s < 3; ++s) {
+  for (int s = 0; s < 4; ++s) {
+    if (s == 3 && qdst == nullptr) break;
 #pragma unroll
     for (int k = 0; k < DQ; ++k) {
       const int c = tid + k * NTHREADS;
@@ -1157,12 +1226,14 @@ __device__ __forceinline__ void env_stage_wide(const EnvView<false>& E, int n) {
 }
 
 // LDS mode: the whole environment of the last write-back, and its alive-edge list.
-__device__ __forceinline__ void env_stage_lds(const EnvView<false>& E, int n) {
-  if (E.variant & 0x100) {  // MD_VARIANT bit 8 (diagnostics): the batched two-pass staging
+// (gq, qdst: also the graph's Q row into LDS, for the batch speculation's candidate)
+__device__ __forceinline__ void env_stage_lds(const EnvView<false>& E, int n, const float* gq = nullptr,
+                                              lds_u8* qdst = nullptr) {
+  if ((E.variant & 0x100) && qdst == nullptr) {  // MD_VARIANT bit 8 (diagnostics): the batched two-pass staging
     env_stage_static(E, n);
     env_stage_dynamic(E, n);
   } else {
-    env_stage_wide(E, n);
+    env_stage_wide(E, n, gq, qdst);
   }
   __syncthreads();
   build_alive<false>(E);
@@ -1339,8 +1410,14 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
   // (this step changes the state without the grid-wide step's class labels: they go stale)
   if (threadIdx.x == 0 && p.lab_ok != nullptr) stc(p.lab_ok + gi.gidx, 0);
   const EnvView<GL> E = env_view<GL>(p, gi, ia);
+  // batch speculation (queue launches): the graph's previous Q row staged beside the state, for
+  // the next step's candidate (after the environment arrays: free until the neighbour lists)
+  const float* qs = nullptr;
   if constexpr (!GL) {
-    if (!staged) env_stage_lds(E, n);
+    const int qoff = env_layout(n, et).total;
+    const bool bq = p.bspec != nullptr && !staged && qoff + n <= A_WORDS;
+    if (bq) qs = (const float*)(ia + qoff);
+    if (!staged) env_stage_lds(E, n, bq ? p.q + gi.node_off : nullptr, bq ? (lds_u8*)(uint8_t*)(ia + qoff) : nullptr);
     __syncthreads();
   }
   QENV(0);
@@ -1422,6 +1499,29 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
       __syncthreads();
     }
   }
+  // queue launches: a speculative environment item (bspec_spec_step) may have run this step for
+  // the node now chosen, from exactly this state (tag: launch, removals so far, node)
+  const int* spec_ptr = spec_slot >= 0 ? p.sres + (size_t)spec_slot * p.sres_stride : nullptr;
+  if constexpr (!GL) {
+    if (p.bspec != nullptr && p.n_spec == 0 && pend_n == 1 && gv.s0_done && !(p.variant & 0x2000)) {
+      const int* sl = bspec_slot(p, gi, gv.steps);
+      if (threadIdx.x == 0) {
+        const int a = pend_first >= 0 ? pend_first
+                                      : __hip_atomic_load(p.pend + gi.node_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long v = __hip_atomic_load((const g_u64*)sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool hit = (unsigned)v == spec_tag(p.launch_seq, gv.steps) && (int)((v >> 32) & 0xffffu) == a;
+        E.tmp[A_TMP_WORDS - 1] = hit ? 1 : 0;
+        E.tmp[A_TMP_WORDS - 2] = (int)(v >> 48);
+      }
+      __syncthreads();
+      if (E.tmp[A_TMP_WORDS - 1]) {
+        spec_ptr = sl;
+        spec_nd = E.tmp[A_TMP_WORDS - 2];
+      }
+      __syncthreads();
+    }
+  }
+  bool spec_used = false;
   MD_PROF_A(1);
   unsigned long long* acc = nullptr;
   if (p.prof != nullptr && blockIdx.x == 0) {
@@ -1449,8 +1549,9 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
     int pr[2], c[2];
     int lm;
     if constexpr (!GL) {
-      if (k == 0 && spec_slot >= 0) {
-        lm = env_apply_spec(E, p.sres + (size_t)spec_slot * p.sres_stride, spec_nd, pr, c);
+      if (k == 0 && spec_ptr != nullptr) {
+        lm = env_apply_spec(E, spec_ptr, spec_nd, pr, c);
+        spec_used = true;
         if (threadIdx.x == 0) gv.spec_hits += 1;
         if (p.df != nullptr && pend_n == 1 && p.run_mode == RUN_ROLLOUT && E.tmp[A_TMP_WORDS - 3] && threadIdx.x == 0 &&
             ((volatile int*)(lds_base + L_MISC))[48] == 0)
@@ -1496,13 +1597,21 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
   int* gdeg1 = p.deg[1] + gi.node_off;
   float* lv = (float*)(p.live + 4 * (size_t)gi.node_off);
   EnvAgg ag;
-  if (spec_slot >= 0 && E.tmp[A_TMP_WORDS - 3]) {
+  if (spec_used && E.tmp[A_TMP_WORDS - 3]) {
     // the speculative workgroup also produced this step's degrees, live list and aggregates
-    ag = env_copy_features(p.sres + (size_t)spec_slot * p.sres_stride, n, et, gdeg0, gdeg1, lv, q);
+    lds_i32* ld0 = nullptr;
+    lds_i32* ld1 = nullptr;
+    if constexpr (!GL) {
+      ld0 = E.deg0;
+      ld1 = E.deg1;
+    }
+    ag = env_copy_features(spec_ptr, n, et, gdeg0, gdeg1, lv, q, qs, E.tmp, ld0, ld1);
     if (acc != nullptr && threadIdx.x == 0) acc[59] = 1;  // diagnostics: slot 75, features copied
   } else {
-    ag = env_features<GL>(E, n, gdeg0, gdeg1, lv, q);
+    ag = env_features<GL>(E, n, gdeg0, gdeg1, lv, q, qs);
   }
+  // the next step's candidate for the batch speculation (-1: none)
+  if (threadIdx.x == 0) ((volatile int*)(lds_base + L_MISC))[20] = qs != nullptr ? ag.cand : -1;
   const int tot = ag.nlive, dm0 = ag.dm0, dm1 = ag.dm1, sd0 = ag.sd0, sd1 = ag.sd1, bad = ag.bad;
   const long long th0 = ag.th0, th1 = ag.th1;
   MD_PROF_A(34);

@@ -2873,6 +2873,119 @@ __device__ __forceinline__ bool env_build_lists(KParams&, const GraphInfo gi, in
   return true;
 }
 
+// ------------------------------------------------------------------ batch speculation
+// Queue launches (wave items, md_queue_kernel): the environment item of step t queues, beside
+// its iteration-1 tiles, a speculative item for the graph's likely next pick -- the live node of
+// largest Q(t - 1) after step t (env_features' candidate) -- that stages the state after step t,
+// covers that node, runs the same mutual-LMCC fixed point and publishes the result in the
+// graph's slot of this removal-count parity (spec_loop's SRES layout and tags) while the forward
+// pass of step t runs.  The environment item of step t + 1 takes it when it picks that node
+// (env_step: apply the kill list, copy the features) and runs the fixed point itself otherwise.
+// Slot ownership: the environment item claims a slot (STARTED = {node, tag}) only when the last
+// item on it has left (EXITED = that item's tag, written after all its stores drained), so no
+// two items ever write one slot; step t + 1 reads a result only through its done and features
+// tags, each written after the data it covers drained, and naming its own launch, removal count
+// and node.  A state staged while step t + 1 already rewrites it can only give a result tagged
+// for removal count t, which no later step asks for.
+__device__ __forceinline__ unsigned bspec_item(int gl, int steps) { return q_item(QK_ENV, 2, gl, steps & 1); }
+
+// The speculative item of graph slot gl (the whole workgroup; phase A's LDS area, so the caller
+// reloads the weights afterwards).
+__device__ __noinline__ void bspec_step(KParams&, int gl, int par) {
+  KParams& p = kp();
+  float* const lds = lds_base();
+  int* misc = (int*)(lds + L_MISC);
+  const int g = p.glist[gl];
+  const GraphInfo gi = p.ginfo[g];
+  const int n = gi.n, et = gi.e[0] + gi.e[1];
+  int* slot = bspec_slot(p, gi, par);
+  if (threadIdx.x == 0) {
+    const unsigned long long stw = __hip_atomic_load((const g_u64*)(slot + SRES_STARTED), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+    const int s_now = ldc(&p.gvar[g].steps), st = ldc(&p.gvar[g].status);
+    const unsigned tag = (unsigned)stw;
+    const int c = (int)(stw >> 32);
+    // still the state this item was queued for (a later environment step already took its place
+    // otherwise), and a state the LDS environment holds
+    const bool ok = tag == spec_tag(p.launch_seq, s_now) && st == ST_RUN && c >= 0 && c < n &&
+                    phase_a_fits_lds(n, et) && (s_now & 1) == par;
+    misc[22] = ok ? 1 : 0;
+    misc[23] = c;
+    misc[24] = (int)tag;
+  }
+  __syncthreads();
+  const unsigned tag = (unsigned)misc[24];
+  if (misc[22]) {
+    const int c = misc[23];
+    int* ia = (int*)(lds + L_W);
+    const EnvView<false> E = env_view<false>(p, gi, ia);
+    env_stage_lds(E, n);
+    __syncthreads();
+    if (threadIdx.x == 0) E.cov8[c] = 1;  // c is live, hence not covered
+    __syncthreads();
+    int pr[2], cc[2];
+    const int lm = mcc_fixed_point<false>(E, pr, nullptr, c, cc);
+    const int nd = E.hdr[1];
+    for (int i = threadIdx.x; i < nd; i += NTHREADS) {
+      const int e = E.dl[i];
+      if (!MD_BOK(e < et, 24)) continue;
+      const int l = e < E.e0 ? 0 : 1, kk = e < E.e0 ? e : e - E.e0;
+      stc(slot + SRES_HDR + 3 * i, e | ((int)E.st[e] << 16));
+      stc(slot + SRES_HDR + 3 * i + 1, E.epos[l][2 * kk]);
+      stc(slot + SRES_HDR + 3 * i + 2, E.epos[l][2 * kk + 1]);
+    }
+    if (threadIdx.x == 0) {
+      stc(slot + 2, lm);
+      stc(slot + 3, pr[0]);
+      stc(slot + 4, pr[1]);
+      stc(slot + 5, cc[0]);
+      stc(slot + 6, cc[1]);
+      stc(slot + 7, nd);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)  // {killed edges << 48 | node << 32 | tag}
+      __hip_atomic_store((g_u64*)slot, ((unsigned long long)(unsigned)(c | (nd << 16)) << 32) | tag, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    const EnvAgg ag = env_features<false>(E, n, slot + sres_deg(et), slot + sres_deg(et) + n,
+                                          (float*)(slot + sres_live(et, n)), nullptr);
+    if (threadIdx.x == 0) {
+      stc(slot + 12, ag.nlive);
+      stc(slot + 13, ag.dm0);
+      stc(slot + 14, ag.dm1);
+      stc(slot + 15, ag.sd0);
+      stc(slot + 16, ag.sd1);
+      stc(slot + 17, ag.bad);
+      stc(slot + 18, (int)(ag.th0 & 0xffffffffll));
+      stc(slot + 19, (int)(ag.th0 >> 32));
+      stc(slot + 20, (int)(ag.th1 & 0xffffffffll));
+      stc(slot + 21, (int)(ag.th1 >> 32));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store((g_u64*)(slot + SRES_FEAT), ((unsigned long long)(unsigned)c << 32) | tag, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // leave the slot (after every store of this item drained)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) stc(slot + BSPEC_EXITED, (int)tag);
+}
+
+// The environment item's side (thread 0, after phase A; the candidate in misc[20]): the slot of
+// the new state's parity, free (EXITED == STARTED) -> claimed for the candidate.  Returns
+// whether to queue the speculative item (bspec_item) with the tiles.  stw / exw: the slot's
+// words, loaded earlier (their round trip overlaps the neighbour lists).
+__device__ __forceinline__ bool bspec_claim(KParams& p, const GraphInfo& gi, int steps, int cand, unsigned long long stw,
+                                            unsigned exw) {
+  if (cand < 0 || (unsigned)stw != exw) return false;
+  __hip_atomic_store((g_u64*)(bspec_slot(p, gi, steps) + SRES_STARTED),
+                     ((unsigned long long)(unsigned)cand << 32) | spec_tag(p.launch_seq, steps), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
 // One tile of one graph for iteration `it` (queue mode; the same pieces and order as the
 // lock-step tile loop).  Neighbour lists: built and cached at iteration 1, reloaded at 2-3.
 __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int it, int j) {
@@ -3833,10 +3946,18 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
     if (kind == QK_EXIT || kind == 0u) break;
     const int it = (int)((item >> 3) & 3u), gl = q_item_gl(item), j = q_item_j(item);
     const int g = p.glist[gl];
+    if (kind == QK_ENV && it == 2) {  // batch speculation: the next step's fixed point for the candidate
+      bspec_step(p, gl, j);
+      pre = q_peek(p, tk);
+      wdirty = true;
+      if (qp != nullptr && threadIdx.x == 0) atomicAdd(qp + kind, (tq = wall_clock64()) - ti);
+      continue;
+    }
     if (kind == QK_ENV) {
 #ifdef MD_QPROF
       const unsigned long long tqa = wall_clock64();
 #endif
+      if (threadIdx.x == 0) misc[20] = -1;  // (env_step sets the candidate)
       const bool lds_env = phase_a(p, g, it != 0, lds, false);
 #ifdef MD_QPROF
       if (qp != nullptr && (p.variant & 8) && threadIdx.x == 0) atomicAdd(qp + 85, wall_clock64() - tqa);
@@ -3877,6 +3998,16 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
 #ifdef MD_QPROF
         const unsigned long long tqb = wall_clock64();
 #endif
+        // batch speculation: the slot words of the new state's parity (loaded before the lists)
+        const GraphVar& gvv = *(const GraphVar*)(lds + L_GV);
+        const bool bsp = p.bspec != nullptr && lds_env;
+        unsigned long long bst = 0ull;
+        unsigned bex = 1u;
+        if (bsp && threadIdx.x == 0) {
+          const int* sl = bspec_slot(p, p.ginfo[g], gvv.steps);
+          bst = __hip_atomic_load((const g_u64*)(sl + SRES_STARTED), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          bex = (unsigned)ldc(sl + BSPEC_EXITED);
+        }
         // (in the tail -- one tile per item -- the iteration-1 tiles build their own lists: the
         // environment item is on the graph's critical path and most workgroups are idle)
         const bool built = lds_env && tpi > 1 && env_build_lists(p, p.ginfo[g], gl);
@@ -3886,8 +4017,11 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
         if (threadIdx.x == 0) {
           stc(p.qg + 2 * gl + 1, ni | (nt << 16) | (tpi << 28));
           stc(p.qg + 2 * QG_CAP + gl, built ? 1 : 0);
+          misc[21] = bsp && bspec_claim(p, p.ginfo[g], gvv.steps, misc[20], bst, bex) ? 1 : 0;
         }
-        q_push(p, ni, [&](int i) { return q_item_tile(1, gl, i, nt, tpi); }, bc);
+        __syncthreads();
+        const int ns = misc[21], steps = gvv.steps;
+        q_push(p, ni + ns, [&](int i) { return i < ni ? q_item_tile(1, gl, i, nt, tpi) : bspec_item(gl, steps); }, bc);
       } else if (st == ST_WAIT_HOST) {
         q_push(p, 1, [&](int) { return q_item(QK_ENV, 1, gl, 0); }, bc);  // poll again later
       } else {

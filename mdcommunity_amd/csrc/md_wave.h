@@ -1009,7 +1009,14 @@ __device__ void wq_env(KParams& p, float* lds, unsigned item) {
   const int ng = p.nglist;
   const int it = (int)((item >> 3) & 3u), gl = q_item_gl(item);
   const int g = p.glist[gl];
-  if (threadIdx.x == 0) wq_event(p, gl, 0);
+  if (it == 2) {  // batch speculation: the next step's fixed point for the candidate
+    bspec_step(p, gl, q_item_j(item));
+    return;
+  }
+  if (threadIdx.x == 0) {
+    wq_event(p, gl, 0);
+    misc[20] = -1;  // (env_step sets the candidate)
+  }
   WQTE_INIT();
   // the tail-park test's words, read before phase A instead of after it (both only move toward
   // parking -- QC_REM down, QC_ADMIT up -- so an early read parks no graph too soon)
@@ -1037,13 +1044,26 @@ __device__ void wq_env(KParams& p, float* lds, unsigned item) {
   WQTE(1);  // park check
   if (st == ST_RUN && !park) {
     const int nt = (nl + TILE - 1) / TILE;
+    // batch speculation: the slot words of the new state's parity (the loads' round trip
+    // overlaps the neighbour lists), then the claim
+    const bool bsp = p.bspec != nullptr && lds_env;
+    unsigned long long bst = 0ull;
+    unsigned bex = 1u;
+    if (bsp && threadIdx.x == 0) {
+      const int* sl = bspec_slot(p, p.ginfo[g], gv.steps);
+      bst = __hip_atomic_load((const g_u64*)(sl + SRES_STARTED), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      bex = (unsigned)ldc(sl + BSPEC_EXITED);
+    }
     const bool built = lds_env && env_build_lists(p, p.ginfo[g], gl);
     WQTE(2);  // neighbour lists
     if (threadIdx.x == 0) {
       stc(p.qg + 2 * gl + 1, nt | (nt << 16) | (1 << 28));
       stc(p.qg + 2 * QG_CAP + gl, built ? 1 : 0);
+      misc[21] = bsp && !(p.variant & 0x4000) && bspec_claim(p, p.ginfo[g], gv.steps, misc[20], bst, bex) ? 1 : 0;
     }
-    q_push(p, nt, [&](int i) { return q_item(QK_TILE, 1, gl, i); }, bc);
+    __syncthreads();
+    const int ns = misc[21], steps = gv.steps;
+    q_push(p, nt + ns, [&](int i) { return i < nt ? q_item(QK_TILE, 1, gl, i) : bspec_item(gl, steps); }, bc);
     if (threadIdx.x == 0) wq_event(p, gl, 5);
     WQTE(3);  // stage word, push
   } else if (st == ST_WAIT_HOST) {

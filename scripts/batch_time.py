@@ -34,4 +34,7 @@ print("batch %d (%s): removals %d, kernel ms best %.2f median %.2f -> %.0f remov
     nb, sys.argv[3] if len(sys.argv) > 3 else "default", rem, ts[0], ts[len(ts) // 2], rem / ts[len(ts) // 2] * 1e3,
     ws[len(ws) // 2], rem / ws[len(ws) // 2] * 1e3), flush=True)
 print("  longest rollout %d removals: %.1f us of kernel per step of it" % (lmax, ts[len(ts) // 2] * 1e3 / lmax), flush=True)
+if os.environ.get("MD_HITS"):  # speculative environment steps taken, over the batch (last rollout)
+    hs = [eng.spec_stats(g) for g in range(nb)]
+    print("  speculative steps taken: %d of %d removals" % (sum(h for h, _ in hs), sum(r for _, r in hs)), flush=True)
 eng.close()

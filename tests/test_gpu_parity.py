@@ -598,6 +598,53 @@ def test_wave_items_match_workgroup_items(monkeypatch, cost):
 
 
 @pytest.mark.parametrize("cost", ["unit", "degree"])
+@pytest.mark.parametrize("wq", ["1", "0"])
+def test_batch_speculation_same_rollouts(monkeypatch, cost, wq):
+    """Queue launches with speculative environment items (MD_BSPEC=1; off by default: the environment
+    item of step t queues the fixed point of the likely next pick, the live node of largest Q(t-1);
+    step t + 1 applies it when it picks that node) give the removal sequences and LMCC traces of
+    queue launches without them (MD_BSPEC=0), in the wave-item kernel and md_queue_kernel, unit and
+    degree cost, over two rollouts of the same load (slots reused across launches); the
+    speculation takes part in a good share of the steps (md_spec_stats)."""
+    rng = np.random.default_rng(7)
+    hub = (3000, _hub_layer(3000, 3, 2400, rng), _hub_layer(3000, 3, 2400, rng))
+    names = ["gmm200_s7", "er100", "er300_dense", "gmm1000_s1", "gmm1000_s0"]
+    graphs = [(int(z["n_nodes"]), z["edges0"], z["edges1"]) for z in map(load_golden, names)]
+    batch = [hub] + [graphs[i % len(graphs)] for i in range(23)]
+    w, mode = ((engine.load_weights(engine.DEFAULT_UNIT), _lib.MD_COST_UNIT) if cost == "unit" else
+               (engine.load_weights(engine.DEFAULT_DEGREE), _lib.MD_COST_DEGREE))
+    node_w = None
+    if cost == "degree":
+        from mdcommunity_amd import graph as mgraph
+        node_w = mgraph.node_weight_array([mgraph.Graph_test.from_edges(n, e0, e1) for n, e0, e1 in batch])
+    monkeypatch.setenv("MD_WQPARK", "0")
+    monkeypatch.setenv("MD_QPARK", "0")
+    monkeypatch.setenv("MD_WQ", wq)
+    out, hits, rem = {}, 0, 0
+    for bs in ("0", "1"):
+        monkeypatch.setenv("MD_BSPEC", bs)
+        e = _lib.Engine(w, cost_mode=mode)
+        try:
+            e.load_graphs(batch, node_w=node_w)
+            runs = []
+            for _ in range(2):
+                e.reset()
+                runs.append([(s.tolist(), r.tolist()) for s, r in e.rollout()])
+            assert runs[0] == runs[1]
+            out[bs] = runs[0]
+            if bs == "1":
+                for g in range(len(batch)):
+                    h, r = e.spec_stats(g)
+                    hits += h
+                    rem += r
+        finally:
+            e.close()
+    for i, (a, b) in enumerate(zip(out["0"], out["1"])):
+        assert a == b, i
+    assert hits > 0.2 * rem, (hits, rem)
+
+
+@pytest.mark.parametrize("cost", ["unit", "degree"])
 def test_dataflow_mode_same_rollouts(monkeypatch, cost):
     """The barrier-free dataflow mode of single-graph rollouts (MD_DF=1, default: tagged granules
     for the step record, rows and partials; the tiles derive phase A's pick from the arg-max
