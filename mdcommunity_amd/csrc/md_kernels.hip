@@ -323,6 +323,17 @@ __device__ __forceinline__ bool md_bok(bool ok, int site) {
 #else
 #define MD_BOK(cond, site) true
 #endif
+// Torn-slot diagnostic build (-DMD_TORN_SLOT, make torn-slot; with MD_DEBUG_BOUNDS): the first-
+// layer row reads of a speculated iteration 1 are checked against [1, dmax] instead of clamped
+// to it; a blocked read is counted (md_profile buffer, step row 0, slot 70 + site: 92 own rows,
+// 93 neighbour rows) and skipped.
+#ifdef MD_TORN_SLOT
+__device__ __forceinline__ bool md_brec(bool ok, int site) {
+  KParams& p = kp();
+  if (!ok && p.prof != nullptr && p.prof_cap > 0) atomicAdd(p.prof + 70 + site, 1ull);
+  return ok;
+}
+#endif
 
 // ------------------------------------------------------------------ dataflow mode: granules
 // Single-graph rollouts in dedicated mode with the layer split run without any grid barrier
@@ -1229,6 +1240,11 @@ __device__ __noinline__ int prebuild_lists(KParams&, const GraphInfo gi, int j, 
   TSTAMP(24);  // diagnostics (one tile's prebuild): slot polled
   if (!misc[44]) return 0;
   const int nd = misc[45], nl = misc[46];
+#ifdef MD_TORN_SLOT
+  const int ndk = misc[25] ? 0 : nd;  // (torn step: the kill list read stale, after the tag checks)
+#else
+  const int ndk = nd;
+#endif
   // the tile's rows from the result's live list (entries as in phase A's list) and every killed
   // edge's three words, all in one round trip
   float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1277,7 +1293,7 @@ __device__ __noinline__ int prebuild_lists(KParams&, const GraphInfo gi, int j, 
 #pragma unroll
   for (int u = 0; u < KPT; ++u) {
     const int i = threadIdx.x + u * NTHREADS;
-    if (i < nd && ((kv[u] & 0xffff) < gi.e[0] ? 0 : 1) == L) {
+    if (i < ndk && ((kv[u] & 0xffff) < gi.e[0] ? 0 : 1) == L) {
       kh_insert(kh, k1[u]);
       kh_insert(kh, k2[u]);
     }
@@ -1454,9 +1470,18 @@ __device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it,
   const lds_u16* nbl = (const lds_u16*)(const uint16_t*)(scr + S_NBL) + l * NB_CAP;
   const int v = rows[r];
   float2 own = {0.f, 0.f}, acc = {0.f, 0.f};
+#ifdef MD_TORN_SLOT
+  // (a torn speculative slot, this step: the degree words of odd nodes read as 0)
+  const bool torn = deg_ovr != nullptr && ((const int*)(lds_base() + L_MISC))[25] != 0;
+  auto rdeg = [&](int x) { return torn && (x & 1) ? 0 : ldc(deg + x); };
+  auto row_of = [&](int d, int site) { return md_brec(d >= 1 && d <= dcap, site) ? d : -1; };
+#else
+  auto rdeg = [&](int x) { return ldc(deg + x); };
+  auto row_of = [&](int d, int) { return min(max(d, 1), dcap); };
+#endif
   if (v >= 0) {
-    const int ov = table ? min(max(ldc(deg + v), 1), dcap) : v;
-    if (MD_BOK(v < gi.n && ov >= 0 && ov < gi.n, 1)) own = ldc2(hp, ov * 256 + q * 8);
+    const int ov = table ? row_of(rdeg(v), 22) : v;
+    if (ov >= 0 && MD_BOK(v < gi.n && ov < gi.n, 1)) own = ldc2(hp, ov * 256 + q * 8);
   }
   const int myoff = hdr[l * 16 + r], mycnt = hdr[32 + l * 16 + r];
   const int totl = hdr[128 + l];
@@ -1472,7 +1497,7 @@ __device__ __noinline__ void gather_tile2s(KParams&, const GraphInfo gi, int it,
       src[i] = -1;
       if (b < nbat && k < SROWS * 16 && row < totl) {
         const int id = nbl[row];
-        src[i] = MD_BOK(id < gi.n, 4) ? (table ? min(max(ldc(deg + id), 1), dcap) : id) : -1;
+        src[i] = MD_BOK(id < gi.n, 4) ? (table ? row_of(rdeg(id), 23) : id) : -1;
         if (!MD_BOK(src[i] < gi.n, 5)) src[i] = -1;
       }
     }
@@ -4697,6 +4722,9 @@ __device__ __noinline__ void df_tiles(KParams&) {
     if (threadIdx.x == 0) {
       misc[60] = pstep;
       misc[30] = 0;  // this step's self-pick not decided yet (df_wait_rec)
+#ifdef MD_TORN_SLOT
+      misc[25] = pstep % 3 == 1;  // every third step: the prebuild reads a torn slot
+#endif
     }
     __syncthreads();
     // the step record; meanwhile the iteration-1 prebuild, first from the self-pick (the result
@@ -4706,9 +4734,16 @@ __device__ __noinline__ void df_tiles(KParams&) {
     // the same state and tile assignment)
     int pre_state = 0, r;
     unsigned long long pre_used = 0ull;
+#ifdef MD_TORN_SLOT
+    unsigned long long torn_tried = 0ull;  // (a torn step's prebuild runs once per early word)
+#endif
     while ((r = df_wait_rec(p, (unsigned)(pstep + 1), true, false, pstep - 1,
                             pstep >= 1 ? (nl_prev + TILE - 1) / TILE : 0)) >= 2) {
       const unsigned long long ew = r == 2 ? *seen : *tried0;  // (4: the self-pick)
+#ifdef MD_TORN_SLOT
+      if (misc[25] && ew == torn_tried) continue;
+      torn_tried = ew;
+#endif
       if (ew != 0ull && ew != pre_used) {
         DF_STAMP_MAX(54);
         pre_used = 0ull;
@@ -4717,6 +4752,14 @@ __device__ __noinline__ void df_tiles(KParams&) {
         pre_state = prebuild_lists(p, gi, j, L, ew, pts, r >= 3 ? *seen : 0ull);
         DF_STAMP_MAX(55);
         if (pre_state) pre_used = ew;
+#ifdef MD_TORN_SLOT
+        // a torn slot belongs to a result phase A does not take: the prebuild's early word (and
+        // so its rows' tag) names the other slot of the pair
+        const unsigned long long ewt = misc[25] ? ew ^ 1ull : ew;
+        if (pre_state) pre_used = ewt;
+#else
+        const unsigned long long ewt = ew;
+#endif
         // a self-pick prebuild that phase A's early word has already overtaken (it names another
         // result) stops after its lists
         const unsigned long long now = ((unsigned long long)(unsigned)misc[37] << 32) | (unsigned)misc[36];
@@ -4725,7 +4768,7 @@ __device__ __noinline__ void df_tiles(KParams&) {
           pre_used = 0ull;
         }
         // the whole of iteration 1 too (MD_VARIANT bit 128: lists only)
-        if (pre_state == 1 && !(p.variant & 128) && spec_iteration1(p, gi, j, L, ew, df_ptag(df_tag(pstep), ew), pts))
+        if (pre_state == 1 && !(p.variant & 128) && spec_iteration1(p, gi, j, L, ew, df_ptag(df_tag(pstep), ewt), pts))
           pre_state = 3;
         DF_STAMP_MAX(56);
         DF_STAMP_TILE(2);
