@@ -1302,7 +1302,10 @@ __device__ __forceinline__ int env_apply_spec(const EnvView<false>& E, const int
   pr[1] = E.tmp[A_TMP_WORDS - 6];
   cc[0] = E.tmp[A_TMP_WORDS - 5];
   cc[1] = E.tmp[A_TMP_WORDS - 4];
-  if (nd > 0) compact_alive<false>(E);
+  // the killed edges stay in the alive list (every pass skips them by their state; the next
+  // fixed point's final compaction drops them): no compaction on the step's critical path
+  // (MD_VARIANT bit 15: compact here)
+  if (nd > 0 && (E.variant & 0x8000)) compact_alive<false>(E);
   if (threadIdx.x == 0) E.hdr[1] = 0;  // written back above
   __syncthreads();
   return lm;
