@@ -3018,6 +3018,8 @@ __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int
   float* scr = lds + L_SCR;
   int* rows = (int*)(scr + S_ROW);
   const GraphInfo gi = p.ginfo[g];
+  // iteration 3: the head granules' tag (predictions so far + 1), read now, used at the attention
+  const int npv = it == 3 ? ldc(&p.gvar[g].npred) : 0;
   lds_i32* hdr = (lds_i32*)(int*)(scr + S_NBH);
   // diagnostics (builds with -DMD_QPROF, md_profile with MD_VARIANT bit 8): per-piece device
   // ticks of the tile items, summed over items in slots 20.. (8 per iteration)
@@ -3124,7 +3126,9 @@ __device__ __noinline__ void queue_tile(KParams&, float* lds, int g, int gl, int
   __syncthreads();
   QTS(5);
   // iteration 3: the graph head was published (tag 1) before this item was pushed
-  if (it == 3) attention_q_tile(p, lds, scr, gi, g, rows, p.apart + (size_t)(gi.tile_off + j) * 4, 1ull, nullptr);
+  if (it == 3)
+    attention_q_tile(p, lds, scr, gi, g, rows, p.apart + (size_t)(gi.tile_off + j) * 4,
+                     (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(npv) + 1ull, nullptr);
   QTS(6);
 #undef QTS
 }
@@ -3507,7 +3511,7 @@ __device__ __noinline__ void normalize_pair() {
 
 // Iteration 3 of both tiles: attention_q_tile's pieces for 32 rows; the arg-max partials stay
 // per tile (tiles j, j + 1).
-__device__ __noinline__ void attention_q_pair(KParams&, const GraphInfo gi, int g, int j) {
+__device__ __noinline__ void attention_q_pair(KParams&, const GraphInfo gi, int g, int j, unsigned long long htag) {
   float* const lds = lds_base();
   float* const scr = lds + L_SCR;
   const int* const rows = (const int*)(scr + P2_ROW);
@@ -3624,7 +3628,7 @@ __device__ __noinline__ void attention_q_pair(KParams&, const GraphInfo gi, int 
   }
   __syncthreads();
   QATS(2);
-  head_receive(p, lds, g, 1ull);
+  head_receive(p, lds, g, htag);
   QATS(3);
   {
     // e[a] = sum_b (h[a] * y[b]) * cp[b] (attention_q_tile's chains, eight per thread)
@@ -3735,6 +3739,7 @@ __device__ __noinline__ void queue_pair(KParams&, float* lds, int g, int gl, int
   float* scr = lds + L_SCR;
   int* rows = (int*)(scr + P2_ROW);
   const GraphInfo gi = p.ginfo[g];
+  const int npv = it == 3 ? ldc(&p.gvar[g].npred) : 0;  // (the head granules' tag - 1, iteration 3)
   lds_i32* flag = (lds_i32*)(int*)(scr + P2_FLAG);
 #ifdef MD_QPROF
   unsigned long long* qd = p.prof != nullptr && (p.variant & 8) ? p.prof + 20 + 8 * (it - 1) : nullptr;
@@ -3856,7 +3861,7 @@ __device__ __noinline__ void queue_pair(KParams&, float* lds, int g, int gl, int
     __syncthreads();
   }
   QTS(5);
-  if (it == 3) attention_q_pair(p, gi, g, j);
+  if (it == 3) attention_q_pair(p, gi, g, j, (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(npv) + 1ull);
   QTS(6);
 #undef QTS
 }
@@ -3886,7 +3891,7 @@ __device__ __noinline__ void queue_vn(KParams&, float* lds, int g, int part) {
     return;
   }
   graph_head(p, lds, scr, gi, gv, false, false);
-  head_publish(p, lds, g, 1ull);
+  head_publish(p, lds, g, (unsigned long long)(unsigned)gv.npred + 1ull);  // (this forward pass's tag)
 }
 
 __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __restrict__ wimg) {
@@ -4101,16 +4106,19 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
       }
       __syncthreads();
       next = bc[3];
-    } else {  // QK_VN part 2
+    } else {  // QK_VN part 2 (the iteration-3 tiles went out with it; MD_VARIANT bit 9: after it)
       queue_vn(p, lds, g, 2);
       pre = q_peek(p, tk);
-      next = 4;
+      next = (p.variant & 512) ? 4 : 0;
     }
     if (next != 0) {
       const int sz = ldc(p.qg + 2 * gl + 1), ni = sz & 0xffff, nt = (sz >> 16) & 0xfff, tpi = (sz >> 28) & 3;
       if (next == 1) {
         q_push(p, ni + 1, [&](int i) { return i < ni ? q_item_tile(2, gl, i, nt, tpi) : q_item(QK_VN, 1, gl, 0); }, bc);
       } else if (next == 2) {
+        // the iteration-3 tiles now: their layer pieces need the iteration-2 rows only, their
+        // attention waits for this forward pass's head granules (part 2, run here next)
+        if (!(p.variant & 512)) q_push(p, ni, [&](int i) { return q_item_tile(3, gl, i, nt, tpi); }, bc);
         cont = q_item(QK_VN, 2, gl, 0);
       } else if (next == 3) {
         cont = q_item(QK_ENV, 1, gl, 0);
