@@ -228,9 +228,17 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *                             (test_iteration1_prebuild_same_rollouts)
  *                       512..1536 (bits 9-10 = 1..3)  tiles per queue work item (default 2)
  *                             (test_queue_admission_limit_matches_single)
+ *                       256   environment staged in batched passes instead of one pass of
+ *                             16-byte chunks (test_iteration3_order_and_staging_same_rollouts)
  *                       2048  K2 end-game shortcut off: one forward pass per removal step (the
  *                             bench's per_step_protocol_value;
  *                             test_k2_endgame_in_one_handshake_matches_per_step)
+ *                       4096  queue launches: iteration-3 tiles queued after virtual-node part 2
+ *                             instead of beside it (test_iteration3_order_and_staging_same_rollouts)
+ *                       8192, 16384  with MD_BSPEC=1: speculative results not used / not queued
+ *                             by wave items (test_batch_speculation_same_rollouts's diagnostics)
+ *                       32768 an applied speculative result compacts the alive list at once
+ *                             (test_iteration3_order_and_staging_same_rollouts)
  *                       bits 16+  queue-mode admission limit (graphs running at once)
  *                             (test_queue_admission_limit_matches_single)
  *   MD_ENV_MODE       0: no dedicated environment workgroups for small batches (shared
@@ -238,8 +246,16 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *   MD_PAIR           0: queue-mode work items run their two tiles one after the other
  *                     instead of jointly (default 1; test_paired_tiles_match_single_tiles)
  *   MD_QPARK          queue mode: once every graph is admitted and at most this many still
- *                     run, they continue in one lock-step launch (default 8, 0 = off, <= 16;
+ *                     run, they continue in one lock-step launch (default 4, 0 = off, <= 16;
  *                     tests/test_gpu_batch.py test_tail_handoff_off_same_rollouts)
+ *   MD_WQ             0: queue launches run one work item per workgroup (md_queue_kernel) from
+ *                     the start instead of one per wave (md_wq_kernel, default 1;
+ *                     test_wave_items_match_workgroup_items)
+ *   MD_WQPARK         wave-item launches of more than this many graphs park the graphs still
+ *                     running once at most this many are left; md_queue_kernel continues them
+ *                     (default 128, 0 = never; test_wave_items_match_workgroup_items runs 0)
+ *   MD_BSPEC          1: queue launches run speculative environment items for the likely next
+ *                     pick (default 0; test_batch_speculation_same_rollouts)
  *   MD_HOST_HANDSHAKE 0: end the launch on a tie and relaunch after the host selection
  *                     (default 1: in-kernel hand-shake through mapped host memory;
  *                     test_host_handshake_modes_same_rollouts)
@@ -265,6 +281,8 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *                     1: candidates ranked by residual degree, as no prediction exists yet;
  *                     test_first_request_same_rollouts)
  * Diagnostics and resources (no effect on any computation):
+ *   MD_VARIANT 4      event log of graph slot 0 in wave-item launches (md_profile;
+ *                     scripts/wq_timeline.py)
  *   MD_VARIANT bit 8  per-piece queue-mode profile stamps (md_profile; qprof build)
  *   MD_POLL_US        host-thread polling interval of the hand-shake (µs)
  *   MD_HOST_STATS     set: print hand-shake timing statistics to stderr

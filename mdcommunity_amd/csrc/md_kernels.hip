@@ -4106,10 +4106,10 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
       }
       __syncthreads();
       next = bc[3];
-    } else {  // QK_VN part 2 (the iteration-3 tiles went out with it; MD_VARIANT bit 9: after it)
+    } else {  // QK_VN part 2 (the iteration-3 tiles went out with it; MD_VARIANT bit 12: after it)
       queue_vn(p, lds, g, 2);
       pre = q_peek(p, tk);
-      next = (p.variant & 512) ? 4 : 0;
+      next = (p.variant & 4096) ? 4 : 0;
     }
     if (next != 0) {
       const int sz = ldc(p.qg + 2 * gl + 1), ni = sz & 0xffff, nt = (sz >> 16) & 0xfff, tpi = (sz >> 28) & 3;
@@ -4118,7 +4118,7 @@ __device__ __noinline__ void queue_loop(KParams&, float* lds, const float* __res
       } else if (next == 2) {
         // the iteration-3 tiles now: their layer pieces need the iteration-2 rows only, their
         // attention waits for this forward pass's head granules (part 2, run here next)
-        if (!(p.variant & 512)) q_push(p, ni, [&](int i) { return q_item_tile(3, gl, i, nt, tpi); }, bc);
+        if (!(p.variant & 4096)) q_push(p, ni, [&](int i) { return q_item_tile(3, gl, i, nt, tpi); }, bc);
         cont = q_item(QK_VN, 2, gl, 0);
       } else if (next == 3) {
         cont = q_item(QK_ENV, 1, gl, 0);

@@ -1239,9 +1239,9 @@ __device__ __forceinline__ void wq_loop(KParams&, const float* __restrict__ wimg
     } else {  // QK_VN part 2
       wq_vn(p, g, 2);
       pre = wq_peek(p, tk);
-      // (the iteration-3 tiles went out with this item; MD_VARIANT bit 9: after it)
-      next = (p.variant & 512) ? 4 : 0;
-      if (!(p.variant & 512) && lane == 0) wq_event(p, gl, 4);
+      // (the iteration-3 tiles went out with this item; MD_VARIANT bit 12: after it)
+      next = (p.variant & 4096) ? 4 : 0;
+      if (!(p.variant & 4096) && lane == 0) wq_event(p, gl, 4);
     }
     if (next != 0) {
       if (lane == 0) wq_event(p, gl, next);
@@ -1251,7 +1251,7 @@ __device__ __forceinline__ void wq_loop(KParams&, const float* __restrict__ wimg
       } else if (next == 2) {
         // the iteration-3 tiles now: their layer pieces need only the iteration-2 rows, and
         // their attention waits for this step's head granules, which part 2 publishes
-        if (!(p.variant & 512)) wq_push(p, nt, [&](int i) { return q_item(QK_TILE, 3, gl, i); });
+        if (!(p.variant & 4096)) wq_push(p, nt, [&](int i) { return q_item(QK_TILE, 3, gl, i); });
         cont = q_item(QK_VN, 2, gl, 0);
       } else if (next == 3) {
         cont = q_item(QK_ENV, 1, gl, 0);

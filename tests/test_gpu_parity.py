@@ -597,6 +597,47 @@ def test_wave_items_match_workgroup_items(monkeypatch, cost):
         assert a == b, i
 
 
+@pytest.mark.parametrize("wq", ["1", "0"])
+def test_iteration3_order_and_staging_same_rollouts(monkeypatch, wq):
+    """Queue launches (wave items and md_queue_kernel, no tail hand-off): the iteration-3 tiles
+    queued beside virtual-node part 2 (default) or after it (MD_VARIANT bit 12), and the
+    environment staged in one pass (default) or in the batched two-pass form (bit 8), give
+    identical rollouts; and a single-graph rollout whose applied speculative results compact
+    the alive list (bit 15) equals the default's."""
+    rng = np.random.default_rng(11)
+    hub = (3000, _hub_layer(3000, 3, 2400, rng), _hub_layer(3000, 3, 2400, rng))
+    names = ["gmm200_s7", "er100", "er300_dense", "gmm1000_s1"]
+    graphs = [(int(z["n_nodes"]), z["edges0"], z["edges1"]) for z in map(load_golden, names)]
+    batch = [hub] + [graphs[i % len(graphs)] for i in range(19)]
+    w = engine.load_weights(engine.DEFAULT_UNIT)
+    monkeypatch.setenv("MD_WQPARK", "0")
+    monkeypatch.setenv("MD_QPARK", "0")
+    monkeypatch.setenv("MD_WQ", wq)
+    out = {}
+    for v in ("0", "4096", "256"):
+        monkeypatch.setenv("MD_VARIANT", v)
+        e = _lib.Engine(w)
+        try:
+            e.load_graphs(batch)
+            e.reset()
+            out[v] = [(s_.tolist(), r.tolist()) for s_, r in e.rollout()]
+        finally:
+            e.close()
+    assert out["0"] == out["4096"] == out["256"]
+    z = load_golden("gmm1000_s0")
+    single = {}
+    for v in ("0", "32768"):
+        monkeypatch.setenv("MD_VARIANT", v)
+        e = _lib.Engine(w)
+        try:
+            e.load_graphs([(int(z["n_nodes"]), z["edges0"], z["edges1"])])
+            e.reset()
+            single[v] = [(s_.tolist(), r.tolist()) for s_, r in e.rollout()]
+        finally:
+            e.close()
+    assert single["0"] == single["32768"]
+
+
 @pytest.mark.parametrize("cost", ["unit", "degree"])
 @pytest.mark.parametrize("wq", ["1", "0"])
 def test_batch_speculation_same_rollouts(monkeypatch, cost, wq):
