@@ -179,6 +179,7 @@ struct md_ctx {
   // later request is out (MD_SPEC_ABORT=0: always runs to the end)
   bool abort_on = true;
   bool fp_short = true;  // MD_FP_SHORTCUT=0: every fixed point runs its confirmation round
+  bool fp_skip = true;   // MD_FP_SKIP=0: every LDS fixed-point round re-unites both layers
   bool first_req = true;  // MD_FIRST_REQ=0: no speculative request at a rollout's first step
   DevBuf<unsigned long long> dfbuf;
   int df_mt = 0, df_n = 0;
@@ -245,6 +246,7 @@ constexpr int SPEC_MAX = 32;  // speculative workgroups per launch at most (CTL_
 Params make_params(md_ctx* c) {
   Params p{};
   p.fp_short = c->fp_short ? 1 : 0;
+  p.fp_skip = c->fp_skip ? 1 : 0;
   p.first_req = c->first_req ? 1 : 0;
   p.w = c->w.p;
   p.ginfo = c->ginfo.p;
@@ -809,6 +811,7 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_EARLY")) c->early_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_SPEC_ABORT")) c->abort_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_FP_SHORTCUT")) c->fp_short = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MD_FP_SKIP")) c->fp_skip = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_FIRST_REQ")) c->first_req = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_DF")) c->df_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_SPEC")) c->spec_n = std::max(0, std::min(SPEC_MAX, std::atoi(v)));

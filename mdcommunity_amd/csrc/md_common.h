@@ -197,6 +197,7 @@ struct Params {
   int df_mt;                       // tiles of the largest graph the buffer is sized for
   int df_n;                        // nodes of that graph
   int fp_short;                    // 1: mutual-LMCC fixed points end by the confirmation shortcut (mcc_fixed_point)
+  int fp_skip;                     // 1: LDS fixed-point rounds skip the layers the last prune left unchanged
   int first_req;                   // 1: a rollout's first step requests degree-ranked speculative results (env_step)
 };
 // global-mode environment scratch words per node (md_env.h env_view: parents, degrees) and the

@@ -539,6 +539,16 @@ __device__ __forceinline__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, 
   bool first = true, dirty = cover >= 0;  // dead entries in the alive list
   bool skipped = false;                   // ended by the confirmation shortcut (labels: table slots in deg1)
   const bool shortcut = !GL && kp().fp_short;
+  // Unchanged layers (LDS mode; MD_FP_SKIP=0: off): a layer none of whose edges the last prune
+  // removed has the same alive edges, hence the same components, labels and spanning forest as
+  // in the last round -- its union and label work is skipped, and so is pruning the other
+  // layer's edges by it (every edge crossing its partition went in that prune).  ch0 / ch1:
+  // the layer's edge set changed since its last union pass (the shortcut's table overwrites
+  // both parent arrays and layer 1's labels: a failed check marks layer 1 changed).  The
+  // alive list is in ascending edge id, so a layer's entries are one range ([0, na0) layer 0).
+  const bool lskip = !GL && kp().fp_skip;
+  bool ch0 = true, ch1 = true;
+  int na0 = -1;  // layer 0's alive-list entries (found at the first skip)
   unsigned long long ab_ew = 0ull, ab_ew2 = 0ull, ab_req = 0ull;  // thread 0: loaded during the previous round's prune
   while (true) {
     unsigned long long tp = wall_clock64();
@@ -552,12 +562,23 @@ __device__ __forceinline__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, 
       }
     }
     for (int x = threadIdx.x; x < n; x += NTHREADS) {
-      uf_store(E.par0, x, x);
-      uf_store(E.par1, x, x);
+      if (ch0) uf_store(E.par0, x, x);
+      if (ch1) uf_store(E.par1, x, x);
     }
     __syncthreads();
     if constexpr (!GL) {
       if (ab != nullptr && !first && E.hdr[3] != 0) return -1;
+      if (!(ch0 && ch1) && na0 < 0) {
+        // (every thread the same bisection: the first entry of layer 1)
+        const lds_u16* al = E.hdr[2] ? E.al_other : E.al;
+        int lo = 0, hi = E.hdr[0];
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if ((int)al[mid] < E.e0) lo = mid + 1;
+          else hi = mid;
+        }
+        na0 = lo;
+      }
     }
     PACC(acc, PA_INIT, tp);
     int k0 = 0, k1 = 0;
@@ -569,8 +590,10 @@ __device__ __forceinline__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, 
       const int na = E.hdr[0];
       const lds_u16* al = E.hdr[2] ? E.al_other : E.al;
       lds_u8* tf = (lds_u8*)(E.hdr[2] ? E.al : E.al_other);
-      const int chunk = (na + NTHREADS - 1) / NTHREADS;
-      const int i0 = min(na, (int)threadIdx.x * chunk), i1 = min(na, i0 + chunk);
+      // (the changed layers' range of the list; a skipped layer keeps its forest flags)
+      const int ra = ch0 ? 0 : na0, rb = ch1 ? na : na0;
+      const int chunk = (rb - ra + NTHREADS - 1) / NTHREADS;
+      const int i0 = min(rb, ra + (int)threadIdx.x * chunk), i1 = min(rb, i0 + chunk);
 #ifdef MD_UNION_PIPE
       // diagnostic variant (timing perturbation only): the next entry's id, state and endpoints
       // loaded one step ahead
@@ -636,9 +659,10 @@ __device__ __forceinline__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, 
     tp = wall_clock64();
     int diff = 0, nr0 = 0, nr1 = 0;
     for (int x = threadIdx.x; x < n; x += NTHREADS) {
-      const int r0 = uf_find(E.par0, x), r1 = uf_find(E.par1, x);
-      uf_store(E.deg0, x, r0);
-      uf_store(E.deg1, x, r1);
+      const int r0 = ch0 ? uf_find(E.par0, x) : uf_load(E.deg0, x);
+      const int r1 = ch1 ? uf_find(E.par1, x) : uf_load(E.deg1, x);
+      if (ch0) uf_store(E.deg0, x, r0);
+      if (ch1) uf_store(E.deg1, x, r1);
       diff |= (r0 != r1);
       nr0 += r0 == x;  // components per layer (their roots)
       nr1 += r1 == x;
@@ -682,7 +706,9 @@ __device__ __forceinline__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, 
       const int na = E.hdr[0];
       const lds_u16* al = E.hdr[2] ? E.al_other : E.al;
       const lds_u8* tf = (const lds_u8*)(E.hdr[2] ? E.al : E.al_other);
-      for (int i = threadIdx.x; i < na; i += NTHREADS) {
+      // (layer-0 edges only when layer 1's labels were redone this round, and vice versa)
+      const int ra = ch1 ? 0 : na0, rb = ch0 ? na : na0;
+      for (int i = ra + (int)threadIdx.x; i < rb; i += NTHREADS) {
         const int e = al[i];
         if (E.st[e] != E_ALIVE) continue;
         const int u = (int)E.u16[e], v = (int)E.v16[e];
@@ -706,6 +732,10 @@ __device__ __forceinline__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, 
     pruned0 += c.x;
     pruned1 += c.y;
     dirty = true;
+    if (lskip) {
+      ch0 = c.x > 0;
+      ch1 = c.y > 0;
+    }
     PACC(acc, PA_PRUNE, tp);
     if constexpr (!GL) {
       // confirmation shortcut (see above): #C0 + t0 == #C1 + t1 is necessary; then count the
@@ -733,6 +763,7 @@ __device__ __forceinline__ int mcc_fixed_point(const EnvView<GL>& Ein, int* pr, 
           compact_alive<GL>(E);
           break;
         }
+        ch1 = true;  // (its labels hold table slots now; layer 0 keeps its labels in deg0)
         __syncthreads();  // (the next round's init overwrites the table)
       }
     }

@@ -725,17 +725,20 @@ def test_dataflow_mode_same_rollouts(monkeypatch, cost):
 
 
 def test_fixed_point_shortcut_same_rollouts(monkeypatch):
-    """MD_FP_SHORTCUT=0 (every mutual-LMCC fixed point runs its confirmation round) gives the
-    removal sequences and LMCC traces of the default shortcut (tests/test_fixed_point_shortcut.py
-    checks the certificate itself on the CPU): single-graph launches (phase A, speculative
-    workgroups, dataflow mode) and a 24-graph queue-mode launch (environment items)."""
+    """MD_FP_SHORTCUT=0 (every mutual-LMCC fixed point runs its confirmation round) and
+    MD_FP_SKIP=0 (every round re-unites both layers, also those the last prune left unchanged)
+    give the removal sequences and LMCC traces of the defaults, alone and together
+    (tests/test_fixed_point_shortcut.py checks the certificate itself on the CPU): single-graph
+    launches (phase A, speculative workgroups, dataflow mode) and a 24-graph queue-mode launch
+    (environment items)."""
     from mdcommunity_amd import gmm
     w = engine.load_weights(engine.DEFAULT_UNIT)
     singles = [load_golden(k) for k in ("gmm200_s7", "er100", "gmm1000_s0", "er300_dense")]
     batch = [(1000,) + gmm.gmm_pair(1000, seed=s) for s in range(24)]
     out = {}
-    for fs in ("0", "1"):
-        monkeypatch.setenv("MD_FP_SHORTCUT", fs)
+    for fs in ("00", "01", "10", "11"):
+        monkeypatch.setenv("MD_FP_SHORTCUT", fs[0])
+        monkeypatch.setenv("MD_FP_SKIP", fs[1])
         e = _lib.Engine(w)
         res = []
         for z in singles:
@@ -748,7 +751,7 @@ def test_fixed_point_shortcut_same_rollouts(monkeypatch):
         res += [(s.tolist(), r.tolist()) for s, r in e.rollout()]
         e.close()
         out[fs] = res
-    assert out["0"] == out["1"]
+    assert out["00"] == out["11"] and out["01"] == out["11"] and out["10"] == out["11"]
 
 
 def test_deferred_reset_same_rollouts():
