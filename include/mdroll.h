@@ -277,9 +277,11 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *   MD_FP_SHORTCUT    0: every mutual-LMCC fixed point runs its confirmation round (default 1:
  *                     a pruned partition certified by its spanning forests ends the fixed point;
  *                     test_fixed_point_shortcut_same_rollouts)
- *   MD_FP_SKIP        0: every round of an LDS-resident mutual-LMCC fixed point re-unites both
- *                     layers (default 1: a layer the last prune left unchanged keeps its
- *                     components and labels; test_fixed_point_shortcut_same_rollouts)
+ *   MD_FP_SKIP        0: every round of a mutual-LMCC fixed point re-unites both layers
+ *                     (default 1: a layer the last prune left unchanged keeps its components
+ *                     and labels -- the LDS-resident and the grid-wide fixed point;
+ *                     test_fixed_point_shortcut_same_rollouts, and the grid-wide step's
+ *                     certified N = 18 000 sequences)
  *   MD_FIRST_REQ      0: no speculative request at a rollout's first environment step (default
  *                     1: candidates ranked by residual degree, as no prediction exists yet;
  *                     test_first_request_same_rollouts)

@@ -1923,8 +1923,15 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
   }
   // (node passes likewise: the thread's first node's class test)
   const bool x1in = T.gt < n && (!rs || uf_load(cls, T.gt) == La);
+  // Unchanged layers (MD_FP_SKIP, as in mcc_fixed_point): a pass that pruned no edge of layer
+  // 1 - l left layer 1 - l's partition as it was, so the next pass has no layer-l edge to prune
+  // (the pass before pruned every one crossing it) and layer l's union would rebuild its last
+  // labels: that pass skips layer l's edges and the label pass its finds.  (From the third
+  // pass on: the first prunes nothing.)  cq0 / cq1: the last pass's pruned counts per layer.
+  long long cq0 = -1, cq1 = -1;
   for (int round = 0;; ++round) {
     const bool first = round == 0;
+    const bool sk0 = p.fp_skip && round >= 2 && cq1 == 0, sk1 = p.fp_skip && round >= 2 && cq0 == 0;
     int* const P0 = pb[round & 1][0];
     int* const P1 = pb[round & 1][1];
     long long k0 = 0, k1 = 0, c0 = 0, c1 = 0;
@@ -1934,6 +1941,7 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
     for (int e = T.gt; e < et; e += T.gs) {
       const bool own = e == T.gt;
       if (own ? !a1 : E.state(e) != E_ALIVE) continue;
+      if (e < e0 ? sk0 : sk1) continue;  // (a skipped layer's edges stay alive and out of this pass)
       const int u = own ? u1 : E.u(e), v = own ? v1 : E.v(e);
       if (!own && rs && uf_load(cls, u) != La) continue;  // an edge of another class (both ends in it)
       if (own) a1 = false;  // (set again below when it stays alive)
@@ -2022,10 +2030,22 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
     const unsigned long long tl0 = T.prof_any != nullptr ? wall_clock64() : 0ull;
     for (int x = T.gt; x < n; x += T.gs) {
       if (x == T.gt ? !x1in : (rs && uf_load(cls, x) != La)) continue;  // labels of the untouched classes stay
-      const int2 rr = uf_find2_h(P0, P1, x);
-      const int r0 = rr.x, r1 = rr.y;
-      uf_store(E.deg0, x, r0);
-      uf_store(E.deg1, x, r1);
+      int r0, r1;
+      if (sk0) {
+        r0 = uf_load(E.deg0, x);
+        r1 = uf_find_h(P1, x);
+        uf_store(E.deg1, x, r1);
+      } else if (sk1) {
+        r0 = uf_find_h(P0, x);
+        r1 = uf_load(E.deg1, x);
+        uf_store(E.deg0, x, r0);
+      } else {
+        const int2 rr = uf_find2_h(P0, P1, x);
+        r0 = rr.x;
+        r1 = rr.y;
+        uf_store(E.deg0, x, r0);
+        uf_store(E.deg1, x, r1);
+      }
       uf_store(Q0, x, x);
       uf_store(Q1, x, x);
       diff += r0 != r1;
@@ -2045,6 +2065,8 @@ __device__ bool team_fixed_point(KParams& p, Team& T, const EnvView<true>& E, in
     }
     pr[0] += (int)t5[3];
     pr[1] += (int)t5[4];
+    cq0 = t5[3];
+    cq1 = t5[4];
     if (t5[0] == 0) break;
   }
   // the LMCC: non-covered nodes per component (layer-0 label = layer-1 label at the fixed point);
