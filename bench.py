@@ -44,7 +44,8 @@ PEAK_HBM_GBS = 8000.0      # MI355X HBM3E peak
 CKPT = "U/models/g0.5_TORCH-Model_GMM_30_50/nrange_30_50_iter_100000.ckpt"
 # sources whose hash ties a committed PMC traffic file to the kernels that ran
 KERNEL_SOURCES = ["mdcommunity_amd/csrc/md_kernels.hip", "mdcommunity_amd/csrc/md_env.h",
-                  "mdcommunity_amd/csrc/md_common.h", "mdcommunity_amd/csrc/md_abi.cpp"]
+                  "mdcommunity_amd/csrc/md_common.h", "mdcommunity_amd/csrc/md_abi.cpp",
+                  "mdcommunity_amd/csrc/md_wave.h"]
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 
 
