@@ -618,6 +618,8 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
     // a tag of an earlier launch that matches this one's
     p.launch_seq = ++c->launch_seq;
     if (c->sres.p) HIPCHK(c, hipMemsetAsync(c->sres.p, 0, sizeof(int) * c->sres.n, c->stream));
+    // the batch-speculation slots carry the same 16-bit launch tag
+    if (c->bspec.p) HIPCHK(c, hipMemsetAsync(c->bspec.p, 0, sizeof(int) * (size_t)(2 * c->bspec_half), c->stream));
   }
   p.run_mode = run_mode;
   p.host_select = host_select;
@@ -981,7 +983,9 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
       int* a = adj[l].data() + gi.coff[l];
       int* ax = adjx[l].data() + gi.coff[l];
       int* ep = epos[l].data() + 2 * (size_t)gi.eoff[l];
-      const bool packs = gi.e[l] <= 65536 && n <= 65536;
+      // packed words are read only for layer-local edge ids < 2^15 (env_build_lists tests x >= 0
+      // for liveness, and k = 65535, u = 65535 would pack to the -1 'not packed' marker)
+      const bool packs = gi.e[l] < ADJX_EDGE_LIMIT && n <= 65536;
       for (int k = 0; k < gi.e[l]; ++k) {
         const int u = eu[l][gi.eoff[l] + k], v = ev[l][gi.eoff[l] + k];
         ep[2 * k] = fill[v];
@@ -1065,7 +1069,8 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->tr_rank.alloc(tn));
   HIPCHK(c, c->tr_stat.alloc(4 * tn));
   HIPCHK(c, c->tr_q.alloc(2 * tn));
-  HIPCHK(c, c->q.alloc(tn));
+  // (+4: env_stage_wide stages the last graph's Q row as 16-byte unclipped buffer loads)
+  HIPCHK(c, c->q.alloc(tn + 4));
   HIPCHK(c, c->glist.alloc(n_graphs));
   HIPCHK(c, c->ctl.alloc(CTL_WORDS));
   if (c->tpart.p == nullptr) HIPCHK(c, c->tpart.alloc(2 * (size_t)TEAM_MAX_WG * 16));

@@ -85,13 +85,18 @@ struct GraphVar {            // mutable per-graph state
   int spec_hits;             // removals whose fixed point came from a speculative workgroup
 };
 
+// adjx packs a layer's CSR entries only below this many edges (positive words, never -1)
+constexpr int ADJX_EDGE_LIMIT = 32768;
+
 struct Params {
   const float* w;                  // packed weights (reference layout)
   const GraphInfo* ginfo;
   GraphVar* gvar;
   const int* rowptr[2];            // static CSR (neighbour order = reference in_edges order)
   const int* adj[2];
-  const int* adjx[2];              // per CSR entry: (layer-local edge id << 16) | neighbour (e_l, n < 2^16; else -1)
+  const int* adjx[2];              // per CSR entry: (layer-local edge id << 16) | neighbour, packed only
+                                   //   when e_l < ADJX_EDGE_LIMIT and n <= 2^16 (else -1): the word stays
+                                   //   >= 0, the reader's liveness test (env_build_lists)
   uint8_t* calive[2];              // per CSR entry: 1 while its edge is alive
   const int* epos[2];              // per undirected edge: its two CSR entry positions
   const int* eu[2];                // undirected endpoints (graph-local ids)

@@ -2684,8 +2684,8 @@ __device__ __forceinline__ bool env_build_lists(KParams&, const GraphInfo gi, in
   const EnvView<false> E = env_view<false>(p, gi, ia);
   const int nl = ((const GraphVar*)(lds + L_GV))->n_live, nt = (nl + TILE - 1) / TILE;
   // (the per-thread packed counts below need fewer than 2^16 CSR entries per layer)
-  if (Lo.total + 5 * nl + 2 * nt + 8 > A_WORDS || p.gtoff[gl] + nt > p.nbc_slots || nl <= 0 || gi.e[0] >= 32768 ||
-      gi.e[1] >= 32768 || n > 65536)
+  if (Lo.total + 5 * nl + 2 * nt + 8 > A_WORDS || p.gtoff[gl] + nt > p.nbc_slots || nl <= 0 || gi.e[0] >= ADJX_EDGE_LIMIT ||
+      gi.e[1] >= ADJX_EDGE_LIMIT || n > 65536)
     return false;
   // scratch after the environment: node of each live position, per layer the per-position
   // prefixes of the CSR extent and of the alive count (nl + 1 each), per-tile alive totals

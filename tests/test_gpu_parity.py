@@ -497,6 +497,51 @@ def test_grid_wide_incremental_steps_random(monkeypatch):
         e.close()
 
 
+@pytest.mark.timeout(300)
+def test_grid_wide_two_graphs_alternating(monkeypatch):
+    """Two loaded graphs share the grid-wide step's scratch (gscr_team: class labels and sizes);
+    a step of one graph must drop the labels the other's steps left there (team_owner / lab_ok,
+    md_abi.cpp).  md_step alternates between gmm1000_s0 and gmm1000_s2 in the grid-wide mode
+    (each launch runs one graph), against one oracle environment per graph: LMCC, covered set
+    and edge counters after every call."""
+    from oracle import refenv
+    monkeypatch.setenv("MD_ENV_MODE", "0")
+    monkeypatch.setenv("MD_VARIANT", "64")
+    names = ("gmm1000_s0", "gmm1000_s2")
+    zs = [load_golden(nm) for nm in names]
+    gs = [refenv.RefGraph(int(z["n_nodes"]), z["edges0"], z["edges1"]) for z in zs]
+    envs = [refenv.RefEnv(g, "unit") for g in gs]
+    e = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
+    try:
+        e.load_graphs([(int(z["n_nodes"]), z["edges0"], z["edges1"]) for z in zs])
+        assert [int(x) for x in e.reset()] == [g.max_rank for g in gs]
+        rng = np.random.default_rng(5)
+        done = [False, False]
+        for it in range(40):
+            k = it % 2
+            if done[k]:
+                continue
+            live = refenv.featurize(gs[k], envs[k].covered, envs[k].removed)[0]
+            if not live:
+                done[k] = True
+                continue
+            a = int(rng.choice(np.asarray(live, np.int64)))
+            acts = np.full(2, -1, np.int32)
+            acts[k] = a
+            lm, term = e.step(acts)
+            r = envs[k].step(a)
+            assert int(lm[k]) == r, (it, k, a)
+            cov, _, _, cnt = e.get_state(k)
+            assert set(np.flatnonzero(cov).tolist()) == envs[k].covered, (it, k)
+            assert [int(cnt[0]), int(cnt[1])] == envs[k].num_covered, (it, k)
+            assert [int(cnt[2]), int(cnt[3])] == [len(envs[k].removed[0]) // 2, len(envs[k].removed[1]) // 2], (it, k)
+            if bool(term[k]) or envs[k].terminal():
+                assert bool(term[k]) == envs[k].terminal()
+                done[k] = True
+    finally:
+        e.close()
+
+
 def test_iteration1_prebuild_same_rollouts(monkeypatch):
     """Single-graph rollouts build iteration 1 (rows, alive-neighbour lists, and the whole
     first message-passing iteration) during phase A from the speculative result phase A
