@@ -282,6 +282,10 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *                     and labels -- the LDS-resident and the grid-wide fixed point;
  *                     test_fixed_point_shortcut_same_rollouts, and the grid-wide step's
  *                     certified N = 18 000 sequences)
+ *   MD_PREFIX         k: the grid-wide environment step applies a prediction's picks
+ *                     (stepRatio > 0) as independent prefix fixed points, one per workgroup,
+ *                     while at least k remain (default 8; 0: one cascade after another;
+ *                     test_gpu_prefix.py, and the certified N = 18 000 stepRatio sequence)
  *   MD_FIRST_REQ      0: no speculative request at a rollout's first environment step (default
  *                     1: candidates ranked by residual degree, as no prediction exists yet;
  *                     test_first_request_same_rollouts)

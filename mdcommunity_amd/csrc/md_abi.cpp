@@ -26,6 +26,8 @@ int lds_bytes();
 int weight_image_floats();
 bool phase_a_fits_lds_host(int n, int edges);
 bool spec_fits_lds_host(int n, int edges);
+bool pfx_fits_host(int n, int edges);
+long long pfx_words_host(int edges);
 void build_weight_image(const float* w, float* img);
 hipError_t launch_rollout(const Params& p, const float* wimg, int grid, hipStream_t s);
 hipError_t launch_h0(const float* w, float* tab, int dm_lo, int dm_hi, hipStream_t s);
@@ -180,6 +182,8 @@ struct md_ctx {
   bool abort_on = true;
   bool fp_short = true;  // MD_FP_SHORTCUT=0: every fixed point runs its confirmation round
   bool fp_skip = true;   // MD_FP_SKIP=0: every LDS fixed-point round re-unites both layers
+  int pfx_min = 8;       // MD_PREFIX: grid-wide steps take >= this many actions as batched prefixes (0: off)
+  DevBuf<int> pfx;       // their scratch (md_env.h pfx_words)
   bool first_req = true;  // MD_FIRST_REQ=0: no speculative request at a rollout's first step
   DevBuf<unsigned long long> dfbuf;
   int df_mt = 0, df_n = 0;
@@ -207,7 +211,7 @@ struct md_ctx {
       H[l][0].release(); H[l][1].release();
     }
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
-    tr_stat.release(); glist.release(); gtoff.release(); ctl.release(); tpart.release(); lab_ok.release(); gscr_team.release(); bspec.release(); prank.release(); q.release(); spart.release();
+    tr_stat.release(); glist.release(); gtoff.release(); ctl.release(); tpart.release(); lab_ok.release(); gscr_team.release(); pfx.release(); bspec.release(); prank.release(); q.release(); spart.release();
     apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); nbc.release(); qslot.release(); qg.release(); tr_q.release(); node_w.release();
     sres.release(); qspec.release(); bars.release(); dfbuf.release();
     df_graph.clear();
@@ -247,6 +251,8 @@ Params make_params(md_ctx* c) {
   Params p{};
   p.fp_short = c->fp_short ? 1 : 0;
   p.fp_skip = c->fp_skip ? 1 : 0;
+  p.pfx = c->pfx_min > 0 ? c->pfx.p : nullptr;
+  p.pfx_min = c->pfx_min;
   p.first_req = c->first_req ? 1 : 0;
   p.w = c->w.p;
   p.ginfo = c->ginfo.p;
@@ -814,6 +820,7 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_SPEC_ABORT")) c->abort_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_FP_SHORTCUT")) c->fp_short = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_FP_SKIP")) c->fp_skip = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MD_PREFIX")) c->pfx_min = std::max(0, std::atoi(v));
   if (const char* v = std::getenv("MD_FIRST_REQ")) c->first_req = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_DF")) c->df_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_SPEC")) c->spec_n = std::max(0, std::min(SPEC_MAX, std::atoi(v)));
@@ -1079,6 +1086,14 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
     int max_n = 1;
     for (int g = 0; g < n_graphs; ++g) max_n = std::max(max_n, (int)n_nodes[g]);
     HIPCHK(c, c->gscr_team.alloc((size_t)GSCR_TEAM_WORDS * max_n));
+    // batched-prefix scratch, sized by the largest graph that can take the prefix path
+    int max_et = 0;
+    for (int g = 0; g < n_graphs; ++g) {
+      const int et = (int)(c->hinfo[g].e[0] + c->hinfo[g].e[1]);
+      if (pfx_fits_host(c->hinfo[g].n, et)) max_et = std::max(max_et, et);
+    }
+    c->pfx.release();
+    if (c->pfx_min > 0 && max_et > 0) HIPCHK(c, c->pfx.alloc((size_t)pfx_words_host(max_et)));
     c->team_owner = -1;
   }
   // speculative environment-step slots of queue launches (bspec_slot): per graph and removal-count

@@ -204,6 +204,10 @@ struct Params {
   int fp_short;                    // 1: mutual-LMCC fixed points end by the confirmation shortcut (mcc_fixed_point)
   int fp_skip;                     // 1: LDS fixed-point rounds skip the layers the last prune left unchanged
   int first_req;                   // 1: a rollout's first step requests degree-ranked speculative results (env_step)
+  // batched prefixes (md_env.h team_prefix_step): the grid-wide step applies a prediction's
+  // actions as independent prefix fixed points, one per workgroup, when at least pfx_min remain
+  int* pfx;                        // scratch, pfx_words(largest et) ints; null: off
+  int pfx_min;                     // MD_PREFIX (0: off)
 };
 // global-mode environment scratch words per node (md_env.h env_view: parents, degrees) and the
 // grid-wide step's own words per node of the graph it runs (team_env_step, one graph per launch)

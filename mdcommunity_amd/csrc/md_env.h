@@ -2165,11 +2165,367 @@ __device__ bool team_features(KParams& p, Team& T, const EnvView<true>& E, int n
   return false;
 }
 
+// ------------------------------------------------------------------ batched prefixes (stepRatio)
+// A prediction with stepRatio > 0 applies k picks a_1..a_k one by one, each followed by the
+// mutual-LMCC cascade (U/MultiDismantler_torch.py:725-735, U/mvc_env.py:74-87, U/Mcc.py:30-38):
+// k dependent grid-wide fixed points.  But the state after a_1..a_j has the same alive edges,
+// partition and LMCC as ONE cascade of the prediction's start state with all of a_1..a_j covered
+// (the fixed point is the coarsest partition whose classes are connected in both layers by
+// edges inside them; the partitions only refine as nodes go, so an edge pruned earlier crosses
+// every later partition: tests/test_prefix_states.py checks it on the oracle).  So the k
+// prefixes are independent: workgroup j - 1 computes prefix j's fixed point in its own LDS, all
+// at once, from the start state's alive edges (a compact list in HBM, read from L2 by every
+// workgroup), and publishes its LMCC, alive counts and alive bitmap; then every alive edge's
+// death step d(e) -- the first prefix without it (the bitmaps are nested) -- decides its fate:
+// covered when it touches a_d(e) (numCoveredEdges, U/mvc_env.py:81-84), pruned otherwise
+// (remove_edge).  The picks stop at the first terminal prefix (GetSolution's `continue`).
+// pfx (HBM, md_abi.cpp): [0, et) compact start list u | v << 16, [et, 2 et) its edge ids,
+// [2 et, + 4 TEAM_MAX_WG) per-prefix records {lmcc, alive 0, alive 1, -}, then per prefix the
+// alive bitmap of the compact list (pfx_bw words).
+__host__ __device__ inline int pfx_bw(int et) { return (et + 31) >> 5; }
+__host__ __device__ inline long long pfx_words(int et) { return 2LL * et + 4LL * TEAM_MAX_WG + (long long)TEAM_MAX_WG * pfx_bw(et); }
+// LDS words of one prefix's fixed point: u16 parents of both layers, the prefix's cover bitmap,
+// the alive bitmap of the compact list, reduction words
+__host__ __device__ inline int pfx_lds_words(int n, int et) { return 2 * ((n + 1) >> 1) + ((n + 31) >> 5) + pfx_bw(et) + 64; }
+__host__ __device__ inline bool pfx_fits(int n, int et) { return n <= 65535 && pfx_lds_words(n, et) <= A_WORDS; }
+
+// u16 union-find in LDS (two parents per word; parents point to smaller ids, so a tree's root is
+// its least node): 16-bit loads and path-halving stores, the hook a 32-bit compare-and-swap of
+// the word holding the root (a change of the other half fails it, and it is retried on the new
+// word: the root's own half decides)
+__device__ __forceinline__ int p16_ld(lds_u16* P, int i) {
+  return __hip_atomic_load(P + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void p16_st(lds_u16* P, int i, int v) {
+  __hip_atomic_store(P + i, (uint16_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool p16_hook(lds_u16* P, int r, int to) {
+  lds_u32* w = (lds_u32*)(P) + (r >> 1);
+  const int sh = (r & 1) << 4;
+  unsigned old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (true) {
+    if (((old >> sh) & 0xffffu) != (unsigned)r) return false;
+    const unsigned nw = (old & ~(0xffffu << sh)) | ((unsigned)to << sh);
+    unsigned ex = old;
+    if (__hip_atomic_compare_exchange_strong(w, &ex, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+      return true;
+    old = ex;
+  }
+}
+__device__ __forceinline__ int p16_find(lds_u16* P, int v) {
+  int cur = p16_ld(P, v);
+  if (cur != v) {
+    int prev = v, next;
+    while (cur > (next = p16_ld(P, cur))) {
+      p16_st(P, prev, next);  // path halving; benign race (values only shrink)
+      prev = cur;
+      cur = next;
+    }
+  }
+  return cur;
+}
+// a root without path stores (the label pass: a halving store could replace a root another
+// thread just stored as x's label with an older ancestor)
+__device__ __forceinline__ int p16_root(lds_u16* P, int v) {
+  int next;
+  while ((next = p16_ld(P, v)) != v) v = next;
+  return v;
+}
+__device__ __forceinline__ void p16_unite(lds_u16* P, int a, int b) {
+  while (true) {
+    a = p16_find(P, a);
+    b = p16_find(P, b);
+    if (a == b) return;
+    if (a > b) { const int t = a; a = b; b = t; }
+    if (p16_hook(P, b, a)) return;
+  }
+}
+
+// The next kc actions (from index k0) of graph E.gi as batched prefixes.  Returns -1 on a grid
+// error, 0 when the batch cannot take this path (an action out of range, covered or repeated: the
+// sequential loop applies the actions before it and reports it, as the reference's assert would),
+// else 1 with *J the actions applied (fewer than kc when a prefix is terminal), cnt the covered /
+// pruned edges per layer {c0, c1, pr0, pr1}, and workgroup 0's books (covered flags, trace,
+// GraphVar counters) updated.  Uses the LDS from L_W on (the caller reloads the weight image).
+__device__ __forceinline__ int pfx_act(KParams& p, const GraphInfo& gi, int k, int pend_first) {
+  return k == 0 && pend_first >= 0 ? pend_first : __hip_atomic_load(p.pend + gi.node_off + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __noinline__ int team_prefix_step(KParams& p, Team& T, const EnvView<true>& E, int k0, int kc, int pend_first, bool books,
+                                int* Jout, int (&cnt)[4]) {
+  const GraphInfo& gi = *E.gi;
+  const int n = gi.n, et = E.et, e0 = E.e0;
+  const int lane = lane_id(), wv = wave_id();
+  int* const puv = p.pfx;
+  int* const pe = p.pfx + et;
+  int* const rec = p.pfx + 2 * et;
+  int* const dbm = p.pfx + 2 * et + 4 * TEAM_MAX_WG;
+  const int bw = pfx_bw(et);
+  // diagnostics (md_profile, scripts/prefix_prof.py): slots 80.. of the step -- 80 most rounds of
+  // any prefix, 81 list + validation (workgroup 0), 82 the slowest prefix's fixed point, 83 death
+  // steps + reduction (workgroup 0), and the last prefix's pieces: 84 init + alive bits, 86 union,
+  // 88 labels, 89 prune, 90 LMCC + stores, 91 its rounds; 92 prefixes, 93 applied
+  unsigned long long* const pa = T.prof_any;
+  unsigned long long tp0 = pa != nullptr ? wall_clock64() : 0ull, tp1 = tp0;
+  // ---- the compact list of the start state's alive edges, in edge order (layer 0 first): each
+  // workgroup a contiguous edge range, each thread a contiguous part of it
+  const int cw = (et + p.n_main - 1) / p.n_main;
+  const int w0 = min(et, (int)blockIdx.x * cw), w1 = min(et, w0 + cw);
+  const int ct = (w1 - w0 + NTHREADS - 1) / NTHREADS;
+  const int x0 = min(w1, w0 + (int)threadIdx.x * ct), x1 = min(w1, x0 + ct);
+  long long na = 0, na0 = 0;
+  for (int e = x0; e < x1; ++e) {
+    const bool a = E.state(e) == E_ALIVE;
+    na += a;
+    na0 += a && e < e0;
+  }
+  int wtot = 0;
+  const int off = block_excl_scan((int)na, T.tmp, &wtot);
+  const long long v2[2] = {na, na0};
+  long long t2[2], before = 0;
+  if (team_reduce<2>(p, T, v2, 0u, t2, &before)) return -1;
+  const int mc = (int)t2[0], mc0 = (int)t2[1];
+  {
+    int k = (int)before + off;
+    for (int e = x0; e < x1; ++e) {
+      if (E.state(e) != E_ALIVE) continue;
+      stc(puv + k, E.u(e) | (E.v(e) << 16));
+      stc(pe + k, e);
+      ++k;
+    }
+  }
+  // ---- LDS (from L_W): P0, P1 (u16), cover bitmap of the prefix, alive bitmap of the list
+  const int h = (n + 1) >> 1, nb = (n + 31) >> 5, ab = (mc + 31) >> 5;
+  lds_u32* const R = (lds_u32*)(unsigned*)(lds_base() + L_W);
+  lds_u16* const P0 = (lds_u16*)(R);
+  lds_u16* const P1 = (lds_u16*)(R + h);
+  lds_u32* const cb = R + 2 * h;
+  lds_u32* const abm = cb + nb;
+  int* const tmp = (int*)(lds_base() + L_W) + 2 * h + nb + ab;
+  // validation (every workgroup, same verdict): range, not covered, no repeats
+  for (int i = threadIdx.x; i < nb; i += NTHREADS) cb[i] = 0u;
+  __syncthreads();
+  bool bad = false;
+  for (int k = threadIdx.x; k < kc; k += NTHREADS) {
+    const int a = pfx_act(p, gi, k0 + k, pend_first);
+    if (a < 0 || a >= n || E.covered(a)) {
+      bad = true;
+    } else {
+      const unsigned m = 1u << (a & 31);
+      if (__hip_atomic_fetch_or(cb + (a >> 5), m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & m) bad = true;
+    }
+  }
+  bad = __syncthreads_or(bad);
+  // (the list's stores must be visible before anyone reads it: every path below crosses a barrier)
+  if (grid_sync(p, *T.target, T.flag)) return -1;
+  if (bad) return 0;
+  const int j = (int)blockIdx.x + 1;  // this workgroup's prefix
+  const bool plast = pa != nullptr && j == kc && threadIdx.x == 0;
+  if (pa != nullptr && blockIdx.x == 0 && threadIdx.x == 0) pa[1] = wall_clock64() - tp0;
+  if (pa != nullptr) tp0 = tp1 = wall_clock64();
+  auto lap = [&](int k) {  // the last prefix's piece k (diagnostics)
+    if (plast) {
+      const unsigned long long t = wall_clock64();
+      pa[k] += t - tp1;
+      tp1 = t;
+    }
+  };
+  if (j <= kc) {
+    for (int i = threadIdx.x; i < nb; i += NTHREADS) cb[i] = 0u;
+    for (int x = threadIdx.x; x < n; x += NTHREADS) {
+      p16_st(P0, x, x);
+      p16_st(P1, x, x);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < j; k += NTHREADS) {
+      const int a = pfx_act(p, gi, k0 + k, pend_first);
+      __hip_atomic_fetch_or(cb + (a >> 5), 1u << (a & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    // alive bits: the start's alive edges without the prefix's covered nodes (a wave's 64 entries
+    // per ballot)
+    for (int ib = wv * 64; ib < mc; ib += NTHREADS) {
+      const int i = ib + lane;
+      bool al = false;
+      if (i < mc) {
+        const unsigned uv = (unsigned)ldc(puv + i);
+        const int u = (int)(uv & 0xffffu), v = (int)(uv >> 16);
+        al = !((cb[u >> 5] >> (u & 31)) & 1u) && !((cb[v >> 5] >> (v & 31)) & 1u);
+      }
+      const unsigned long long m = __ballot(al);
+      if (lane == 0) abm[ib >> 5] = (unsigned)m;
+      if (lane == 1 && (ib >> 5) + 1 < ab) abm[(ib >> 5) + 1] = (unsigned)(m >> 32);
+    }
+    __syncthreads();
+    lap(4);
+    // Jacobi rounds (mcc_fixed_point's): union both layers, label, prune each layer's edges by
+    // the other layer's labels; a layer that lost no edge keeps its labels (no reset, union or
+    // relabel); no edge pruned = the partitions agree = the fixed point
+    bool ch0 = true, ch1 = true;
+    const int cr = (mc + NTHREADS - 1) / NTHREADS;
+    const int r0 = min(mc, (int)threadIdx.x * cr), r1 = min(mc, r0 + cr);
+    for (int round = 0;; ++round) {
+      if (round > 0) {
+        for (int x = threadIdx.x; x < n; x += NTHREADS) {
+          if (ch0) p16_st(P0, x, x);
+          if (ch1) p16_st(P1, x, x);
+        }
+        __syncthreads();
+      }
+      // union: a contiguous run of the list per thread (consecutive edges share endpoints)
+      {
+        const int ia = ch0 ? r0 : max(r0, mc0), ib = ch1 ? r1 : min(r1, mc0);
+        unsigned nxt = ia < ib ? (unsigned)ldc(puv + ia) : 0u;
+        for (int i = ia; i < ib; ++i) {
+          const unsigned uv = nxt;
+          if (i + 1 < ib) nxt = (unsigned)ldc(puv + i + 1);  // one entry ahead
+          if (!((abm[i >> 5] >> (i & 31)) & 1u)) continue;
+          p16_unite(i < mc0 ? P0 : P1, (int)(uv & 0xffffu), (int)(uv >> 16));
+        }
+      }
+      __syncthreads();
+      lap(6);
+      // labels: every node's root, stored as its parent
+      for (int x = threadIdx.x; x < n; x += NTHREADS) {
+        if (ch0) p16_st(P0, x, p16_root(P0, x));
+        if (ch1) p16_st(P1, x, p16_root(P1, x));
+      }
+      __syncthreads();
+      lap(8);
+      // prune (coalesced: entries strided over the block)
+      int c0 = 0, c1 = 0;
+      for (int i = threadIdx.x; i < mc; i += NTHREADS) {
+        if (!((abm[i >> 5] >> (i & 31)) & 1u)) continue;
+        const unsigned uv = (unsigned)ldc(puv + i);
+        const int u = (int)(uv & 0xffffu), v = (int)(uv >> 16);
+        lds_u16* const other = i < mc0 ? P1 : P0;  // layer-0 edges by the layer-1 labels
+        if (p16_ld(other, u) != p16_ld(other, v)) {
+          __hip_atomic_fetch_and(abm + (i >> 5), ~(1u << (i & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (i < mc0) c0++; else c1++;
+        }
+      }
+      const int2 cs = block_sum2(c0, c1, tmp);
+      __syncthreads();
+      lap(9);
+      if (plast) pa[11] += 1;
+      if (pa != nullptr && threadIdx.x == 0)
+        __hip_atomic_fetch_max(pa, (unsigned long long)(round + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cs.x == 0 && cs.y == 0) break;
+      ch0 = cs.x > 0;
+      ch1 = cs.y > 0;
+    }
+    // LMCC: non-covered nodes per layer-0 label, counted in P1's words (two u16 counts each)
+    for (int i = threadIdx.x; i < h; i += NTHREADS) R[h + i] = 0u;
+    __syncthreads();
+    for (int x = threadIdx.x; x < n; x += NTHREADS) {
+      if ((cb[x >> 5] >> (x & 31)) & 1u) continue;
+      if (E.covered(x)) continue;
+      const int r = p16_ld(P0, x);
+      __hip_atomic_fetch_add(R + h + (r >> 1), 1u << ((r & 1) << 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    int best = 0, al0 = 0, al1 = 0;
+    for (int i = threadIdx.x; i < h; i += NTHREADS) {
+      const unsigned w = R[h + i];
+      best = max(best, (int)max(w & 0xffffu, w >> 16));
+    }
+    for (int i = threadIdx.x; i < ab; i += NTHREADS) {
+      const unsigned w = abm[i];
+      stc(dbm + (size_t)(j - 1) * bw + i, (int)w);
+      // bits of entries [32 i, 32 i + 32): layer 0 below mc0
+      const int lo = 32 * i;
+      const unsigned m0 = mc0 <= lo ? 0u : (mc0 >= lo + 32 ? ~0u : ((1u << (mc0 - lo)) - 1u));
+      al0 += __popc(w & m0);
+      al1 += __popc(w & ~m0);
+    }
+    best = block_max_int(best, tmp);
+    const int2 al = block_sum2(al0, al1, tmp);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      stc(rec + 4 * (j - 1), best);
+      stc(rec + 4 * (j - 1) + 1, al.x);
+      stc(rec + 4 * (j - 1) + 2, al.y);
+    }
+    lap(10);
+    if (pa != nullptr && threadIdx.x == 0)
+      __hip_atomic_fetch_max(pa + 2, wall_clock64() - tp0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (grid_sync(p, *T.target, T.flag)) return -1;
+  if (pa != nullptr) tp0 = wall_clock64();
+  // ---- the applied prefix: the first terminal one, else kc (every workgroup, same answer)
+  int jt = kc;
+  for (int q = threadIdx.x; q < kc; q += NTHREADS) {
+    if (ldc(rec + 4 * q + 1) == 0 || ldc(rec + 4 * q + 2) == 0) {
+      jt = q + 1;
+      break;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) jt = min(jt, __shfl_xor(jt, o, 64));
+  int* const ltmp = T.tmp;
+  if (lane == 0) ltmp[wv] = jt;
+  __syncthreads();
+  int J = ltmp[0];
+#pragma unroll
+  for (int q = 1; q < NTHREADS / 64; ++q) J = min(J, ltmp[q]);
+  __syncthreads();
+  // ---- each start edge's death step (the bitmaps are nested: binary search over 1..J)
+  long long c0 = 0, c1 = 0, q0 = 0, q1 = 0;
+  for (int i = T.gt; i < mc; i += T.gs) {
+    const unsigned m = 1u << (i & 31);
+    if ((unsigned)ldc(dbm + (size_t)(J - 1) * bw + (i >> 5)) & m) continue;  // alive after the batch
+    int lo = 1, hi = J;  // first prefix without the edge
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if ((unsigned)ldc(dbm + (size_t)(mid - 1) * bw + (i >> 5)) & m) lo = mid + 1; else hi = mid;
+    }
+    const int a = pfx_act(p, gi, k0 + lo - 1, pend_first);
+    const unsigned uv = (unsigned)ldc(puv + i);
+    const bool cov = (int)(uv & 0xffffu) == a || (int)(uv >> 16) == a;
+    E.kill(ldc(pe + i), cov ? E_COVERED : E_PRUNED);
+    if (i < mc0) { if (cov) c0++; else q0++; } else { if (cov) c1++; else q1++; }
+  }
+  const long long v4[4] = {c0, c1, q0, q1};
+  long long t4[4];
+  if (team_reduce<4>(p, T, v4, 0u, t4, nullptr)) return -1;
+  for (int k = 0; k < 4; ++k) cnt[k] = (int)t4[k];
+  if (pa != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+    pa[3] = wall_clock64() - tp0;
+    pa[12] = (unsigned long long)kc;
+    pa[13] = (unsigned long long)J;
+  }
+  if (books) {
+    GraphVar& gv = *(GraphVar*)(lds_base() + L_GV);
+    const int st0 = gv.steps;
+    for (int q = threadIdx.x; q < J; q += NTHREADS) {
+      const int a = pfx_act(p, gi, k0 + q, pend_first);
+      stc(E.gcov + a, (uint8_t)1);
+      if (MD_BOK(st0 + q < gi.n, 8)) {
+        p.tr_action[gi.node_off + st0 + q] = a;
+        p.tr_rank[gi.node_off + st0 + q] = ldc(rec + 4 * q);
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      gv.counter[0] += cnt[0];
+      gv.counter[1] += cnt[1];
+      gv.removed[0] += cnt[2];
+      gv.removed[1] += cnt[3];
+      gv.alive[0] -= cnt[0] + cnt[2];
+      gv.alive[1] -= cnt[1] + cnt[3];
+      gv.n_cov += J;
+      gv.lmcc = ldc(rec + 4 * (J - 1));
+      gv.steps += J;
+    }
+    __syncthreads();
+  }
+  *Jout = J;
+  return 1;
+}
+
 // The environment step of graph g on every workgroup of the launch (env_step's work once the
 // actions are known): workgroup 0 holds the graph's GraphVar in LDS and keeps its books (the
 // others read the counts they need from the partials); pend_n actions, the first pend_first
 // (or p.pend[0] when < 0).  Returns an ERR_* code (0: ok) in *err; true on a grid error.
-__device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_first, int* err) {
+__device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_first, int* err, bool* wdirty) {
   const GraphInfo gi = p.ginfo[g];
   const int n = gi.n;
   GraphVar& gv = *(GraphVar*)(lds_base() + L_GV);
@@ -2201,7 +2557,34 @@ __device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_f
     rk = dst;
   }
   *err = 0;
-  for (int k = 0; k < pend_n; ++k) {
+  // batched prefixes (stepRatio): chunks of up to n_main actions at once while at least
+  // pfx_min remain (team_prefix_step); an invalid action leaves them to the loop below
+  int k0 = 0;
+  *wdirty = false;
+  while (p.pfx != nullptr && p.pfx_min > 0 && s0_done && pend_n - k0 >= p.pfx_min && alive0 > 0 && alive1 > 0 &&
+         pfx_fits(n, E.et)) {
+    const int kc = min(pend_n - k0, p.n_main);
+    int J = 0, cnt[4];
+    *wdirty = true;  // (the LDS from L_W on, even when the batch is refused)
+    const int r = team_prefix_step(p, T, E, k0, kc, pend_first, books, &J, cnt);
+    if (r < 0) return true;
+    if (r == 0) break;
+    labels = false;  // (the class labels are the last fixed point's of the sequential loop)
+    alive0 -= cnt[0] + cnt[2];
+    alive1 -= cnt[1] + cnt[3];
+    k0 += J;
+    if (J < kc) {  // terminal
+      k0 = pend_n;
+      break;
+    }
+  }
+  if (*wdirty && rk != nullptr) {  // the static ranks again (their LDS was the prefixes')
+    lds_u16* dst = (lds_u16*)(uint16_t*)(lds_base() + L_SCR + TEAM_RANK_OFF);
+    const unsigned* src = (const unsigned*)(p.prank + gi.rank_off);
+    for (int i = threadIdx.x; i < ((n + 1) >> 1); i += NTHREADS) ((lds_u32*)(unsigned*)dst)[i] = src[i];
+    __syncthreads();
+  }
+  for (int k = k0; k < pend_n; ++k) {
     if (alive0 == 0 || alive1 == 0) break;  // terminal between queued actions
     const int a = k == 0 && pend_first >= 0 ? pend_first
                                             : __hip_atomic_load(p.pend + gi.node_off + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -4981,7 +4981,9 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
           if (threadIdx.x == 0) p.prof[(size_t)pstep * PROF_SLOTS + 87] = wall_clock64();
         }
         int terr = 0;
-        if (team_env_step(p, T, p.glist[0], pn, pf, &terr)) break;
+        bool wdirty = false;
+        if (team_env_step(p, T, p.glist[0], pn, pf, &terr, &wdirty)) break;
+        if (wdirty) load_weights(lds + L_W, wimg);
         if (T.acc != nullptr && threadIdx.x == 0) T.acc[7] = wall_clock64() - T.acc[7];  // slot 87: step total
         if (blockIdx.x == 0) {
           GraphVar& gv = *(GraphVar*)(lds + L_GV);
@@ -5418,6 +5420,8 @@ namespace md {
 int lds_bytes() { return L_TOTAL * 4; }
 int weight_image_floats() { return W_IEND; }
 bool phase_a_fits_lds_host(int n, int et) { return phase_a_fits_lds(n, et); }
+bool pfx_fits_host(int n, int et) { return pfx_fits(n, et); }
+long long pfx_words_host(int et) { return pfx_words(et); }
 // speculative workgroups: the environment plus the candidate ranking keys in LDS
 bool spec_fits_lds_host(int n, int et) {
   return phase_a_fits_lds(n, et) && env_layout(n, et).total + spec_rank_words(n) <= A_WORDS;

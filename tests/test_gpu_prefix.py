@@ -1,0 +1,58 @@
+"""Batched prefixes in the grid-wide environment step (md_env.h team_prefix_step, MD_PREFIX):
+a prediction's picks (stepRatio > 0: np.argsort(-q)[:step], U/MultiDismantler_torch.py:
+725-735) are applied as independent prefix fixed points, one per workgroup, instead of one
+cascade after another (tests/test_prefix_states.py: the property it rests on, on the oracle).
+
+MD_ENV_MODE=0 + MD_VARIANT=64 force the grid-wide step on graphs that fit LDS; MD_PREFIX=k takes
+batches of at least k actions that way (0: the sequential loop).  Rollouts with several picks
+per prediction must be identical -- sequence, LMCC trace -- and leave the identical state
+(covered set, removed edges per layer, covered / pruned counters), including batches cut short
+by a terminal prefix, batches longer than the launch's workgroups (chunks), and picks of
+nodes without alive edges; the LMCC trace is checked against the oracle environment stepped
+along the device's sequence (U/mvc_env.py:74-87, U/Mcc.py:30-38)."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from mdcommunity_amd import _lib, engine
+
+pytestmark = pytest.mark.gpu
+
+CASES = [("er100", 3), ("er100", 20), ("gmm200_s7", 5), ("er300_dense", 9), ("gmm1000_s0", 16), ("er1000", 64)]
+
+
+def run(monkeypatch, prefix, name, step):
+    monkeypatch.setenv("MD_ENV_MODE", "0")
+    monkeypatch.setenv("MD_VARIANT", "64")
+    monkeypatch.setenv("MD_PREFIX", str(prefix))
+    z = load_golden(name)
+    n = int(z["n_nodes"])
+    e = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
+    try:
+        e.load_graphs([(n, z["edges0"], z["edges1"])])
+        mr = int(e.reset()[0])
+        seq, ranks = e.rollout(step=step)[0]
+        cov, r0, r1, cnt = e.get_state(0)
+        return mr, seq.copy(), ranks.copy(), (cov.tobytes(), r0.tobytes(), r1.tobytes(), cnt.tolist())
+    finally:
+        e.close()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("name,step", CASES)
+def test_prefix_batches_same_rollouts(monkeypatch, name, step):
+    from oracle import refenv
+    base = run(monkeypatch, 0, name, step)
+    pre = run(monkeypatch, 2, name, step)
+    assert pre[0] == base[0]
+    assert pre[1].tolist() == base[1].tolist(), name
+    assert pre[2].tolist() == base[2].tolist(), name
+    assert pre[3] == base[3], name
+    z = load_golden(name)
+    g = refenv.RefGraph(int(z["n_nodes"]), z["edges0"], z["edges1"])
+    env = refenv.RefEnv(g, "unit")
+    assert [env.step(int(a)) for a in pre[1].tolist()] == pre[2].tolist()
+    assert env.terminal()
+    cnt = pre[3][3]
+    assert [int(cnt[0]), int(cnt[1])] == env.num_covered
+    assert [int(cnt[2]), int(cnt[3])] == [len(env.removed[0]) // 2, len(env.removed[1]) // 2]
