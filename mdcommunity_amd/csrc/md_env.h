@@ -2231,6 +2231,16 @@ __device__ __forceinline__ int p16_root(lds_u16* P, int v) {
   while ((next = p16_ld(P, v)) != v) v = next;
   return v;
 }
+// both layers' roots of x, the two read-only walks in lockstep
+__device__ __forceinline__ int2 p16_root2(lds_u16* P0, lds_u16* P1, int x) {
+  int a = x, b = x;
+  while (true) {
+    const int na = p16_ld(P0, a), nb = p16_ld(P1, b);
+    if (na == a && nb == b) return make_int2(a, b);
+    a = na;
+    b = nb;
+  }
+}
 __device__ __forceinline__ void p16_unite(lds_u16* P, int a, int b) {
   while (true) {
     a = p16_find(P, a);
@@ -2318,6 +2328,12 @@ __device__ __noinline__ int team_prefix_step(KParams& p, Team& T, const EnvView<
   // (the list's stores must be visible before anyone reads it: every path below crosses a barrier)
   if (grid_sync(p, *T.target, T.flag)) return -1;
   if (bad) return 0;
+  // The list is read-only from here to the next batch: one L1 invalidate (an agent-scope acquire)
+  // and then plain loads, which the L1 serves (a thread's run of the union pass walks its lines
+  // 16 bytes at a time) -- the agent-coherent loads elsewhere in this file always go to the L2.
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const unsigned* const puvc = (const unsigned*)puv;
+  const uint4* const puv4 = (const uint4*)puv;  // (p.pfx is 256-byte aligned)
   const int j = (int)blockIdx.x + 1;  // this workgroup's prefix
   const bool plast = pa != nullptr && j == kc && threadIdx.x == 0;
   if (pa != nullptr && blockIdx.x == 0 && threadIdx.x == 0) pa[1] = wall_clock64() - tp0;
@@ -2347,7 +2363,7 @@ __device__ __noinline__ int team_prefix_step(KParams& p, Team& T, const EnvView<
       const int i = ib + lane;
       bool al = false;
       if (i < mc) {
-        const unsigned uv = (unsigned)ldc(puv + i);
+        const unsigned uv = puvc[i];
         const int u = (int)(uv & 0xffffu), v = (int)(uv >> 16);
         al = !((cb[u >> 5] >> (u & 31)) & 1u) && !((cb[v >> 5] >> (v & 31)) & 1u);
       }
@@ -2361,8 +2377,9 @@ __device__ __noinline__ int team_prefix_step(KParams& p, Team& T, const EnvView<
     // the other layer's labels; a layer that lost no edge keeps its labels (no reset, union or
     // relabel); no edge pruned = the partitions agree = the fixed point
     bool ch0 = true, ch1 = true;
-    const int cr = (mc + NTHREADS - 1) / NTHREADS;
-    const int r0 = min(mc, (int)threadIdx.x * cr), r1 = min(mc, r0 + cr);
+    // the union pass's runs: whole 4-entry chunks per thread
+    const int nq = (mc + 3) >> 2, cq = (nq + NTHREADS - 1) / NTHREADS;
+    const int q0 = min(nq, (int)threadIdx.x * cq), q1 = min(nq, q0 + cq);
     for (int round = 0;; ++round) {
       if (round > 0) {
         for (int x = threadIdx.x; x < n; x += NTHREADS) {
@@ -2373,21 +2390,34 @@ __device__ __noinline__ int team_prefix_step(KParams& p, Team& T, const EnvView<
       }
       // union: a contiguous run of the list per thread (consecutive edges share endpoints)
       {
-        const int ia = ch0 ? r0 : max(r0, mc0), ib = ch1 ? r1 : min(r1, mc0);
-        unsigned nxt = ia < ib ? (unsigned)ldc(puv + ia) : 0u;
-        for (int i = ia; i < ib; ++i) {
-          const unsigned uv = nxt;
-          if (i + 1 < ib) nxt = (unsigned)ldc(puv + i + 1);  // one entry ahead
-          if (!((abm[i >> 5] >> (i & 31)) & 1u)) continue;
-          p16_unite(i < mc0 ? P0 : P1, (int)(uv & 0xffffu), (int)(uv >> 16));
+        const int ia = ch0 ? 0 : mc0, ib = ch1 ? mc : mc0;  // entries of the layers to unite
+        const int qa = max(q0, ia >> 2), qb = min(q1, (ib + 3) >> 2);
+        uint4 nxt = qa < qb ? puv4[qa] : make_uint4(0u, 0u, 0u, 0u);
+        for (int q = qa; q < qb; ++q) {
+          const uint4 w = nxt;
+          if (q + 1 < qb) nxt = puv4[q + 1];  // one chunk ahead
+          const unsigned bits = abm[q >> 3] >> ((q & 7) << 2);  // the chunk's 4 alive bits
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int i = 4 * q + k;
+            if (i < ia || i >= ib || !((bits >> k) & 1u)) continue;
+            const unsigned uv = k == 0 ? w.x : k == 1 ? w.y : k == 2 ? w.z : w.w;
+            p16_unite(i < mc0 ? P0 : P1, (int)(uv & 0xffffu), (int)(uv >> 16));
+          }
         }
       }
       __syncthreads();
       lap(6);
       // labels: every node's root, stored as its parent
       for (int x = threadIdx.x; x < n; x += NTHREADS) {
-        if (ch0) p16_st(P0, x, p16_root(P0, x));
-        if (ch1) p16_st(P1, x, p16_root(P1, x));
+        if (ch0 && ch1) {
+          const int2 r = p16_root2(P0, P1, x);
+          p16_st(P0, x, r.x);
+          p16_st(P1, x, r.y);
+        } else {
+          if (ch0) p16_st(P0, x, p16_root(P0, x));
+          if (ch1) p16_st(P1, x, p16_root(P1, x));
+        }
       }
       __syncthreads();
       lap(8);
@@ -2395,7 +2425,7 @@ __device__ __noinline__ int team_prefix_step(KParams& p, Team& T, const EnvView<
       int c0 = 0, c1 = 0;
       for (int i = threadIdx.x; i < mc; i += NTHREADS) {
         if (!((abm[i >> 5] >> (i & 31)) & 1u)) continue;
-        const unsigned uv = (unsigned)ldc(puv + i);
+        const unsigned uv = puvc[i];
         const int u = (int)(uv & 0xffffu), v = (int)(uv >> 16);
         lds_u16* const other = i < mc0 ? P1 : P0;  // layer-0 edges by the layer-1 labels
         if (p16_ld(other, u) != p16_ld(other, v)) {

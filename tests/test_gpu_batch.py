@@ -7,7 +7,9 @@ bench.py's `batch` object.
 
 Every graph's (removal sequence, LMCC trace) must equal its own single-graph rollout
 (md_rollout_kernel, dedicated mode), and seeds 0-2 must reproduce the certified sequences and
-the reference's bit-exact AUDC (tests/test_certificates.py).  Per-graph semantics are
+the reference's bit-exact AUDC (tests/test_certificates.py), as must the seeds of
+tests/golden/batch_certs.npz (the longest rollouts among 3..511 and C5 seeds up to 4095, each
+certified against the reference itself by tests/golden/make_batch_certs.py).  Per-graph semantics are
 single-graph semantics: the reference's Predict batching quirk is not
 replicated.
 """
@@ -88,6 +90,31 @@ def check_goldens(mr, outs):
         assert audc(ranks, int(mr[s]), N) == float(z["score"])  # bit-exact
 
 
+def check_batch_certs(mr, outs, lo=0):
+    """Seeds beyond 0-2 pinned to the REFERENCE (tests/golden/make_batch_certs.py: the longest
+    rollouts of seeds 3..511 and C5 seeds above 511): the batch's sequence is the certified one,
+    its LMCC trace is the reference's along it, its AUDC the reference's bit for bit (also the
+    reference's own rollout's), every pick inside the reference's near-tie band.  Returns the
+    seeds checked."""
+    import os
+    from conftest import GOLDEN
+    with np.load(os.path.join(GOLDEN, "batch_certs.npz")) as z:
+        c = {k: z[k] for k in z.files}
+    done = []
+    for s in c["seeds"].tolist():
+        if not lo <= s < lo + len(outs):
+            continue
+        seq, ranks = outs[s - lo]
+        assert int(mr[s - lo]) == int(c[f"s{s}_max_rank"]), s
+        assert seq.tolist() == c[f"s{s}_gpu_seq"].tolist(), s
+        assert ranks.tolist() == c[f"s{s}_ref_ranks_along"].tolist(), s
+        a = audc(ranks, int(mr[s - lo]), N)
+        assert a == float(c[f"s{s}_ref_score_along"]) == float(c[f"s{s}_ref_score"]), s  # bit-exact
+        assert float(np.max(c[f"s{s}_margin"])) <= 2e-5, s
+        done.append(s)
+    return done
+
+
 @pytest.mark.timeout(240)
 def test_c3_256_graphs_one_queue_launch_and_tail(graphs, weights, single):
     """configs[2]: 256 graphs in one queue-mode launch (its last <= 8 running graphs continue
@@ -101,6 +128,7 @@ def test_c3_256_graphs_one_queue_launch_and_tail(graphs, weights, single):
     assert sum(len(s) for s, _ in outs) > 256 * 20
     check_against_single(mr, outs, single, 0)
     check_goldens(mr, outs)
+    assert len(check_batch_certs(mr, outs)) >= 2  # the C3 tail's longest rollouts (seeds 24, 178)
 
 
 @pytest.mark.timeout(240)
@@ -111,6 +139,7 @@ def test_c5_slice_512_graphs_one_queue_launch_and_tail(graphs, weights, single):
     assert launches in (1, 2, 3)  # (see the C3 test)
     check_against_single(mr, outs, single, 0)
     check_goldens(mr, outs)
+    assert len(check_batch_certs(mr, outs)) >= 6
 
 
 @pytest.mark.timeout(240)
@@ -180,6 +209,7 @@ def test_c5_4096_graphs_one_queue_launch(weights, graphs):
     # end through their K2 end-game hand-shakes before any is parked)
     assert launches in (1, 2)
     check_goldens(mr, outs)
+    assert len(check_batch_certs(mr, outs)) >= 10  # (and the C5 seeds above 511)
     bad = []
     for lo in range(0, 4096, 512):
         cmr, couts, _ = batch_rollout(weights, big[lo:lo + 512])
