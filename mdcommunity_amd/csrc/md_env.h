@@ -2183,6 +2183,7 @@ __device__ bool team_features(KParams& p, Team& T, const EnvView<true>& E, int n
 // [2 et, + 4 TEAM_MAX_WG) per-prefix records {lmcc, alive 0, alive 1, -}, then per prefix the
 // alive bitmap of the compact list (pfx_bw words).
 __host__ __device__ inline int pfx_bw(int et) { return (et + 31) >> 5; }
+constexpr int PFX_PROF_ROW = 2048;  // diagnostics: per-prefix rounds and ticks of the last batch (md_profile)
 __host__ __device__ inline long long pfx_words(int et) { return 2LL * et + 4LL * TEAM_MAX_WG + (long long)TEAM_MAX_WG * pfx_bw(et); }
 // LDS words of one prefix's fixed point: u16 parents of both layers, the prefix's cover bitmap,
 // the alive bitmap of the compact list, reduction words
@@ -2380,6 +2381,7 @@ __device__ __noinline__ int team_prefix_step(KParams& p, Team& T, const EnvView<
     // the union pass's runs: whole 4-entry chunks per thread
     const int nq = (mc + 3) >> 2, cq = (nq + NTHREADS - 1) / NTHREADS;
     const int q0 = min(nq, (int)threadIdx.x * cq), q1 = min(nq, q0 + cq);
+    int nrounds = 0;
     for (int round = 0;; ++round) {
       if (round > 0) {
         for (int x = threadIdx.x; x < n; x += NTHREADS) {
@@ -2436,6 +2438,7 @@ __device__ __noinline__ int team_prefix_step(KParams& p, Team& T, const EnvView<
       const int2 cs = block_sum2(c0, c1, tmp);
       __syncthreads();
       lap(9);
+      ++nrounds;
       if (plast) pa[11] += 1;
       if (pa != nullptr && threadIdx.x == 0)
         __hip_atomic_fetch_max(pa, (unsigned long long)(round + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2476,8 +2479,15 @@ __device__ __noinline__ int team_prefix_step(KParams& p, Team& T, const EnvView<
       stc(rec + 4 * (j - 1) + 2, al.y);
     }
     lap(10);
-    if (pa != nullptr && threadIdx.x == 0)
-      __hip_atomic_fetch_max(pa + 2, wall_clock64() - tp0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (pa != nullptr && threadIdx.x == 0) {
+      const unsigned long long dt = wall_clock64() - tp0;
+      __hip_atomic_fetch_max(pa + 2, dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // per prefix (rows PFX_PROF_ROW..; MD_PROF_ALL=1 reads them): rounds, device ticks
+      if (p.prof_cap > PFX_PROF_ROW + 24 && j <= 1024) {
+        p.prof[(size_t)PFX_PROF_ROW * PROF_SLOTS + (j - 1)] = (unsigned long long)nrounds;
+        p.prof[(size_t)PFX_PROF_ROW * PROF_SLOTS + 1024 + (j - 1)] = dt;
+      }
+    }
   }
   if (grid_sync(p, *T.target, T.flag)) return -1;
   if (pa != nullptr) tp0 = wall_clock64();

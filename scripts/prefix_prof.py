@@ -32,10 +32,18 @@ seq, _ = eng.rollout(step=step)[0]
 ms, _ = eng.last_timing()
 P = eng.profile_read().astype(np.int64)
 eng.profile(0)
-R = P[P[:, 92] > 0]
+R = P[:2048][P[:2048, 92] > 0]
 print(f"N={n}, step {step}: {len(seq)} removals, rollout kernel {ms:.2f} ms; {len(R)} prefix batches", flush=True)
 for r in R:
     us = lambda k: r[k] / 100.0
     print(f"  prefixes {r[92]} applied {r[93]}: most rounds {r[80]}; list+validation {us(81):.1f} us, slowest prefix "
           f"{us(82):.1f} us, death steps {us(83):.1f} us; last prefix ({r[91]} rounds): init {us(84):.1f} union "
           f"{us(86):.1f} labels {us(88):.1f} prune {us(89):.1f} lmcc+stores {us(90):.1f} us; step total {us(87):.1f} us")
+if os.environ.get("MD_PROF_ALL") == "1" and len(P) > 2048:
+    flat = np.zeros(24 * 96, np.int64)
+    blk = P[2048:2048 + 24].reshape(-1)
+    flat[:len(blk)] = blk
+    rounds, ticks = flat[:1024], flat[1024:2048] / 100.0
+    k = int(np.count_nonzero(rounds))
+    print(f"  last batch, per prefix j=1..{k}: rounds " + " ".join(str(int(x)) for x in rounds[:k]))
+    print("  fixed-point us: " + " ".join("%.0f" % x for x in ticks[:k]))
