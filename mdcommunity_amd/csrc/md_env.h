@@ -2565,7 +2565,9 @@ __device__ __noinline__ int team_prefix_step(KParams& p, Team& T, const EnvView<
 // actions are known): workgroup 0 holds the graph's GraphVar in LDS and keeps its books (the
 // others read the counts they need from the partials); pend_n actions, the first pend_first
 // (or p.pend[0] when < 0).  Returns an ERR_* code (0: ok) in *err; true on a grid error.
-__device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_first, int* err, bool* wdirty) {
+// (*err bit 30: the weight image's LDS was used -- the caller reloads it)
+constexpr int TEAM_WDIRTY = 1 << 30;
+__device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_first, int* err) {
   const GraphInfo gi = p.ginfo[g];
   const int n = gi.n;
   GraphVar& gv = *(GraphVar*)(lds_base() + L_GV);
@@ -2600,12 +2602,12 @@ __device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_f
   // batched prefixes (stepRatio): chunks of up to n_main actions at once while at least
   // pfx_min remain (team_prefix_step); an invalid action leaves them to the loop below
   int k0 = 0;
-  *wdirty = false;
+  bool wdirty = false;
   while (p.pfx != nullptr && p.pfx_min > 0 && s0_done && pend_n - k0 >= p.pfx_min && alive0 > 0 && alive1 > 0 &&
          pfx_fits(n, E.et)) {
     const int kc = min(pend_n - k0, p.n_main);
     int J = 0, cnt[4];
-    *wdirty = true;  // (the LDS from L_W on, even when the batch is refused)
+    wdirty = true;  // (the LDS from L_W on, even when the batch is refused)
     const int r = team_prefix_step(p, T, E, k0, kc, pend_first, books, &J, cnt);
     if (r < 0) return true;
     if (r == 0) break;
@@ -2618,7 +2620,7 @@ __device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_f
       break;
     }
   }
-  if (*wdirty && rk != nullptr) {  // the static ranks again (their LDS was the prefixes')
+  if (wdirty && rk != nullptr) {  // the static ranks again (their LDS was the prefixes')
     lds_u16* dst = (lds_u16*)(uint16_t*)(lds_base() + L_SCR + TEAM_RANK_OFF);
     const unsigned* src = (const unsigned*)(p.prank + gi.rank_off);
     for (int i = threadIdx.x; i < ((n + 1) >> 1); i += NTHREADS) ((lds_u32*)(unsigned*)dst)[i] = src[i];
@@ -2690,5 +2692,6 @@ __device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_f
     h0_update(p, gi, gv, ag.dm0, ag.dm1, hd0, hd1);
     __syncthreads();
   }
+  if (wdirty) *err |= TEAM_WDIRTY;
   return false;
 }

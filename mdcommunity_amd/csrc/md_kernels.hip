@@ -4943,6 +4943,7 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
     MD_PROF(0);
     if (threadIdx.x == 0) ((int*)(lds + L_MISC))[60] = pstep;
     __syncthreads();
+    bool wdirty = false;  // the weight image's LDS was used (reloaded below, one call site)
     if (ded) {
       if (is_env) staged = phase_a(p, p.glist[blockIdx.x], have_q, lds, staged);
     } else if (team) {
@@ -4981,9 +4982,9 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
           if (threadIdx.x == 0) p.prof[(size_t)pstep * PROF_SLOTS + 87] = wall_clock64();
         }
         int terr = 0;
-        bool wdirty = false;
-        if (team_env_step(p, T, p.glist[0], pn, pf, &terr, &wdirty)) break;
-        if (wdirty) load_weights(lds + L_W, wimg);
+        if (team_env_step(p, T, p.glist[0], pn, pf, &terr)) break;
+        wdirty = (terr & TEAM_WDIRTY) != 0;
+        terr &= ~TEAM_WDIRTY;
         if (T.acc != nullptr && threadIdx.x == 0) T.acc[7] = wall_clock64() - T.acc[7];  // slot 87: step total
         if (blockIdx.x == 0) {
           GraphVar& gv = *(GraphVar*)(lds + L_GV);
@@ -5000,13 +5001,12 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
         }
       }
     } else {
-      bool wdirty = false;
       for (int gi = blockIdx.x; gi < ng; gi += p.n_main) {
         phase_a(p, p.glist[gi], have_q, lds, false);
         wdirty = true;
       }
-      if (wdirty) load_weights(lds + L_W, wimg);
     }
+    if (wdirty) load_weights(lds + L_W, wimg);
     MD_PROF(3);
     // iteration-1 prebuild (p.pre_ew): a single graph's tile workgroups wait at barrier A for
     // the release or for phase A's early word, and build their iteration-1 rows and lists from
