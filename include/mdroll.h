@@ -166,6 +166,10 @@ md_status md_set_team_size(md_ctx* ctx, int team_size);
  * md_rollout call, measured with HIP events on the context's stream, and their count. */
 md_status md_last_timing(md_ctx* ctx, double* kernel_ms, int32_t* launches);
 
+/* Host selection requests (ties, stepRatio predictions the device did not pick itself) served
+ * during the last md_reset / md_predict / md_step / md_rollout call. */
+md_status md_host_requests(md_ctx* ctx, int32_t* n_requests);
+
 /* Diagnostics: record device wall-clock (100 MHz) phase timestamps of workgroup 0,
  * MD_PROF_SLOTS slots per removal step (0-15 timestamps, 16-31 accumulated sub-phase
  * durations and counters of the environment step, 64-72 speculative-step timeline), for up to `steps` steps per launch of the

@@ -25,7 +25,7 @@ PROF_SLOTS = 96  # MD_PROF_SLOTS in include/mdroll.h
 EXPORTS = ("md_create", "md_destroy", "md_last_error", "md_set_weights", "md_load_graphs", "md_reset",
            "md_reset_deferred", "md_max_rank",
            "md_predict", "md_step", "md_rollout", "md_rollout_trace", "md_get_state", "md_set_state",
-           "md_set_team_size", "md_set_tie_argsort", "md_last_timing", "md_profile", "md_profile_read",
+           "md_set_team_size", "md_set_tie_argsort", "md_last_timing", "md_host_requests", "md_profile", "md_profile_read",
            "md_version", "md_device_count", "md_spec_stats", "md_gmm_last_error", "md_gmm_nodes", "md_gmm_links")
 
 _i32p = ctypes.POINTER(ctypes.c_int32)
@@ -75,6 +75,7 @@ def load_library(path=LIB_PATH):
         "md_set_team_size": (ctypes.c_int, [vp, ctypes.c_int]),
         "md_set_tie_argsort": (ctypes.c_int, [vp, vp]),
         "md_last_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), _i32p]),
+        "md_host_requests": (ctypes.c_int, [vp, _i32p]),
         "md_profile": (ctypes.c_int, [vp, ctypes.c_int]),
         "md_profile_read": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, _i32p]),
         "md_version": (ctypes.c_char_p, []),
@@ -305,6 +306,12 @@ class Engine:
         self._check(self.lib.md_profile_read(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), cap,
                                              ctypes.byref(k)))
         return out[:k.value]
+
+    def host_requests(self):
+        """Host selection requests served during the last call (ties, stepRatio predictions)."""
+        n = ctypes.c_int32()
+        self._check(self.lib.md_host_requests(self.h, ctypes.byref(n)))
+        return n.value
 
     def last_timing(self):
         ms = ctypes.c_double()

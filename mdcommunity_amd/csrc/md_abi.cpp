@@ -182,7 +182,9 @@ struct md_ctx {
   bool abort_on = true;
   bool fp_short = true;  // MD_FP_SHORTCUT=0: every fixed point runs its confirmation round
   bool fp_skip = true;   // MD_FP_SKIP=0: every LDS fixed-point round re-unites both layers
+  int last_served = 0;   // host selection requests served by the last API call's launches
   int pfx_min = 8;       // MD_PREFIX: grid-wide steps take >= this many actions as batched prefixes (0: off)
+  bool dev_topk = true;  // MD_DEVTOPK=0: every stepRatio prediction goes to the host's numpy routine
   DevBuf<int> pfx;       // their scratch (md_env.h pfx_words)
   bool first_req = true;  // MD_FIRST_REQ=0: no speculative request at a rollout's first step
   DevBuf<unsigned long long> dfbuf;
@@ -629,6 +631,10 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
   }
   p.run_mode = run_mode;
   p.host_select = host_select;
+  // the k largest Q of a grid-wide step's prediction on the device when tie-free (numpy's own
+  // routine is the selection rule: a Python selector keeps every request; MD_DEVTOPK=0: off)
+  p.sel_step = sel != nullptr ? sel->step : 1;
+  p.dev_topk = host_select && sel != nullptr && c->tie_argsort != nullptr && c->dev_topk ? 1 : 0;
   const bool hs = sel != nullptr && c->host_mode != 0 && c->h_req.d != nullptr;
   if (hs) {
     for (int g : v) {
@@ -683,6 +689,7 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
           if (r != 0 && r != __atomic_load_n(c->h_ans.h + g, __ATOMIC_RELAXED)) {
             const auto ts = std::chrono::steady_clock::now();
             serve_request(c, sel, g, r, qd, acts);
+            c->last_served += 1;
             if (host_stats) {
               serve_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
               ++n_served;
@@ -821,6 +828,7 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_FP_SHORTCUT")) c->fp_short = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_FP_SKIP")) c->fp_skip = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_PREFIX")) c->pfx_min = std::max(0, std::atoi(v));
+  if (const char* v = std::getenv("MD_DEVTOPK")) c->dev_topk = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_FIRST_REQ")) c->first_req = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_DF")) c->df_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_SPEC")) c->spec_n = std::max(0, std::min(SPEC_MAX, std::atoi(v)));
@@ -1231,6 +1239,7 @@ md_status md_reset(md_ctx* c, int32_t* max_rank_out) {
   p.nglist = c->ng;
   HIPCHK(c, launch_reset(p, c->stream));
   c->last_ms = 0.0;
+  c->last_served = 0;
   c->last_launches = 0;
   md_status st = launch(c, gl, RUN_STEP, 0);  // s0: initial prune (U/mvc_env.py:52)
   if (st != MD_OK) return st;
@@ -1250,6 +1259,7 @@ md_status md_reset_deferred(md_ctx* c) {
   p.nglist = c->ng;
   HIPCHK(c, launch_reset(p, c->stream));
   c->last_ms = 0.0;
+  c->last_served = 0;
   c->last_launches = 0;
   // the host view md_rollout starts from (it pushes it to the device): as md_reset_kernel left
   // the GraphVar, with the edge counts as alive counts (a graph with edges in both layers runs;
@@ -1311,6 +1321,7 @@ md_status md_predict(md_ctx* c, float* q_out, int32_t* argmax, int32_t* n_tie, f
   md_status st = push_vars(c);
   if (st != MD_OK) return st;
   c->last_ms = 0.0;
+  c->last_served = 0;
   c->last_launches = 0;
   if (!gl.empty()) {
     // graphs with no live node keep their (all masked) q
@@ -1351,6 +1362,7 @@ md_status md_step(md_ctx* c, const int32_t* actions, int32_t* lmcc_out, uint8_t*
   md_status st = push_vars(c);
   if (st != MD_OK) return st;
   c->last_ms = 0.0;
+  c->last_served = 0;
   c->last_launches = 0;
   st = launch(c, gl, RUN_STEP, 0);
   if (st != MD_OK) return st;
@@ -1369,6 +1381,7 @@ md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, i
   HIPCHK(c, hipSetDevice(c->device));
   const int host_select = step > 1 ? 1 : 0;
   c->last_ms = 0.0;
+  c->last_served = 0;
   c->last_launches = 0;
   std::vector<int> gl, idle;
   for (int g = 0; g < c->ng; ++g) {
@@ -1585,6 +1598,12 @@ md_status md_profile_read(md_ctx* c, uint64_t* out, int capacity_steps, int32_t*
   const int k = std::min(have, capacity_steps);
   if (out) std::memcpy(out, c->prof_host.data(), sizeof(uint64_t) * PROF_SLOTS * (size_t)k);
   if (n_steps) *n_steps = k;
+  return MD_OK;
+}
+
+md_status md_host_requests(md_ctx* c, int32_t* n_requests) {
+  if (!c || !n_requests) return MD_EINVAL;
+  *n_requests = c->last_served;
   return MD_OK;
 }
 

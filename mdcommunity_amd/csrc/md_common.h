@@ -160,6 +160,9 @@ struct Params {
   int variant;                     // diagnostics: algorithm variant (MD_VARIANT env, 0 = default)
   int run_mode;                    // RUN_*
   int host_select;                 // 1: every prediction goes to the host (step > 1)
+  int sel_step;                    // step > 1: picks per prediction; dev_topk: the grid-wide step's
+  int dev_topk;                    //   prediction picks its k largest Q on the device when they are
+                                   //   distinct and above the rest (md_kernels.hip device_topk)
   int* err;                        // device error word (nonzero = failure code)
   unsigned long long* prof;        // optional phase timestamps of workgroup 0 (wall clock)
   int prof_cap;                    // steps of 16 timestamp slots available in prof

@@ -675,6 +675,122 @@ __device__ __forceinline__ bool endgame_state(KParams& p, const GraphInfo& gi, c
          gv.dmax[0] == 1 && gv.dmax[1] == 1;
 }
 
+// stepRatio picks on the device: np.argsort(-q)[:k] (U/MultiDismantler_torch.py:725) is the
+// unique descending order of the k largest Q when those are distinct and the k-th is above the
+// (k+1)-th -- then no tie order of numpy's sort can matter.  Radix select of the k-th largest
+// key (four 8-bit digit passes over the graph's Q row), a count of the keys equal to it, the k
+// candidates collected and bitonic-sorted in LDS, a check for equal neighbours.  Returns k with
+// the picks in p.pend, or 0 (a tie at or above the k-th value, or k > TOPK_MAX): the host's
+// numpy routine then decides, as for every tie.  k <= the live nodes (the finite Q), so the
+// k-th largest is above the masked -inf rows.  Grid-wide step only: the tile scratch of
+// workgroup 0 is free at phase A there.
+constexpr int TOPK_MAX = 1024;
+__device__ __forceinline__ unsigned topk_key(float f) {
+  const unsigned u = __float_as_uint(f == 0.f ? 0.f : f);  // (-0 == +0 for numpy's compare)
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);       // unsigned order = float order
+}
+__device__ __noinline__ int device_topk(KParams&, const GraphInfo gi, int k) {
+  KParams& p = kp();
+  const float* q = p.q + gi.node_off;
+  const int n = gi.n;
+  int* const hist = (int*)(lds_base() + L_SCR);  // [256]
+  int* const ctl = hist + 256;                    // [8]: prefix, need, equal count, collected
+  unsigned* const ck = (unsigned*)(ctl + 8);      // [TOPK_MAX] keys
+  int* const ci = (int*)(ck + TOPK_MAX);          // [TOPK_MAX] node ids
+  if (k < 1 || k > TOPK_MAX || k > n) return 0;
+  const int lane = lane_id();
+  unsigned prefix = 0u, pmask = 0u;
+  int need = k, eq = 0;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    if (threadIdx.x < 256) hist[threadIdx.x] = 0;
+    __syncthreads();
+    for (int x = threadIdx.x; x < n; x += NTHREADS) {
+      const unsigned key = topk_key(ldc(q + x));
+      if ((key & pmask) == prefix) atomicAdd(hist + ((key >> shift) & 255u), 1);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      // the digit holding the need-th largest key: lane l sums digits 255 - 4l .. 252 - 4l,
+      // an inclusive scan over the lanes from the top digit down
+      const int b0 = 255 - 4 * lane;
+      const int h0 = hist[b0], h1 = hist[b0 - 1], h2 = hist[b0 - 2], h3 = hist[b0 - 3];
+      const int s = h0 + h1 + h2 + h3;
+      int incl = s;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+      }
+      const int before = incl - s;
+      const unsigned long long m = __ballot(incl >= need);
+      const int hit = __ffsll((long long)m) - 1;  // first lane whose range reaches rank `need`
+      if (lane == hit) {
+        int c = before, d = b0, hd = h0;
+        const int hs[4] = {h0, h1, h2, h3};
+        for (int t = 0; t < 4; ++t) {
+          d = b0 - t;
+          hd = hs[t];
+          if (c + hd >= need) break;
+          c += hd;
+        }
+        ctl[0] = d;
+        ctl[1] = need - c;  // rank inside the digit's group
+        ctl[2] = hd;
+      }
+    }
+    __syncthreads();
+    prefix |= (unsigned)ctl[0] << shift;
+    pmask |= 255u << shift;
+    need = ctl[1];
+    eq = ctl[2];
+    __syncthreads();
+  }
+  // prefix is the k-th largest key; eq keys equal it, k - need of them are larger
+  if (eq != 1) return 0;  // a tie at the k-th value (need == 1 then: k - 1 keys above it)
+  if (threadIdx.x == 0) ctl[3] = 0;
+  for (int i = threadIdx.x; i < TOPK_MAX; i += NTHREADS) ck[i] = 0u;  // (pads sort last)
+  __syncthreads();
+  for (int x = threadIdx.x; x < n; x += NTHREADS) {
+    const unsigned key = topk_key(ldc(q + x));
+    if (key >= prefix) {
+      const int at = atomicAdd(ctl + 3, 1);
+      if (at < TOPK_MAX) {
+        ck[at] = key;
+        ci[at] = x;
+      }
+    }
+  }
+  __syncthreads();
+  if (ctl[3] != k) return 0;  // (cannot happen: k - 1 above, one equal)
+  // bitonic sort, descending by key, over the next power of two >= k
+  int m2 = 1;
+  while (m2 < k) m2 <<= 1;
+  for (int size = 2; size <= m2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < m2; i += NTHREADS) {
+        const int jx = i ^ stride;
+        if (jx > i) {
+          const bool desc = (i & size) == 0;
+          const unsigned a = ck[i], b = ck[jx];
+          if (desc ? a < b : a > b) {
+            ck[i] = b;
+            ck[jx] = a;
+            const int t = ci[i];
+            ci[i] = ci[jx];
+            ci[jx] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  bool dup = false;
+  for (int i = threadIdx.x; i + 1 < k; i += NTHREADS) dup |= ck[i] == ck[i + 1];
+  if (__syncthreads_or(dup)) return 0;
+  for (int i = threadIdx.x; i < k; i += NTHREADS)
+    __hip_atomic_store(p.pend + gi.node_off + i, ci[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return k;
+}
+
 // Synchronous form (one graph per launch: nothing else could run meanwhile): request, then
 // wait for the answer.  Returns the number of actions (0 on error; the error word is set).
 __device__ __noinline__ int host_handshake(KParams&, const GraphInfo gi, int g, int npred, float qmax, int ntie, int* misc,
@@ -811,6 +927,11 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
     if (p.run_mode == RUN_PREDICT) {
       if (threadIdx.x == 0) gv.status = ST_PAUSED;
       stop = true;
+    } else if (p.host_select && p.dev_topk && team_out != nullptr && p.nglist == 1 &&
+               (pend_n = device_topk(p, gi, min(p.sel_step, gv.n_live))) > 0) {
+      // (stepRatio picks of the grid-wide step taken on the device: see device_topk; with
+      // fewer live nodes than picks only the live ones -- the graph is terminal once they are
+      // gone, so the masked picks after them are never applied)
     } else if (p.host_select || misc[2] != 1) {
 #ifndef MD_NO_HS
       if (p.h_req != nullptr) {

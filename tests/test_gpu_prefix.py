@@ -32,8 +32,9 @@ def run(monkeypatch, prefix, name, step):
         e.load_graphs([(n, z["edges0"], z["edges1"])])
         mr = int(e.reset()[0])
         seq, ranks = e.rollout(step=step)[0]
+        served = e.host_requests()
         cov, r0, r1, cnt = e.get_state(0)
-        return mr, seq.copy(), ranks.copy(), (cov.tobytes(), r0.tobytes(), r1.tobytes(), cnt.tolist())
+        return mr, seq.copy(), ranks.copy(), (cov.tobytes(), r0.tobytes(), r1.tobytes(), cnt.tolist()), served
     finally:
         e.close()
 
@@ -56,3 +57,25 @@ def test_prefix_batches_same_rollouts(monkeypatch, name, step):
     cnt = pre[3][3]
     assert [int(cnt[0]), int(cnt[1])] == env.num_covered
     assert [int(cnt[2]), int(cnt[3])] == [len(env.removed[0]) // 2, len(env.removed[1]) // 2]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("name,step", [("er100", 3), ("gmm1000_s0", 16), ("er1000", 64)])
+def test_device_topk_same_rollouts(monkeypatch, name, step):
+    """The grid-wide step's stepRatio picks taken on the device when the k largest Q are
+    distinct and above the rest (md_kernels.hip device_topk; MD_DEVTOPK=0: every prediction
+    through the host's np.argsort) -- identical sequences, LMCC traces and final states, with
+    and without the batched prefixes."""
+    out = {}
+    for dev in ("0", "1"):
+        for prefix in (0, 2):
+            monkeypatch.setenv("MD_DEVTOPK", dev)
+            out[(dev, prefix)] = run(monkeypatch, prefix, name, step)
+    ref = out[("0", 0)]
+    for key, r in out.items():
+        assert r[0] == ref[0] and r[1].tolist() == ref[1].tolist() and r[2].tolist() == ref[2].tolist(), key
+        assert r[3] == ref[3], key
+    # the device took predictions itself (fewer host requests than predictions)
+    preds = -(-len(ref[1]) // step)
+    assert out[("0", 0)][4] == preds
+    assert out[("1", 0)][4] < preds, (out[("1", 0)][4], preds)
