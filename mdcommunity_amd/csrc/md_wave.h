@@ -1146,9 +1146,12 @@ __device__ __forceinline__ void wq_loop(KParams&, const float* __restrict__ wimg
     }
     // admission: every wave of the chip runs its own items, so more graphs run at once than in
     // md_queue_kernel: up to two per workgroup (sweep over 4096 graphs: 160 / 512 / 1024 / all ->
-    // 366 / 265 / 271 / 281 ms); MD_VARIANT bits 16+ override
+    // 366 / 265 / 271 / 281 ms), one per workgroup when no more than two per workgroup wait
+    // (512 graphs, the C5 shard at world 8: 256 / 384 / 512 admitted -> 37.2 / 37.8 / 38.0 ms;
+    // 256 graphs: 128 / 192 / 256 -> 26.4 / 25.0 / 24.8 ms); MD_VARIANT bits 16+ override
     const int vadm = (int)((unsigned)p.variant >> 16);
-    const int first = min(tot, vadm > 0 ? vadm : 2 * (int)gridDim.x);
+    const int grid = (int)gridDim.x;
+    const int first = min(tot, vadm > 0 ? vadm : (tot > 2 * grid ? 2 * grid : grid));
     if (threadIdx.x == 0) {
       __hip_atomic_store((g_u32*)(p.qctl + QC_REM), (unsigned)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store((g_u32*)(p.qctl + QC_ADMIT), (unsigned)(first < tot ? run[first] : ng), __ATOMIC_RELAXED,
