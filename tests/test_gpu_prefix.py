@@ -21,15 +21,24 @@ pytestmark = pytest.mark.gpu
 CASES = [("er100", 3), ("er100", 20), ("gmm200_s7", 5), ("er300_dense", 9), ("gmm1000_s0", 16), ("er1000", 64)]
 
 
-def run(monkeypatch, prefix, name, step):
+def run(monkeypatch, prefix, name, step, graph=None, degree=False):
     monkeypatch.setenv("MD_ENV_MODE", "0")
     monkeypatch.setenv("MD_VARIANT", "64")
     monkeypatch.setenv("MD_PREFIX", str(prefix))
-    z = load_golden(name)
-    n = int(z["n_nodes"])
-    e = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
+    if graph is None:
+        z = load_golden(name)
+        graph = (int(z["n_nodes"]), z["edges0"], z["edges1"])
+    n = graph[0]
+    nw = None
+    if degree:
+        from mdcommunity_amd import graph as mgraph
+        gg = mgraph.Graph_test.from_edges(n, graph[1], graph[2])
+        mgraph.ensure_degree_weights(gg)
+        nw = mgraph.node_weight_array([gg])
+    e = _lib.Engine(engine.load_weights(engine.DEFAULT_DEGREE if degree else engine.DEFAULT_UNIT),
+                    cost_mode=_lib.MD_COST_DEGREE if degree else _lib.MD_COST_UNIT)
     try:
-        e.load_graphs([(n, z["edges0"], z["edges1"])])
+        e.load_graphs([graph], node_w=nw)
         mr = int(e.reset()[0])
         seq, ranks = e.rollout(step=step)[0]
         served = e.host_requests()
@@ -79,3 +88,29 @@ def test_device_topk_same_rollouts(monkeypatch, name, step):
     preds = -(-len(ref[1]) // step)
     assert out[("0", 0)][4] == preds
     assert out[("1", 0)][4] < preds, (out[("1", 0)][4], preds)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("name,step", [("deg_gmm200_s7", 5), ("deg_gmm1000_s0", 12)])
+def test_prefix_batches_degree_cost(monkeypatch, name, step):
+    """Degree cost (D/mvc_env.py:75-134): the environment step is the same cascade, so the
+    batched prefixes give the sequential loop's rollouts and states."""
+    base = run(monkeypatch, 0, name, step, degree=True)
+    pre = run(monkeypatch, 2, name, step, degree=True)
+    for a, b in zip(base[:4], pre[:4]):
+        assert (a.tolist() if hasattr(a, "tolist") else a) == (b.tolist() if hasattr(b, "tolist") else b), name
+
+
+@pytest.mark.timeout(300)
+def test_prefix_batches_edge_graphs(monkeypatch):
+    """The edge-case graphs (tests/edge_graphs.py: K2, a shared-hub star, isolated nodes, 63 / 65
+    nodes, two clusters, a tree against a dense layer, an empty second layer) with 3 and 7 picks
+    per prediction: batched prefixes == the sequential loop (sequence, LMCC trace, final state)."""
+    from edge_graphs import cases
+    for name, n, e0, e1 in cases():
+        for step in (3, 7):
+            base = run(monkeypatch, 0, name, step, graph=(n, e0, e1))
+            pre = run(monkeypatch, 2, name, step, graph=(n, e0, e1))
+            assert base[0] == pre[0], name
+            assert base[1].tolist() == pre[1].tolist() and base[2].tolist() == pre[2].tolist(), (name, step)
+            assert base[3] == pre[3], (name, step)
