@@ -131,6 +131,13 @@ md_status md_step(md_ctx* ctx, const int32_t* actions, int32_t* lmcc_out, uint8_
 md_status md_rollout(md_ctx* ctx, int step, int32_t* seq_out, int32_t* lmcc_out, int32_t* seq_len,
                      md_select_cb cb, void* user);
 
+/* md_rollout with the outputs packed: graph g's removal order and LMCC trace at offsets
+ * sum_{h<g} seq_len[h] of seq_packed / lmcc_packed (capacity sum(n_nodes) each; only the
+ * removals are written and copied -- one device-to-host copy of the removals instead of every
+ * node slot of a large batch).  seq_len is required. */
+md_status md_rollout_packed(md_ctx* ctx, int step, int32_t* seq_packed, int32_t* lmcc_packed, int32_t* seq_len,
+                            md_select_cb cb, void* user);
+
 /* Per-step diagnostics of the last md_rollout for graph g (capacity n_nodes[g] rows):
  * live nodes, alive edges in layer 0 and 1, number of nodes tied at the max, per prediction,
  * and (float) the best Q and top-2 gap.  Returns the number of predictions made. */

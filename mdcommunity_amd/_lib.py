@@ -24,7 +24,7 @@ PROF_SLOTS = 96  # MD_PROF_SLOTS in include/mdroll.h
 
 EXPORTS = ("md_create", "md_destroy", "md_last_error", "md_set_weights", "md_load_graphs", "md_reset",
            "md_reset_deferred", "md_max_rank",
-           "md_predict", "md_step", "md_rollout", "md_rollout_trace", "md_get_state", "md_set_state",
+           "md_predict", "md_step", "md_rollout", "md_rollout_packed", "md_rollout_trace", "md_get_state", "md_set_state",
            "md_set_team_size", "md_set_tie_argsort", "md_last_timing", "md_host_requests", "md_profile", "md_profile_read",
            "md_version", "md_device_count", "md_spec_stats", "md_gmm_last_error", "md_gmm_nodes", "md_gmm_links")
 
@@ -68,6 +68,7 @@ def load_library(path=LIB_PATH):
         "md_predict": (ctypes.c_int, [vp, _f32p, _i32p, _i32p, _f32p]),
         "md_step": (ctypes.c_int, [vp, _i32p, _i32p, _u8p]),
         "md_rollout": (ctypes.c_int, [vp, ctypes.c_int, _i32p, _i32p, _i32p, SELECT_CB_ADDR, vp]),
+        "md_rollout_packed": (ctypes.c_int, [vp, ctypes.c_int, _i32p, _i32p, _i32p, SELECT_CB_ADDR, vp]),
         "md_rollout_trace": (ctypes.c_int, [vp, ctypes.c_int, _i32p, _i32p, _i32p, _i32p, _f32p, _f32p, _i32p]),
         "md_spec_stats": (ctypes.c_int, [vp, ctypes.c_int, _i32p, _i32p]),
         "md_get_state": (ctypes.c_int, [vp, ctypes.c_int, _u8p, _u8p, _u8p, _i32p]),
@@ -250,19 +251,20 @@ class Engine:
             self._check(self.lib.md_set_tie_argsort(self.h, native))
             self._tie_native = native
         tot = int(self.node_off[-1])
+        # packed outputs (md_rollout_packed): only the removals cross the link; each call's
+        # arrays are fresh, so the per-graph views below are not shared with later calls
         seq = np.empty(tot, np.int32)
         lm = np.empty(tot, np.int32)
         ln = np.zeros(len(self.n_nodes), np.int32)
         self._cb_error = None
-        st = self.lib.md_rollout(self.h, int(step), _ptr(seq, _i32p), _ptr(lm, _i32p), _ptr(ln, _i32p), self._ccb, None)
+        st = self.lib.md_rollout_packed(self.h, int(step), _ptr(seq, _i32p), _ptr(lm, _i32p), _ptr(ln, _i32p),
+                                        self._ccb, None)
         if self._cb_error is not None:
             raise self._cb_error
         self._check(st)
-        out = []
-        for g in range(len(self.n_nodes)):
-            o = int(self.node_off[g])
-            out.append((seq[o:o + ln[g]].copy(), lm[o:o + ln[g]].copy()))
-        return out
+        ends = np.cumsum(ln).tolist()
+        starts = [0] + ends[:-1]
+        return [(seq[a:b], lm[a:b]) for a, b in zip(starts, ends)]
 
     def trace(self, g):
         n = int(self.n_nodes[g])

@@ -33,6 +33,7 @@ hipError_t launch_rollout(const Params& p, const float* wimg, int grid, hipStrea
 hipError_t launch_h0(const float* w, float* tab, int dm_lo, int dm_hi, hipStream_t s);
 hipError_t launch_reset(const Params& p, hipStream_t s);
 hipError_t launch_clear(void* const* ptr, const size_t* bytes, int n, hipStream_t s);
+hipError_t launch_pack(const int* desc, int ng, int tot, const int* act, const int* rank, int* out, hipStream_t s);
 hipError_t set_kernel_attrs();
 }  // namespace md
 
@@ -186,6 +187,7 @@ struct md_ctx {
   int pfx_min = 8;       // MD_PREFIX: grid-wide steps take >= this many actions as batched prefixes (0: off)
   bool dev_topk = true;  // MD_DEVTOPK=0: every stepRatio prediction goes to the host's numpy routine
   DevBuf<int> pfx;       // their scratch (md_env.h pfx_words)
+  DevBuf<int> pack_desc, pack_out;  // md_rollout_packed: per-graph {slot, packed offset, length}, outputs
   bool first_req = true;  // MD_FIRST_REQ=0: no speculative request at a rollout's first step
   DevBuf<unsigned long long> dfbuf;
   int df_mt = 0, df_n = 0;
@@ -213,7 +215,7 @@ struct md_ctx {
       H[l][0].release(); H[l][1].release();
     }
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
-    tr_stat.release(); glist.release(); gtoff.release(); ctl.release(); tpart.release(); lab_ok.release(); gscr_team.release(); pfx.release(); bspec.release(); prank.release(); q.release(); spart.release();
+    tr_stat.release(); glist.release(); gtoff.release(); ctl.release(); tpart.release(); lab_ok.release(); gscr_team.release(); pfx.release(); pack_desc.release(); pack_out.release(); bspec.release(); prank.release(); q.release(); spart.release();
     apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); nbc.release(); qslot.release(); qg.release(); tr_q.release(); node_w.release();
     sres.release(); qspec.release(); bars.release(); dfbuf.release();
     df_graph.clear();
@@ -1374,9 +1376,8 @@ md_status md_step(md_ctx* c, const int32_t* actions, int32_t* lmcc_out, uint8_t*
   return MD_OK;
 }
 
-md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, int32_t* seq_len, md_select_cb cb,
-                     void* user) {
-  if (!c || step < 1) return MD_EINVAL;
+// The device rollout loop of md_rollout / md_rollout_packed (launches until every graph stops).
+md_status rollout_run(md_ctx* c, int step, md_select_cb cb, void* user) {
   if (c->ng == 0) return fail(c, MD_ESTATE, "no graphs loaded");
   HIPCHK(c, hipSetDevice(c->device));
   const int host_select = step > 1 ? 1 : 0;
@@ -1463,11 +1464,45 @@ md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, i
     }
     gl.swap(next);
   }
+  return MD_OK;
+}
+
+md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, int32_t* seq_len, md_select_cb cb,
+                     void* user) {
+  if (!c || step < 1) return MD_EINVAL;
+  const md_status st = rollout_run(c, step, cb, user);
+  if (st != MD_OK) return st;
   if (seq_out) HIPCHK(c, hipMemcpyAsync(seq_out, c->tr_action.p, sizeof(int) * c->tot_n, hipMemcpyDeviceToHost, c->stream));
   if (lmcc_out) HIPCHK(c, hipMemcpyAsync(lmcc_out, c->tr_rank.p, sizeof(int) * c->tot_n, hipMemcpyDeviceToHost, c->stream));
   if (seq_out || lmcc_out) HIPCHK(c, hipStreamSynchronize(c->stream));
   if (seq_len)
     for (int g = 0; g < c->ng; ++g) seq_len[g] = c->hvar[g].steps;
+  return MD_OK;
+}
+
+md_status md_rollout_packed(md_ctx* c, int step, int32_t* seq_packed, int32_t* lmcc_packed, int32_t* seq_len,
+                            md_select_cb cb, void* user) {
+  if (!c || step < 1 || !seq_packed || !lmcc_packed || !seq_len) return MD_EINVAL;
+  const md_status st = rollout_run(c, step, cb, user);
+  if (st != MD_OK) return st;
+  std::vector<int> desc(3 * (size_t)c->ng);
+  int tot = 0;
+  for (int g = 0; g < c->ng; ++g) {
+    const int len = c->hvar[g].steps;
+    desc[3 * g] = c->hinfo[g].node_off;
+    desc[3 * g + 1] = tot;
+    desc[3 * g + 2] = len;
+    seq_len[g] = len;
+    tot += len;
+  }
+  if (tot == 0) return MD_OK;
+  if (c->pack_desc.n < desc.size()) HIPCHK(c, c->pack_desc.alloc(desc.size()));
+  if (c->pack_out.n < 2 * (size_t)tot) HIPCHK(c, c->pack_out.alloc(2 * (size_t)c->tot_n));
+  HIPCHK(c, hipMemcpyAsync(c->pack_desc.p, desc.data(), sizeof(int) * desc.size(), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, launch_pack(c->pack_desc.p, c->ng, tot, c->tr_action.p, c->tr_rank.p, c->pack_out.p, c->stream));
+  HIPCHK(c, hipMemcpyAsync(seq_packed, c->pack_out.p, sizeof(int) * tot, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(lmcc_packed, c->pack_out.p + tot, sizeof(int) * tot, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return MD_OK;
 }
 

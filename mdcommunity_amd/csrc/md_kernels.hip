@@ -5617,6 +5617,27 @@ hipError_t launch_clear(void* const* ptr, const size_t* bytes, int n, hipStream_
   return hipGetLastError();
 }
 
+// Rollout outputs packed (md_rollout_packed): graph g's removal sequence and LMCC trace, its
+// first desc[3 g + 2] node slots from desc[3 g], land at desc[3 g + 1] of the packed sequence
+// (out[0, tot)) and LMCC trace (out[tot, 2 tot)) -- a device-to-host copy of the removals
+// instead of every node slot of the batch.
+__global__ void __launch_bounds__(256) md_pack_kernel(const int* __restrict__ desc, int ng, int tot,
+                                                      const int* __restrict__ act, const int* __restrict__ rank,
+                                                      int* __restrict__ out) {
+  for (int g = blockIdx.x; g < ng; g += gridDim.x) {
+    const int src = desc[3 * g], dst = desc[3 * g + 1], len = desc[3 * g + 2];
+    for (int i = threadIdx.x; i < len; i += blockDim.x) {
+      out[dst + i] = act[src + i];
+      out[tot + dst + i] = rank[src + i];
+    }
+  }
+}
+hipError_t launch_pack(const int* desc, int ng, int tot, const int* act, const int* rank, int* out, hipStream_t s) {
+  if (ng <= 0 || tot <= 0) return hipSuccess;
+  hipLaunchKernelGGL(md_pack_kernel, dim3(std::min(ng, 1024)), dim3(256), 0, s, desc, ng, tot, act, rank, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_reset(const Params& p, hipStream_t s) {
   hipLaunchKernelGGL(md_reset_kernel, dim3(p.nglist), dim3(256), 0, s, p);
   return hipGetLastError();

@@ -205,9 +205,10 @@ def test_c5_4096_graphs_one_queue_launch(weights, graphs):
         e0, e1 = gmm.gmm_pair(N, seed=s)
         assert np.array_equal(big[s][1], e0) and np.array_equal(big[s][2], e1)
     mr, outs, launches = batch_rollout(weights, big)
-    # (+ a lock-step tail launch when graphs were parked: with 4096 graphs the last ones often
-    # end through their K2 end-game hand-shakes before any is parked)
-    assert launches in (1, 2)
+    # (+ md_queue_kernel and lock-step tail launches when graphs were parked: with 4096 graphs
+    # the last ones often end through their K2 end-game hand-shakes before any is parked; how
+    # many launches run depends on the order the workgroups reach them, as in the C3 test)
+    assert launches in (1, 2, 3)
     check_goldens(mr, outs)
     assert len(check_batch_certs(mr, outs)) >= 10  # (and the C5 seeds above 511)
     bad = []
