@@ -186,6 +186,7 @@ struct md_ctx {
   int last_served = 0;   // host selection requests served by the last API call's launches
   int pfx_min = 8;       // MD_PREFIX: grid-wide steps take >= this many actions as batched prefixes (0: off)
   bool dev_topk = true;  // MD_DEVTOPK=0: every stepRatio prediction goes to the host's numpy routine
+  bool eg_apply = true;  // MD_EG_APPLY=0: a K2 end-game answer is applied action by action
   DevBuf<int> pfx;       // their scratch (md_env.h pfx_words)
   DevBuf<int> pack_desc, pack_out;  // md_rollout_packed: per-graph {slot, packed offset, length}, outputs
   bool first_req = true;  // MD_FIRST_REQ=0: no speculative request at a rollout's first step
@@ -651,8 +652,11 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
     p.h_chk = c->h_chk.d;
     // K2 end-games in one hand-shake: single-node steps picked by numpy's own argsort routine
     // (the callback path keeps one request per step); MD_VARIANT bit 2048 turns it off
+    // (bit 2: the answer applied in one pass, env_endgame_apply; MD_EG_APPLY=0: action by action)
     p.endgame = run_mode == RUN_ROLLOUT && c->tie_argsort != nullptr && sel->step == 1 &&
-                c->cost_mode == MD_COST_UNIT && !(c->variant & 2048);
+                c->cost_mode == MD_COST_UNIT && !(c->variant & 2048)
+                    ? 1 | (c->eg_apply ? 2 : 0)
+                    : 0;
   }
   // completion record: the last workgroup copies the GraphVars and the error word to mapped
   // host memory and then writes the launch tag (kernel_exit)
@@ -831,6 +835,7 @@ md_status md_create(int device, const float* weights, size_t n_floats, int cost_
   if (const char* v = std::getenv("MD_FP_SKIP")) c->fp_skip = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_PREFIX")) c->pfx_min = std::max(0, std::atoi(v));
   if (const char* v = std::getenv("MD_DEVTOPK")) c->dev_topk = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MD_EG_APPLY")) c->eg_apply = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_FIRST_REQ")) c->first_req = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_DF")) c->df_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("MD_SPEC")) c->spec_n = std::max(0, std::min(SPEC_MAX, std::atoi(v)));

@@ -173,7 +173,8 @@ struct Params {
   unsigned* qctl;                  // queue mode: {head ticket, tail ticket, running graphs}
   unsigned long long* qslot;       // queue mode: Q_CAP item slots {ticket + 1, item}
   int* qg;                         // queue mode: per graph slot {tiles done in the stage, tiles}
-  int endgame;                     // 1: the host runs K2 end-games in one hand-shake (see md_kernels.hip)
+  int endgame;                     // bit 1: the host runs K2 end-games in one hand-shake (see md_kernels.hip);
+                                   // bit 2: the device applies the answer in one pass (env_endgame_apply)
   // speculative environment steps (single-graph rollouts, md_kernels.hip spec_loop): workgroups
   // [n_main, n_main + n_spec) precompute the next step's mutual-LMCC cascade for the likely
   // next removals while the tiles compute Q; the grid barrier counts the n_main others only

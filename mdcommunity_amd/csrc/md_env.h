@@ -1429,6 +1429,133 @@ __device__ __forceinline__ void df_early_record(KParams& p, const EnvView<GL>& E
   }
 }
 
+// env_step's pend_first when the actions were applied already (env_endgame_apply): the step
+// only recomputes the features
+constexpr int PEND_APPLIED = -2;
+
+// K2 end-game answer applied in one pass (LDS mode; p.endgame bit 2, MD_EG_APPLY=0: off).  The
+// answer's state (endgame_state: residual degree <= 1 in both layers after a fixed point) is a
+// set of pairs joined in both layers plus isolated nodes.  Covering a node of a pair kills its
+// two edges and isolates its partner; nothing is pruned and the other pairs stay components of
+// both layers, so after action j the LMCC (U/Mcc.py:30-38, over non-covered nodes) is 2 while
+// pairs remain, else 1 while a non-covered node remains, else 0; the loop stops after the
+// action that takes the last pair (env_step's terminal check).  Returns the actions applied,
+// with the trace, covered flags, killed edges (dead list) and books as env_step's loop leaves
+// them, or -1 when the state or the actions do not have that form (nothing changed: the
+// caller's loop runs).  Scratch: the parent and degree arrays (free until the fixed point /
+// the features pass).  Stages the state into LDS first unless `staged`.
+__device__ __noinline__ int env_endgame_apply(KParams&, const GraphInfo gi, int pend_n, bool staged) {
+  KParams& p = kp();
+  GraphVar& gv = *(GraphVar*)(md::lds_base() + L_GV);
+  const EnvView<false> E = env_view<false>(p, gi, (int*)(md::lds_base() + L_W));
+  if (!staged) {
+    env_stage_lds(E, gi.n);
+    __syncthreads();
+  }
+  const int n = gi.n;
+  lds_i32* mark = E.par0;  // node -> 1 + its action index (0: not picked)
+  lds_i32* act = E.par1;   // action index -> node
+  lds_i32* part = E.deg0;  // node -> layer-0 partner (-1: isolated)
+  int* w = E.tmp + A_TMP_WORDS - 32;  // {bad, first action that takes the last pair}
+  if (pend_n <= 0 || pend_n > n || gv.dmax[0] > 1 || gv.dmax[1] > 1 || gv.alive[0] != gv.alive[1] || gv.alive[0] <= 0 ||
+      !gv.s0_done)
+    return -1;
+  for (int x = threadIdx.x; x < n; x += NTHREADS) {
+    mark[x] = 0;
+    part[x] = -1;
+  }
+  if (threadIdx.x == 0) {
+    w[0] = 0;
+    w[1] = pend_n;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < pend_n; i += NTHREADS) {
+    const int a = __hip_atomic_load(p.pend + gi.node_off + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    act[i] = a;
+    if (a < 0 || a >= n || E.covered(a)) w[0] = 1;
+    else mark[a] = i + 1;
+  }
+  const int na = E.hdr[0];
+  const lds_u16* al = E.hdr[2] ? E.al_other : E.al;
+  for (int i = threadIdx.x; i < na; i += NTHREADS) {
+    const int e = al[i];
+    if (e < E.e0 && E.st[e] == E_ALIVE) {
+      const int u = E.u16[e], v = E.v16[e];
+      part[u] = v;
+      part[v] = u;
+    }
+  }
+  __syncthreads();
+  // (duplicates: one index per node survives; layer 1 must join the same pairs)
+  for (int i = threadIdx.x; i < pend_n; i += NTHREADS) {
+    const int a = act[i];
+    if (a >= 0 && a < n && mark[a] != i + 1) w[0] = 1;
+  }
+  for (int i = threadIdx.x; i < na; i += NTHREADS) {
+    const int e = al[i];
+    if (e >= E.e0 && E.st[e] == E_ALIVE) {
+      const int u = E.u16[e], v = E.v16[e];
+      if (part[u] != v || part[v] != u) w[0] = 1;
+    }
+  }
+  __syncthreads();
+  if (w[0]) return -1;
+  // action i takes a pair when its partner is not picked before it; pairs left after it
+  const int P = gv.alive[0];
+  const int chunk = (pend_n + NTHREADS - 1) / NTHREADS;
+  const int i0 = min(pend_n, (int)threadIdx.x * chunk), i1 = min(pend_n, i0 + chunk);
+  int hits = 0;
+  for (int i = i0; i < i1; ++i) {
+    const int b = part[act[i]];
+    hits += b >= 0 && (mark[b] == 0 || mark[b] > i + 1);
+  }
+  int tot = 0;
+  int h = block_excl_scan(hits, E.tmp, &tot);
+  const int ncov0 = gv.n_cov, steps0 = gv.steps;
+  for (int i = i0; i < i1; ++i) {
+    const int b = part[act[i]];
+    h += b >= 0 && (mark[b] == 0 || mark[b] > i + 1);
+    if (h == P) atomicMin(w + 1, i + 1);
+    E.deg1[i] = P - h;  // pairs left after action i
+  }
+  __syncthreads();
+  const int m = w[1];
+  for (int i = threadIdx.x; i < m; i += NTHREADS) {
+    const int a = act[i];
+    stc(E.gcov + a, (uint8_t)1);
+    E.cov8[a] = 1;
+    const int lm = E.deg1[i] > 0 ? 2 : (n - ncov0 - (i + 1) > 0 ? 1 : 0);
+    if (MD_BOK(steps0 + i < n, 8)) {
+      p.tr_action[gi.node_off + steps0 + i] = a;
+      p.tr_rank[gi.node_off + steps0 + i] = lm;
+    }
+  }
+  int k0 = 0, k1 = 0;
+  for (int i = threadIdx.x; i < na; i += NTHREADS) {
+    const int e = al[i];
+    if (E.st[e] != E_ALIVE) continue;
+    const int mu = mark[E.u16[e]], mv = mark[E.v16[e]];
+    if ((mu > 0 && mu <= m) || (mv > 0 && mv <= m)) {
+      E.st[e] = E_COVERED;
+      if (e < E.e0) k0++; else k1++;
+    }
+  }
+  const int2 kk = block_sum2(k0, k1, E.tmp);
+  __syncthreads();
+  compact_alive(E);
+  if (threadIdx.x == 0) {
+    gv.counter[0] += kk.x;
+    gv.counter[1] += kk.y;
+    gv.alive[0] -= kk.x;
+    gv.alive[1] -= kk.y;
+    gv.n_cov += m;
+    gv.lmcc = E.deg1[m - 1] > 0 ? 2 : (n - ncov0 - m > 0 ? 1 : 0);
+    gv.steps += m;
+  }
+  __syncthreads();
+  return m;
+}
+
 template <bool GL>
 __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, float*, int pend_n,
                         int pend_first, const float*, bool staged) {
@@ -1563,7 +1690,7 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
     if (ps < p.prof_cap) acc = p.prof + (size_t)ps * PROF_SLOTS + 16;
   }
   int err = 0;
-  for (int k = 0; k < pend_n; ++k) {
+  for (int k = pend_first == PEND_APPLIED ? pend_n : 0; k < pend_n; ++k) {
     if (gv.alive[0] == 0 || gv.alive[1] == 0) break;  // terminal between queued actions
     const int a = k == 0 && pend_first >= 0
                       ? pend_first

@@ -620,18 +620,24 @@ __device__ __noinline__ void host_request(KParams&, const GraphInfo gi, int g, i
 __device__ __forceinline__ unsigned host_tag_eg(KParams& p, int npred, bool endgame) {
   return host_tag(p, npred) ^ (endgame ? 0x8000u : 0u);
 }
-// Thread 0 only: the host's answer to request `npred` of graph g, copied to p.pend.
-// Returns the number of actions, 0 when not answered yet, -1 on a bad answer.
+// Thread 0 only: whether the host answered request `npred` of graph g.  Returns the number of
+// actions, 0 when not answered yet, -1 on a bad answer; host_copy_actions then moves them.
 __device__ __forceinline__ int host_answer(KParams& p, const GraphInfo& gi, int g, int npred, bool endgame = false) {
   if (__hip_atomic_load(p.h_ans + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != host_tag_eg(p, npred, endgame))
     return 0;
   const int k = __hip_atomic_load(p.h_nact + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (k <= 0 || k > gi.n) return -1;
-  for (int i = 0; i < k; ++i)
+  return k <= 0 || k > gi.n ? -1 : k;
+}
+// Whole workgroup, after the answer's count was seen: the k actions from mapped host memory to
+// p.pend, one load per thread (each is a bus round trip: a stepRatio or end-game answer no longer
+// waits k of them back to back).  Ends with the workgroup's stores drained.
+__device__ __forceinline__ void host_copy_actions(KParams& p, const GraphInfo& gi, int k) {
+  for (int i = threadIdx.x; i < k; i += NTHREADS)
     __hip_atomic_store(p.pend + gi.node_off + i,
                        __hip_atomic_load(p.h_act + gi.node_off + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return k;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 }
 // K2 end-game (unit cost): when every live node has residual degree 1 in both layers, the
 // graph is a set of disjoint pairs joined in both layers, every live node's Q is the same
@@ -812,7 +818,19 @@ __device__ __noinline__ int host_handshake(KParams&, const GraphInfo gi, int g, 
     misc[3] = k;
   }
   __syncthreads();
-  return max(misc[3], 0);
+  const int k = misc[3];
+  if (k > 0) host_copy_actions(p, gi, k);
+  return max(k, 0);
+}
+
+// K2 end-game answer of k actions (LDS mode): applied in one pass when the state has the
+// end-game form (env_endgame_apply; env_step then gets PEND_APPLIED and only recomputes the
+// features).  Stages the state first when it is not (staged: in LDS afterwards either way).
+__device__ __forceinline__ bool eg_apply(KParams& p, const GraphInfo& gi, int k, bool& staged) {
+  if (!(p.endgame & 2) || k < 2) return false;
+  const bool ok = env_endgame_apply(p, gi, k, staged) >= 0;
+  staged = true;
+  return ok;
 }
 
 // Phase A of one graph: reduce the previous prediction, then apply / MCC / features.
@@ -834,6 +852,7 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
   }
   __syncthreads();
   int pend_n = 0, pend_first = -1;
+  bool eg_ans = false;  // the actions answer an end-game request
   bool stop = false;
   if (gv.status == ST_WAIT_HOST) {
     // asynchronous hand-shake (several graphs per launch): the graph sat out the steps since
@@ -847,6 +866,8 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
     __syncthreads();
     if (misc[3] <= 0) return staged;
     pend_n = misc[3];
+    eg_ans = gv.ntie < 0;
+    host_copy_actions(p, gi, pend_n);
   } else if (gv.status != ST_RUN) {
     return staged;
   } else if (have_q) {
@@ -977,8 +998,9 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
       return staged;
     }
     float* area = lds + L_W;
-    const bool was_staged = staged && fits;
+    bool was_staged = staged && fits;
     staged = fits;
+    if (eg_ans && fits && eg_apply(p, gi, pend_n, was_staged)) pend_first = PEND_APPLIED;
     int err = fits ? env_step<false>(p, gi, gv, area, pend_n, pend_first, lds, was_staged)
                    : env_step<true>(p, gi, gv, area, pend_n, pend_first, lds, false);
     // the prebuild confirmation: the state after this phase A is exactly the speculative
@@ -1008,7 +1030,7 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
         const int k = host_handshake(p, gi, g, gv.npred, 0.f, gv.n_live, misc, true);
         cw = 0ull;
         if (k > 0) {
-          err = fits ? env_step<false>(p, gi, gv, area, k, -1, lds, true)
+          err = fits ? env_step<false>(p, gi, gv, area, k, eg_apply(p, gi, k, staged) ? PEND_APPLIED : -1, lds, true)
                      : env_step<true>(p, gi, gv, area, k, -1, lds, false);
           if (threadIdx.x == 0) {
             if (err) raise_err(p, err);

@@ -381,6 +381,44 @@ def test_k2_endgame_in_one_handshake_matches_per_step(monkeypatch):
     assert fast[1][0] < slow[1][0]
 
 
+def test_k2_endgame_one_pass_apply_same_state(monkeypatch):
+    """The K2 end-game answer applied in one pass (md_env.h env_endgame_apply) against action by
+    action (MD_EG_APPLY=0): identical sequences, LMCC traces and final states (covered set,
+    removed edges per layer, counters), single graphs (the synchronous hand-shake) and a batch
+    (the asynchronous one); the LMCC trace also against the oracle environment stepped along
+    the sequence (U/mvc_env.py:74-87, U/Mcc.py:30-38)."""
+    from oracle import refenv
+    from edge_graphs import cases
+    names = ["gmm1000_s0", "gmm1000_s1", "gmm1000_s2", "er1000", "gmm200_s7", "er100"]
+    graphs = [(int(z["n_nodes"]), z["edges0"], z["edges1"]) for z in map(load_golden, names)]
+    graphs += [(n, e0, e1) for _, n, e0, e1 in cases()]
+
+    def run(apply):
+        monkeypatch.setenv("MD_EG_APPLY", str(apply))
+        e = _lib.Engine(engine.load_weights(engine.DEFAULT_UNIT))
+        try:
+            out = []
+            for g in graphs:
+                e.load_graphs([g])
+                e.reset()
+                (s, r), = e.rollout()
+                cov, r0, r1, cnt = e.get_state(0)
+                out.append((s.tolist(), r.tolist(), cov.tobytes(), r0.tobytes(), r1.tobytes(), cnt.tolist()))
+            e.load_graphs(graphs * 2)
+            e.reset()
+            out.append([(s.tolist(), r.tolist()) for s, r in e.rollout()])
+            return out
+        finally:
+            e.close()
+
+    one, each = run(1), run(0)
+    assert one == each
+    for (n, e0, e1), got in zip(graphs, one):
+        env = refenv.RefEnv(refenv.RefGraph(n, e0, e1), "unit")
+        assert [env.step(int(a)) for a in got[0]] == got[1]
+        assert env.terminal()
+
+
 @pytest.mark.parametrize("name", ["gmm1000_s0", "gmm1000_s2", "er1000", "er300_dense"])
 def test_speculative_steps_match_plain(monkeypatch, name):
     """Speculative environment workgroups (MD_SPEC, single-graph rollouts) change nothing:
