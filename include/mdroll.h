@@ -133,8 +133,8 @@ md_status md_rollout(md_ctx* ctx, int step, int32_t* seq_out, int32_t* lmcc_out,
 
 /* md_rollout with the outputs packed: graph g's removal order and LMCC trace at offsets
  * sum_{h<g} seq_len[h] of seq_packed / lmcc_packed (capacity sum(n_nodes) each; only the
- * removals are written and copied -- one device-to-host copy of the removals instead of every
- * node slot of a large batch).  seq_len is required. */
+ * removals are read: each graph's trace reaches mapped host memory as the graph ends, so no
+ * copy follows the launch).  seq_len is required. */
 md_status md_rollout_packed(md_ctx* ctx, int step, int32_t* seq_packed, int32_t* lmcc_packed, int32_t* seq_len,
                             md_select_cb cb, void* user);
 

@@ -33,7 +33,6 @@ hipError_t launch_rollout(const Params& p, const float* wimg, int grid, hipStrea
 hipError_t launch_h0(const float* w, float* tab, int dm_lo, int dm_hi, hipStream_t s);
 hipError_t launch_reset(const Params& p, hipStream_t s);
 hipError_t launch_clear(void* const* ptr, const size_t* bytes, int n, hipStream_t s);
-hipError_t launch_pack(const int* desc, int ng, int tot, const int* act, const int* rank, int* out, hipStream_t s);
 hipError_t set_kernel_attrs();
 }  // namespace md
 
@@ -188,7 +187,7 @@ struct md_ctx {
   bool dev_topk = true;  // MD_DEVTOPK=0: every stepRatio prediction goes to the host's numpy routine
   bool eg_apply = true;  // MD_EG_APPLY=0: a K2 end-game answer is applied action by action
   DevBuf<int> pfx;       // their scratch (md_env.h pfx_words)
-  DevBuf<int> pack_desc, pack_out;  // md_rollout_packed: per-graph {slot, packed offset, length}, outputs
+  HostBuf<int> h_tr;         // mapped host mirrors of tr_action [tot_n] and tr_rank [tot_n] (trace_publish)
   bool first_req = true;  // MD_FIRST_REQ=0: no speculative request at a rollout's first step
   DevBuf<unsigned long long> dfbuf;
   int df_mt = 0, df_n = 0;
@@ -216,12 +215,12 @@ struct md_ctx {
       H[l][0].release(); H[l][1].release();
     }
     covered.release(); live.release(); gscr.release(); pend.release(); tr_action.release(); tr_rank.release();
-    tr_stat.release(); glist.release(); gtoff.release(); ctl.release(); tpart.release(); lab_ok.release(); gscr_team.release(); pfx.release(); pack_desc.release(); pack_out.release(); bspec.release(); prank.release(); q.release(); spart.release();
+    tr_stat.release(); glist.release(); gtoff.release(); ctl.release(); tpart.release(); lab_ok.release(); gscr_team.release(); pfx.release(); bspec.release(); prank.release(); q.release(); spart.release();
     apart.release(); ybuf.release(); hbuf.release(); xbuf.release(); nbc.release(); qslot.release(); qg.release(); tr_q.release(); node_w.release();
     sres.release(); qspec.release(); bars.release(); dfbuf.release();
     df_graph.clear();
     h_req.release(); h_ans.release(); h_nact.release(); h_act.release(); h_q.release(); h_chk.release();
-    h_done.release(); h_gvar.release();
+    h_done.release(); h_gvar.release(); h_tr.release();
     ng = 0;
     hinfo.clear();
     hvar.clear();
@@ -297,6 +296,8 @@ Params make_params(md_ctx* c) {
   p.pend = c->pend.p;
   p.tr_action = c->tr_action.p;
   p.tr_rank = c->tr_rank.p;
+  p.h_tra = c->h_tr.d;
+  p.h_trr = c->h_tr.d != nullptr ? c->h_tr.d + c->tot_n : nullptr;
   p.tr_stat = c->tr_stat.p;
   p.tr_q = c->tr_q.p;
   p.node_w = c->cost_mode == MD_COST_DEGREE ? c->node_w.p : nullptr;
@@ -513,6 +514,7 @@ bool queue_mode_ok(const md_ctx* c, int run_mode) {
 }
 
 md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int host_select, Selector* sel) {
+  const auto t_fn = std::chrono::steady_clock::now();
   std::vector<int> v(gl_in, gl_in + ngl);
   // graphs with more edges first: the queue's first round-robin positions go to the longest
   // rollouts (the rollout length grows with the edge count), so the launch does not end on a
@@ -683,6 +685,7 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
     std::vector<int32_t> acts;
     auto last = std::chrono::steady_clock::now();
     const auto t_launch = last;
+    auto t_tag = last;
     static const bool host_stats = std::getenv("MD_HOST_STATS") != nullptr;  // diagnostics
     double serve_s = 0.0;
     int n_served = 0;
@@ -705,7 +708,10 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
         }
       }
       if (done) break;
-      if (rec && !tagged && __atomic_load_n(c->h_done.h, __ATOMIC_ACQUIRE) == p.launch_seq) tagged = true;
+      if (rec && !tagged && __atomic_load_n(c->h_done.h, __ATOMIC_ACQUIRE) == p.launch_seq) {
+        tagged = true;
+        if (host_stats) t_tag = std::chrono::steady_clock::now();
+      }
       const auto now = std::chrono::steady_clock::now();
       if (tagged || (!served && now - last >= std::chrono::microseconds(20))) {
         last = now;
@@ -723,8 +729,10 @@ md_status launch_chunk(md_ctx* c, const int* gl_in, int ngl, int run_mode, int h
       }
     }
     if (hs && host_stats)
-      std::fprintf(stderr, "md host: %d requests served in %.3f ms of a %.3f ms launch wait\n", n_served, 1e3 * serve_s,
-                   1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t_launch).count());
+      std::fprintf(stderr, "md host: prelude %.3f ms; %d requests served in %.3f ms of a %.3f ms launch wait (tag seen at %.3f ms)\n",
+                   1e3 * std::chrono::duration<double>(t_launch - t_fn).count(), n_served, 1e3 * serve_s,
+                   1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t_launch).count(),
+                   1e3 * std::chrono::duration<double>(t_tag - t_launch).count());
   }
   if (trace_on()) std::fprintf(stderr, "md trace: ctx %p launch %u done\n", (void*)c, p.launch_seq);
   int dev_err = 0;
@@ -1089,6 +1097,7 @@ md_status md_load_graphs(md_ctx* c, int n_graphs, const int32_t* n_nodes, const 
   HIPCHK(c, c->pend.alloc(tn));
   HIPCHK(c, c->tr_action.alloc(tn));
   HIPCHK(c, c->tr_rank.alloc(tn));
+  HIPCHK(c, c->h_tr.alloc(2 * tn));
   HIPCHK(c, c->tr_stat.alloc(4 * tn));
   HIPCHK(c, c->tr_q.alloc(2 * tn));
   // (+4: env_stage_wide stages the last graph's Q row as 16-byte unclipped buffer loads)
@@ -1477,9 +1486,9 @@ md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, i
   if (!c || step < 1) return MD_EINVAL;
   const md_status st = rollout_run(c, step, cb, user);
   if (st != MD_OK) return st;
-  if (seq_out) HIPCHK(c, hipMemcpyAsync(seq_out, c->tr_action.p, sizeof(int) * c->tot_n, hipMemcpyDeviceToHost, c->stream));
-  if (lmcc_out) HIPCHK(c, hipMemcpyAsync(lmcc_out, c->tr_rank.p, sizeof(int) * c->tot_n, hipMemcpyDeviceToHost, c->stream));
-  if (seq_out || lmcc_out) HIPCHK(c, hipStreamSynchronize(c->stream));
+  // (every graph is terminal: its trace went to the host mirrors as it ended, trace_publish)
+  if (seq_out) std::memcpy(seq_out, c->h_tr.h, sizeof(int) * c->tot_n);
+  if (lmcc_out) std::memcpy(lmcc_out, c->h_tr.h + c->tot_n, sizeof(int) * c->tot_n);
   if (seq_len)
     for (int g = 0; g < c->ng; ++g) seq_len[g] = c->hvar[g].steps;
   return MD_OK;
@@ -1488,26 +1497,30 @@ md_status md_rollout(md_ctx* c, int step, int32_t* seq_out, int32_t* lmcc_out, i
 md_status md_rollout_packed(md_ctx* c, int step, int32_t* seq_packed, int32_t* lmcc_packed, int32_t* seq_len,
                             md_select_cb cb, void* user) {
   if (!c || step < 1 || !seq_packed || !lmcc_packed || !seq_len) return MD_EINVAL;
+  static const bool host_stats = std::getenv("MD_HOST_STATS") != nullptr;  // diagnostics
+  const auto t0 = std::chrono::steady_clock::now();
   const md_status st = rollout_run(c, step, cb, user);
   if (st != MD_OK) return st;
-  std::vector<int> desc(3 * (size_t)c->ng);
+  struct PackStats {
+    std::chrono::steady_clock::time_point t0, t1;
+    bool on;
+    ~PackStats() {
+      if (on)
+        std::fprintf(stderr, "md host: rollout %.3f ms, outputs %.3f ms\n",
+                     1e3 * std::chrono::duration<double>(t1 - t0).count(),
+                     1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count());
+    }
+  } ps{t0, std::chrono::steady_clock::now(), host_stats};
+  // (every graph is terminal: its trace went to the host mirrors as it ended, trace_publish;
+  // only the removals are read, from host memory)
   int tot = 0;
   for (int g = 0; g < c->ng; ++g) {
-    const int len = c->hvar[g].steps;
-    desc[3 * g] = c->hinfo[g].node_off;
-    desc[3 * g + 1] = tot;
-    desc[3 * g + 2] = len;
+    const int len = c->hvar[g].steps, off = (int)c->hinfo[g].node_off;
+    std::memcpy(seq_packed + tot, c->h_tr.h + off, sizeof(int) * len);
+    std::memcpy(lmcc_packed + tot, c->h_tr.h + c->tot_n + off, sizeof(int) * len);
     seq_len[g] = len;
     tot += len;
   }
-  if (tot == 0) return MD_OK;
-  if (c->pack_desc.n < desc.size()) HIPCHK(c, c->pack_desc.alloc(desc.size()));
-  if (c->pack_out.n < 2 * (size_t)tot) HIPCHK(c, c->pack_out.alloc(2 * (size_t)c->tot_n));
-  HIPCHK(c, hipMemcpyAsync(c->pack_desc.p, desc.data(), sizeof(int) * desc.size(), hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, launch_pack(c->pack_desc.p, c->ng, tot, c->tr_action.p, c->tr_rank.p, c->pack_out.p, c->stream));
-  HIPCHK(c, hipMemcpyAsync(seq_packed, c->pack_out.p, sizeof(int) * tot, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(lmcc_packed, c->pack_out.p + tot, sizeof(int) * tot, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
   return MD_OK;
 }
 

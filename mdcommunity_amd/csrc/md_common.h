@@ -145,6 +145,8 @@ struct Params {
   unsigned* exit_ctr;              // device: workgroups that finished this launch (cleared per launch)
   unsigned* h_done;                // mapped host: {launch tag, error word}
   int* h_gvar;                     // mapped host: GraphVar copies [n_graphs]
+  int* h_tra;                      // mapped host: mirrors of tr_action / tr_rank, a graph's range
+  int* h_trr;                      //   written once it is final (trace_publish)
   unsigned* h_req;                 // per graph: request tag (device writes)
   unsigned* h_ans;                 // per graph: answer tag (host writes)
   int* h_nact;                     // per graph: actions answered (-1: abort)

@@ -1526,8 +1526,8 @@ __device__ __noinline__ int env_endgame_apply(KParams&, const GraphInfo gi, int 
     E.cov8[a] = 1;
     const int lm = E.deg1[i] > 0 ? 2 : (n - ncov0 - (i + 1) > 0 ? 1 : 0);
     if (MD_BOK(steps0 + i < n, 8)) {
-      p.tr_action[gi.node_off + steps0 + i] = a;
-      p.tr_rank[gi.node_off + steps0 + i] = lm;
+      stc(p.tr_action + gi.node_off + steps0 + i, a);
+      stc(p.tr_rank + gi.node_off + steps0 + i, lm);
     }
   }
   int k0 = 0, k1 = 0;
@@ -1733,8 +1733,8 @@ __device__ __noinline__ int env_step(KParams&, const GraphInfo gi, GraphVar&, fl
       gv.n_cov += 1;
       gv.lmcc = lm;
       if (MD_BOK(gv.steps < gi.n, 8)) {
-        p.tr_action[gi.node_off + gv.steps] = a;
-        p.tr_rank[gi.node_off + gv.steps] = lm;
+        stc(p.tr_action + gi.node_off + gv.steps, a);
+        stc(p.tr_rank + gi.node_off + gv.steps, lm);
       }
       gv.steps += 1;
     }
@@ -2666,8 +2666,8 @@ __device__ __noinline__ int team_prefix_step(KParams& p, Team& T, const EnvView<
       const int a = pfx_act(p, gi, k0 + q, pend_first);
       stc(E.gcov + a, (uint8_t)1);
       if (MD_BOK(st0 + q < gi.n, 8)) {
-        p.tr_action[gi.node_off + st0 + q] = a;
-        p.tr_rank[gi.node_off + st0 + q] = ldc(rec + 4 * q);
+        stc(p.tr_action + gi.node_off + st0 + q, a);
+        stc(p.tr_rank + gi.node_off + st0 + q, ldc(rec + 4 * q));
       }
     }
     __syncthreads();
@@ -2777,8 +2777,8 @@ __device__ bool team_env_step(KParams& p, Team& T, int g, int pend_n, int pend_f
       gv.n_cov += 1;
       gv.lmcc = lm;
       if (MD_BOK(gv.steps < gi.n, 8)) {
-        p.tr_action[gi.node_off + gv.steps] = a;
-        p.tr_rank[gi.node_off + gv.steps] = lm;
+        stc(p.tr_action + gi.node_off + gv.steps, a);
+        stc(p.tr_rank + gi.node_off + gv.steps, lm);
       }
       gv.steps += 1;
     }

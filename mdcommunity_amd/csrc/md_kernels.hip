@@ -833,6 +833,22 @@ __device__ __forceinline__ bool eg_apply(KParams& p, const GraphInfo& gi, int k,
   return ok;
 }
 
+// A graph that just became terminal: its removal trace [0, steps) to the mapped host mirrors
+// (p.h_tra / p.h_trr), so md_rollout reads it without a copy after the launch.  Whole
+// workgroup; the trace slots may have been written by other threads (or, in the grid-wide
+// step, other workgroups before the step's last barrier).
+__device__ __forceinline__ void trace_publish(KParams& p, const GraphInfo& gi, int steps) {
+  if (p.h_tra == nullptr) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int i = threadIdx.x; i < min(steps, gi.n); i += NTHREADS) {
+    __hip_atomic_store(p.h_tra + gi.node_off + i, ldc(p.tr_action + gi.node_off + i), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(p.h_trr + gi.node_off + i, ldc(p.tr_rank + gi.node_off + i), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // Phase A of one graph: reduce the previous prediction, then apply / MCC / features.
 // team_out (grid-wide environment step): when the step would run in global mode, phase A stops
 // once the actions are known: {pend_n, pend_first, 1} in team_out, the GraphVar left in LDS for
@@ -1041,6 +1057,7 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
     }
   }
   __syncthreads();
+  if (gv.status == ST_TERMINAL) trace_publish(p, gi, gv.steps);  // (phase A never starts on a terminal graph)
   gv_store(p, g, &gv);
   if (p.pre_cw != nullptr && threadIdx.x == 0)  // every phase A: a stale confirmation must not match
     __hip_atomic_store((g_u64*)p.pre_cw, cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -5139,6 +5156,7 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
             else gv.status = ST_RUN;
           }
           __syncthreads();
+          if (gv.status == ST_TERMINAL) trace_publish(p, p.ginfo[p.glist[0]], gv.steps);
           gv_store(p, p.glist[0], &gv);
           __syncthreads();
         }
@@ -5636,27 +5654,6 @@ hipError_t launch_clear(void* const* ptr, const size_t* bytes, int n, hipStream_
   if (cl.n == 0) return hipSuccess;
   const int blocks = (int)std::min<size_t>(1024, (tot / 4 + 255) / 256);
   hipLaunchKernelGGL(md_clear_kernel, dim3(std::max(1, blocks)), dim3(256), 0, s, cl);
-  return hipGetLastError();
-}
-
-// Rollout outputs packed (md_rollout_packed): graph g's removal sequence and LMCC trace, its
-// first desc[3 g + 2] node slots from desc[3 g], land at desc[3 g + 1] of the packed sequence
-// (out[0, tot)) and LMCC trace (out[tot, 2 tot)) -- a device-to-host copy of the removals
-// instead of every node slot of the batch.
-__global__ void __launch_bounds__(256) md_pack_kernel(const int* __restrict__ desc, int ng, int tot,
-                                                      const int* __restrict__ act, const int* __restrict__ rank,
-                                                      int* __restrict__ out) {
-  for (int g = blockIdx.x; g < ng; g += gridDim.x) {
-    const int src = desc[3 * g], dst = desc[3 * g + 1], len = desc[3 * g + 2];
-    for (int i = threadIdx.x; i < len; i += blockDim.x) {
-      out[dst + i] = act[src + i];
-      out[tot + dst + i] = rank[src + i];
-    }
-  }
-}
-hipError_t launch_pack(const int* desc, int ng, int tot, const int* act, const int* rank, int* out, hipStream_t s) {
-  if (ng <= 0 || tot <= 0) return hipSuccess;
-  hipLaunchKernelGGL(md_pack_kernel, dim3(std::min(ng, 1024)), dim3(256), 0, s, desc, ng, tot, act, rank, out);
   return hipGetLastError();
 }
 
