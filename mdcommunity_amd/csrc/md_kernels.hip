@@ -833,10 +833,14 @@ __device__ __forceinline__ bool eg_apply(KParams& p, const GraphInfo& gi, int k,
   return ok;
 }
 
-// A graph that just became terminal: its removal trace [0, steps) to the mapped host mirrors
-// (p.h_tra / p.h_trr), so md_rollout reads it without a copy after the launch.  Whole
-// workgroup; the trace slots may have been written by other threads (or, in the grid-wide
-// step, other workgroups before the step's last barrier).
+// A graph's final removal trace [0, steps) to the mapped host mirrors (p.h_tra / p.h_trr), so
+// md_rollout reads it without a copy after the launch.  Launches of at most PUB_EXIT_MAX graphs
+// publish in kernel_exit, once every workgroup is done (a system-scope store during the
+// single-graph rollout showed as ~0.25 MB of extra WRITE_SIZE each, no time); queue launches
+// publish each graph as it becomes terminal (the workgroup that ended it).  Whole workgroup;
+// the trace slots may have been written by other threads or workgroups (agent-coherent
+// stores).
+constexpr int PUB_EXIT_MAX = 16;
 __device__ __forceinline__ void trace_publish(KParams& p, const GraphInfo& gi, int steps) {
   if (p.h_tra == nullptr) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1057,7 +1061,8 @@ __device__ __forceinline__ bool phase_a(KParams&, int g, bool have_q, float* lds
     }
   }
   __syncthreads();
-  if (gv.status == ST_TERMINAL) trace_publish(p, gi, gv.steps);  // (phase A never starts on a terminal graph)
+  // (phase A never starts on a terminal graph)
+  if (gv.status == ST_TERMINAL && p.nglist > PUB_EXIT_MAX) trace_publish(p, gi, gv.steps);
   gv_store(p, g, &gv);
   if (p.pre_cw != nullptr && threadIdx.x == 0)  // every phase A: a stale confirmation must not match
     __hip_atomic_store((g_u64*)p.pre_cw, cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -5156,7 +5161,6 @@ __device__ __forceinline__ void engine_body(KParams& p, const float* __restrict_
             else gv.status = ST_RUN;
           }
           __syncthreads();
-          if (gv.status == ST_TERMINAL) trace_publish(p, p.ginfo[p.glist[0]], gv.steps);
           gv_store(p, p.glist[0], &gv);
           __syncthreads();
         }
@@ -5460,6 +5464,14 @@ __device__ __noinline__ void kernel_exit(KParams&) {
     const int g = p.glist[i / GV_WORDS], k = i % GV_WORDS;
     __hip_atomic_store(p.h_gvar + (size_t)g * GV_WORDS + k, ldc((const int*)(p.gvar + g) + k), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (p.nglist <= PUB_EXIT_MAX) {
+    // the terminal graphs' traces (trace_publish: small launches publish here)
+    for (int i = 0; i < p.nglist; ++i) {
+      const int g = p.glist[i];
+      const GraphVar* v = p.gvar + g;
+      if (ldc(&v->status) == ST_TERMINAL) trace_publish(p, p.ginfo[g], ldc(&v->steps));
+    }
   }
   if (threadIdx.x == 0)
     __hip_atomic_store(p.h_done + 1, (unsigned)__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
