@@ -31,3 +31,9 @@ print(f"{name} MD_FP_SHORTCUT={os.environ.get('MD_FP_SHORTCUT', '1')}: kernel {m
       f"{P[:, 16].sum()} rounds; us total: init {tot(56):.0f} unite {tot(17):.0f} label {tot(18):.0f} prune+check {tot(19):.0f} "
       f"count {tot(20):.0f} cover {tot(22):.0f}; per fixed point {(tot(56) + tot(17) + tot(18) + tot(19) + tot(20)) / len(P):.1f} us",
       flush=True)
+# per fixed point (first 12 and the slowest 5): rounds and the round accounting in us
+rows = lambda idx: "\n".join(f"  fp {i:3d}: rounds {P[i, 16]:2d}  init {P[i, 56] / 100:.1f}  unite {P[i, 17] / 100:.1f}  label {P[i, 18] / 100:.1f}  "
+                             f"prune+check {P[i, 19] / 100:.1f}  count {P[i, 20] / 100:.1f}" for i in idx)
+print(rows(range(min(12, len(P)))), flush=True)
+cost = P[:, 56] + P[:, 17] + P[:, 18] + P[:, 19] + P[:, 20]
+print("  slowest:\n" + rows(np.argsort(-cost)[:5]), flush=True)
