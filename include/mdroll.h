@@ -297,6 +297,11 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *                     (stepRatio > 0) as independent prefix fixed points, one per workgroup,
  *                     while at least k remain (default 8; 0: one cascade after another;
  *                     test_gpu_prefix.py, and the certified N = 18 000 stepRatio sequence)
+ *   MD_DEVTOPK        0: every stepRatio prediction of the grid-wide step goes to the host's
+ *                     numpy routine (default 1: the device takes the k largest Q when they are
+ *                     tie-free; test_device_topk_same_rollouts)
+ *   MD_EG_APPLY       0: a K2 end-game answer is applied action by action (default 1: in one
+ *                     pass, env_endgame_apply; test_k2_endgame_one_pass_apply_same_state)
  *   MD_FIRST_REQ      0: no speculative request at a rollout's first environment step (default
  *                     1: candidates ranked by residual degree, as no prediction exists yet;
  *                     test_first_request_same_rollouts)
@@ -305,7 +310,8 @@ md_status md_gmm_links(int device, int n_layers, int n, const double* kappa, con
  *                     scripts/wq_timeline.py)
  *   MD_VARIANT bit 8  per-piece queue-mode profile stamps (md_profile; qprof build)
  *   MD_POLL_US        host-thread polling interval of the hand-shake (µs)
- *   MD_HOST_STATS     set: print hand-shake timing statistics to stderr
+ *   MD_HOST_STATS     set: print hand-shake and host-side timing (launch prelude, wait,
+ *                     outputs) to stderr
  *   MD_PROF_ALL       md_profile_read returns every non-empty record row (the dataflow mode's
  *                     per-tile rows after the step records), not only the step records
  *   MD_TRACE          1: every device allocation and kernel launch to stderr (maps a GPU
