@@ -219,3 +219,30 @@ def test_c5_4096_graphs_one_queue_launch(weights, graphs):
             if int(m) != int(mr[lo + i]) or seq.tolist() != o[0].tolist() or ranks.tolist() != o[1].tolist():
                 bad.append(lo + i)
     assert not bad, f"{len(bad)} graphs differ between the 4096-graph launch and 512-graph launches: {bad[:10]}"
+
+
+@pytest.mark.timeout(240)
+def test_c3_endgame_one_pass_apply_same_states(monkeypatch, graphs, weights):
+    """The K2 end-game answers of a wave-item launch (asynchronous hand-shakes; the graph's state
+    is staged into the workgroup's LDS for the one-pass apply, md_kernels.hip eg_apply) against
+    the per-action loop (MD_EG_APPLY=0): the same rollouts and the same final states (covered
+    set, removed edges per layer, counters) for all 256 graphs."""
+    def run(apply):
+        monkeypatch.setenv("MD_EG_APPLY", apply)
+        eng = _lib.Engine(weights)
+        try:
+            eng.load_graphs(graphs[:256])
+            mr = eng.reset().copy()
+            outs = [(s.tolist(), r.tolist()) for s, r in eng.rollout()]
+            states = []
+            for g in range(256):
+                cov, r0, r1, cnt = eng.get_state(g)
+                states.append((cov.tobytes(), r0.tobytes(), r1.tobytes(), cnt.tolist()))
+            return mr.tolist(), outs, states
+        finally:
+            eng.close()
+
+    one, each = run("1"), run("0")
+    assert one[0] == each[0]
+    bad = [g for g in range(256) if one[1][g] != each[1][g] or one[2][g] != each[2][g]]
+    assert not bad, f"{len(bad)} graphs differ, seeds {bad[:10]}"
